@@ -1,0 +1,68 @@
+"""The C-ABI library: loads, exports every symbol include/vstyler.h declares, validates arguments
+before launching (no GPU needed: invalid calls return VS_E_INVALID/VS_E_UNSUPPORTED up front)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "vstyler.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const char\*|int)\s+(vs_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_abi():
+    syms = header_symbols()
+    assert "vs_gemm" in syms and "vs_attn_fwd" in syms and len(syms) >= 13
+
+
+def test_library_exports_every_header_symbol():
+    from vstyler import _lib
+    lib = _lib.load()
+    for s in header_symbols():
+        assert hasattr(lib, s), s
+        assert s in _lib.SIGNATURES, f"{s} has no ctypes signature"
+    assert lib.vs_abi_version() == 1
+
+
+def test_error_codes_and_messages():
+    from vstyler import _lib
+    lib = _lib.load()
+    assert lib.vs_strerror(0) == b"VS_OK"
+    assert lib.vs_strerror(1).startswith(b"VS_E_INVALID")
+    assert lib.vs_strerror(3).startswith(b"VS_E_UNSUPPORTED")
+
+
+def test_invalid_arguments_rejected_before_launch():
+    from vstyler import _lib
+    lib = _lib.load()
+    ep = _lib.VsEpilogue()
+    # null pointers
+    assert lib.vs_gemm(None, 64, None, 64, None, 64, 8, 8, 64, 0, ep, None, 0, None, 0, 0, None) == 1
+    fake = 1 << 20   # aligned non-null (never dereferenced: validation fails first)
+    # K not a multiple of 64
+    assert lib.vs_gemm(fake, 48, fake, 48, fake, 8, 8, 8, 48, 0, ep, None, 0, None, 0, 0, None) == 1
+    # bad epilogue id
+    assert lib.vs_gemm(fake, 64, fake, 64, fake, 8, 8, 8, 64, 9, ep, None, 0, None, 0, 0, None) == 1
+    # gate-residual without residual
+    assert lib.vs_gemm(fake, 64, fake, 64, fake, 8, 8, 8, 64, 3, ep, None, 0, None, 0, 0, None) == 1
+    # head_dim != 128 is unsupported, misaligned stride invalid
+    assert lib.vs_attn_fwd(fake, fake, fake, fake, 1, 16, 16, 1, 64, 64, 64, 64, 64, 0, 0, 0, 0, 1.0, None) == 3
+    assert lib.vs_attn_fwd(fake, fake, fake, fake, 1, 16, 16, 1, 128, 130, 128, 128, 128, 0, 0, 0, 0, 1.0, None) == 1
+    # rmsnorm dim too large / not multiple of 8
+    assert lib.vs_rmsnorm_rope(fake, 8000, 4, 8000, 128, fake, 1e-6, None, 0, 1, 1, 1, 0, 0, None) == 1
+    assert lib.vs_layernorm_modulate(fake, 12, fake, 12, 4, 12, 0, None, None, 0, None, None, 1e-6, None) == 1
+    # RoPE token range beyond the grid
+    assert lib.vs_rmsnorm_rope(fake, 256, 4, 256, 128, fake, 1e-6, fake, 1024, 1, 1, 2, 4, 0, None) == 1
+    # Ulysses permute: columns not a multiple of 8
+    assert lib.vs_ulysses_permute(fake, fake, 1, 4, 2, 12, 24, 48, 0, None) == 1
+
+
+def test_wrappers_raise_on_bad_dtype():
+    import torch
+    from vstyler import kernels as K
+    with pytest.raises(ValueError):
+        K.gemm(torch.zeros(4, 64), torch.zeros(4, 64), torch.zeros(4, 4))

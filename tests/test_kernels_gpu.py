@@ -1,0 +1,213 @@
+"""Per-kernel parity: libvstyler (through the C ABI) vs the CPU oracle on the same seeded inputs.
+
+Tolerances (bf16 path, fp32 accumulation): GEMM / attention rel-L2 <= 1e-2 and max-abs <= a few
+bf16 ulps of the output scale; elementwise kernels bit-exact or <= 1 bf16 ulp (stated per test).
+"""
+import math
+
+import pytest
+import torch
+
+from oracle import wan_oracle as O
+from gpu_util import BF16, err
+
+pytestmark = pytest.mark.gpu
+
+
+def rnd(*shape, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (scale * torch.randn(*shape, generator=g)).to(BF16)
+
+
+@pytest.fixture(scope="module")
+def K():
+    from vstyler import kernels
+    return kernels
+
+
+@pytest.mark.parametrize("M,N,Kd", [(300, 320, 256), (1, 64, 64), (517, 1536, 1536), (128, 8960 // 4, 512)])
+def test_gemm_bias(K, M, N, Kd):
+    a, w, b = rnd(M, Kd, seed=1), rnd(N, Kd, scale=0.05, seed=2), rnd(N, scale=0.1, seed=3)
+    ref = O.linear(a, w, b)
+    out = torch.empty(M, N, dtype=BF16, device="cuda")
+    K.gemm(a.cuda(), w.cuda(), out, bias=b.cuda())
+    mx, rl = err(out, ref)
+    assert rl < 4e-3 and mx < 0.05 * ref.float().abs().max().item() + 1e-2, (mx, rl)
+
+
+def test_gemm_asymmetric_exact(K):
+    # integer-valued operands: fp32 accumulation is exact -> bit-exact result; catches C transposes
+    M, N, Kd = 130, 132, 128
+    g = torch.Generator().manual_seed(4)
+    a = torch.randint(-3, 4, (M, Kd), generator=g).to(BF16)
+    w = torch.randint(-3, 4, (N, Kd), generator=g).to(BF16)
+    w[:, 0] += torch.arange(N).to(BF16) % 7
+    ref = O.linear(a, w)
+    out = torch.empty(M, N, dtype=BF16, device="cuda")
+    K.gemm(a.cuda(), w.cuda(), out)
+    assert torch.equal(out.cpu(), ref)
+
+
+def test_gemm_epilogues(K):
+    M, N, Kd, S = 300, 256, 192, 150
+    a, w, b = rnd(M, Kd, seed=5), rnd(N, Kd, scale=0.05, seed=6), rnd(N, scale=0.1, seed=7)
+    y = O.linear(a, w, b)
+    dev = lambda t: t.cuda()
+    out = torch.empty(M, N, dtype=BF16, device="cuda")
+    K.gemm(dev(a), dev(w), out, epilogue=K.VS_EPI_GELU, bias=dev(b))
+    assert err(out, O.gelu_tanh(y))[1] < 5e-3
+    K.gemm(dev(a), dev(w), out, epilogue=K.VS_EPI_SILU, bias=dev(b))
+    assert err(out, O.silu(y))[1] < 5e-3
+    # gate-residual with per-batch gate rows (2 batches of S rows) + VACE hint
+    res = rnd(M, N, seed=8)
+    gate = rnd(2, N, scale=0.5, seed=9)
+    hint = rnd(M, N, seed=10)
+    ref = torch.cat([O.gate_residual(res[:S], gate[0], y[:S]), O.gate_residual(res[S:], gate[1], y[S:])])
+    ref_h = O.add(ref, O.bf(hint.float() * 0.75))
+    x = dev(res.clone())
+    K.gemm(dev(a), dev(w), x, epilogue=K.VS_EPI_GATE_RES, bias=dev(b), residual=x, gate=dev(gate), gate_bstride=N,
+           rows_per_batch=S)
+    mx, rl = err(x, ref)
+    assert rl < 4e-3, (mx, rl)
+    x = dev(res.clone())
+    K.gemm(dev(a), dev(w), x, epilogue=K.VS_EPI_GATE_RES, bias=dev(b), residual=x, gate=dev(gate), gate_bstride=N,
+           rows_per_batch=S, hint=dev(hint), hint_scale=0.75)
+    assert err(x, ref_h)[1] < 4e-3
+    # residual add with alpha (LoRA merge form)
+    x = dev(res.clone())
+    K.gemm(dev(a), dev(w), x, epilogue=K.VS_EPI_RES, bias=dev(b), residual=x, alpha=0.5)
+    assert err(x, O.add(res, O.bf(0.5 * y.float())))[1] < 4e-3
+
+
+def test_gemm_lora_second_phase(K):
+    M, N, Kd, r = 200, 320, 256, 128
+    x, w, b = rnd(M, Kd, seed=11), rnd(N, Kd, scale=0.05, seed=12), rnd(N, scale=0.1, seed=13)
+    la, lb = rnd(r, Kd, scale=0.05, seed=14), rnd(N, r, scale=0.05, seed=15)
+    ref = O.lora_linear(x, w, b, la, lb)
+    t = torch.empty(M, r, dtype=BF16, device="cuda")
+    K.gemm(x.cuda(), la.cuda(), t)
+    out = torch.empty(M, N, dtype=BF16, device="cuda")
+    K.gemm(x.cuda(), w.cuda(), out, bias=b.cuda(), a2=t, w2=lb.cuda())
+    assert err(out, ref)[1] < 5e-3
+
+
+@pytest.mark.parametrize("B,Sq,Skv,H", [(1, 256, 256, 1), (2, 300, 300, 2), (2, 300, 77, 2), (1, 1000, 512, 3)])
+def test_attention(K, B, Sq, Skv, H):
+    D = H * 128
+    q, k, v = rnd(B, Sq, D, seed=20), rnd(B, Skv, D, seed=21), rnd(B, Skv, D, seed=22)
+    ref = O.attention(q, k, v, H)
+    out = torch.empty(B * Sq, D, dtype=BF16, device="cuda")
+    K.attention(q.cuda().view(B * Sq, D), k.cuda().view(B * Skv, D), v.cuda().view(B * Skv, D), out, H, B)
+    mx, rl = err(out.view(B, Sq, D), ref)
+    assert mx < 3e-2 and rl < 1e-2, (mx, rl)
+
+
+def test_attention_online_rescale_spike(K):
+    """Rule 26 of the CDNA guide: force the running-max rescale by a late large score."""
+    B, S, H = 1, 512, 1
+    q, k, v = rnd(B, S, 128, seed=30), rnd(B, S, 128, seed=31), rnd(B, S, 128, seed=32)
+    q[0, 5] = 4.0
+    k[0, 400] = 4.0          # tile 6 spikes query row 5's max
+    ref = O.attention(q, k, v, H)
+    out = torch.empty(S, 128, dtype=BF16, device="cuda")
+    K.attention(q.cuda().view(S, 128), k.cuda().view(S, 128), v.cuda().view(S, 128), out, H, B)
+    mx, rl = err(out.view(B, S, 128), ref)
+    assert mx < 3e-2, mx
+
+
+def test_attention_strided_views(K):
+    # q/k/v as column slices of a fused [M, 3D] buffer (row stride 3D)
+    B, S, H = 1, 200, 2
+    D = H * 128
+    qkv = rnd(B * S, 3 * D, seed=40)
+    ref = O.attention(qkv[:, :D].reshape(B, S, D), qkv[:, D:2 * D].reshape(B, S, D), qkv[:, 2 * D:].reshape(B, S, D), H)
+    d = qkv.cuda()
+    out = torch.empty(B * S, D, dtype=BF16, device="cuda")
+    K.attention(d[:, :D], d[:, D:2 * D], d[:, 2 * D:], out, H, B)
+    assert err(out.view(B, S, D), ref)[1] < 1e-2
+
+
+def test_layernorm_modulate(K):
+    B, S, D = 2, 37, 1536
+    x = rnd(B * S, D, scale=2.0, seed=50)
+    mod = rnd(B, 6, D, scale=0.3, seed=51)
+    ref = torch.cat([O.modulate(O.layer_norm(x[b * S:(b + 1) * S]), mod[b, 0], mod[b, 1]) for b in range(B)])
+    out = torch.empty(B * S, D, dtype=BF16, device="cuda")
+    md = mod.cuda()
+    K.layernorm_modulate(x.cuda(), out, 1e-6, shift=md[:, 0], scale=md[:, 1], mod_bstride=6 * D, rows_per_batch=S)
+    mx, _ = err(out, ref)
+    assert mx <= 2 ** -5 * max(1.0, ref.float().abs().max().item()), mx
+    w, b = rnd(D, scale=0.1, seed=52) + 1, rnd(D, scale=0.1, seed=53)
+    ref = O.layer_norm(x, 1e-6, w, b)
+    K.layernorm_modulate(x.cuda(), out, 1e-6, weight=w.cuda(), bias=b.cuda())
+    assert err(out, ref)[0] <= 2 ** -5 * max(1.0, ref.float().abs().max().item())
+
+
+def test_rmsnorm_rope(K):
+    B, grid, H = 2, (3, 4, 5), 2
+    S, D = 60, 256
+    x = rnd(B * S, D, scale=3.0, seed=60)
+    w = (1 + 0.1 * torch.randn(D, generator=torch.Generator().manual_seed(61))).to(BF16)
+    freqs = O.rope_freqs(*grid)
+    ref = O.rope_apply(O.rms_norm(x.view(B, S, D), w), freqs, H).reshape(B * S, D)
+    from vstyler.models import rope_table
+    xd = x.cuda()
+    K.rmsnorm_rope(xd, w.cuda(), 1e-6, rope=rope_table(device="cuda"), grid=grid, rows_per_batch=S)
+    mx, rl = err(xd, ref)
+    assert mx <= 2 ** -6 * 4 and rl < 2e-3, (mx, rl)
+    # no rope (cross-attention q/k) is exact to the rounding of the two bf16 products
+    xd = x.cuda()
+    K.rmsnorm_rope(xd, w.cuda(), 1e-6)
+    assert err(xd, O.rms_norm(x, w))[0] <= 2 ** -6 * 4
+    # SP shard: rows are the tokens [20, 40) of the grid
+    xs = x.view(B, S, D)[:, 20:40].reshape(B * 20, D).contiguous().cuda()
+    K.rmsnorm_rope(xs, w.cuda(), 1e-6, rope=rope_table(device="cuda"), grid=grid, rows_per_batch=20, token_offset=20)
+    assert err(xs.view(B, 20, D), ref.view(B, S, D)[:, 20:40])[1] < 2e-3
+
+
+def test_patchify_unpatchify_time_modadd_cfg(K):
+    lat = rnd(2, 16, 3, 8, 12, seed=70)
+    D = 64
+    cols = torch.empty(2 * 3 * 4 * 6, 64, dtype=BF16, device="cuda")
+    K.patchify(lat.cuda(), cols)
+    eye = torch.eye(D).reshape(D, 16, 1, 2, 2).to(BF16)
+    ref, grid = O.patchify(lat, eye, torch.zeros(D, dtype=BF16))
+    assert torch.equal(cols.cpu().view_as(ref), ref)
+    tok = rnd(2 * 3 * 4 * 6, 64, seed=71)
+    back = torch.empty(2, 16, 3, 8, 12, dtype=BF16, device="cuda")
+    K.unpatchify(tok.cuda(), back)
+    assert torch.equal(back.cpu(), O.unpatchify(tok.view(2, -1, 64), grid, 16))
+    t = torch.tensor([1000.0, 833.3333]).to(BF16)
+    s = torch.empty(2, 256, dtype=BF16, device="cuda")
+    K.time_sinusoid(t.cuda(), s)
+    assert torch.equal(s.cpu(), O.sinusoidal_embedding_1d(256, t))
+    p, tv = rnd(1, 6, 64, seed=72), rnd(2, 6, 64, seed=73)
+    out = torch.empty(2, 6, 64, dtype=BF16, device="cuda")
+    K.mod_add(p.cuda().view(6, 64), tv.cuda(), out, 6 * 64, 64)
+    assert torch.equal(out.cpu(), O.bf(p.float() + tv.float()))
+    vp, vn, x = rnd(1, 16, 2, 16, 16, seed=74), rnd(1, 16, 2, 16, 16, seed=75), rnd(1, 16, 2, 16, 16, seed=76)
+    sig, _ = O.set_timesteps(2)
+    ds = O.euler_delta(sig, 0)
+    ref = O.cfg_euler(vp, vn, x, 5.0, ds)
+    xd = x.cuda()
+    K.cfg_euler(vp.cuda(), vn.cuda(), xd, 5.0, float(ds))
+    assert torch.equal(xd.cpu(), ref)
+
+
+def test_ulysses_permute_roundtrip(K):
+    B, Sl, P, cpr = 2, 24, 4, 128
+    D = P * cpr
+    local = rnd(B * Sl, D, seed=80).cuda()
+    packed = torch.empty(P * B * Sl * cpr, dtype=BF16, device="cuda")
+    K.ulysses_permute(local, packed, B, Sl, P, cpr, D, B * Sl * cpr, 0)
+    ref = local.view(B, Sl, P, cpr).permute(2, 0, 1, 3).reshape(-1)
+    assert torch.equal(packed, ref)
+    back = torch.empty_like(local)
+    K.ulysses_permute(packed, back, B, Sl, P, cpr, D, B * Sl * cpr, 1)
+    assert torch.equal(back, local)
+    full = torch.empty(B * P * Sl, cpr, dtype=BF16, device="cuda")
+    K.ulysses_permute(packed, full, B, Sl, P, cpr, D, B * Sl * cpr, 2)
+    assert torch.equal(full.view(B, P, Sl, cpr), packed.view(P, B, Sl, cpr).permute(1, 0, 2, 3))
+    packed2 = torch.empty_like(packed)
+    K.ulysses_permute(full, packed2, B, Sl, P, cpr, D, B * Sl * cpr, 3)
+    assert torch.equal(packed2, packed)

@@ -1,0 +1,78 @@
+"""The oracle against the reference's own known-answer constants.
+
+The reference has no golden vectors; these KATs pin the oracle's structure: the md5 key-layout
+hashes from diffsynth/configs/model_config.py:142-179 (+ wan_video_dit.py:509,523,
+wan_video_vace.py:100) and the closed-form flow-matching schedule (schedulers/flow_match.py:34-58).
+"""
+import math
+
+import torch
+
+from oracle import wan_oracle as O
+
+
+def test_dit_key_layout_hashes_match_reference():
+    assert O.hash_state_dict_keys(O.dit_param_shapes(O.WAN_CONFIGS["1.3B"])) == "9269f8db9040a9d860eaca435be61814"
+    assert O.hash_state_dict_keys(O.dit_param_shapes(O.WAN_CONFIGS["14B"])) == "aafcfd9672c3a2456dc46e1cb6e52c70"
+
+
+def test_vace_key_layout_hashes_match_reference():
+    assert O.hash_state_dict_keys(O.vace_param_shapes(O.WAN_CONFIGS["14B"])) == "3b2726384e4f64837bdf216eea3f310d"
+    # combined DiT+VACE single-file hashes registered for (WanModel, VaceWanModel) (model_config.py:157-158)
+    registered = {"a61453409b67cd3246cf0c3bebad47ba", "7a513e1f257a861512b1afd387a8ecd9"}
+    for name in ("1.3B", "14B"):
+        c = O.WAN_CONFIGS[name]
+        both = dict(O.dit_param_shapes(c))
+        both.update(O.vace_param_shapes(c))
+        assert O.hash_state_dict_keys(both) in registered
+
+
+def test_product_model_keys_equal_oracle_layout():
+    from vstyler.models import VaceWanModel, WanModel
+    c = dict(O.WAN_CONFIGS["1.3B"])
+    dit = WanModel(dim=c["dim"], in_dim=16, ffn_dim=c["ffn_dim"], out_dim=16, text_dim=4096, freq_dim=256, eps=1e-6,
+                   patch_size=(1, 2, 2), num_heads=c["num_heads"], num_layers=c["num_layers"], device="meta")
+    shapes = {k: tuple(v.shape) for k, v in dit.state_dict().items()}
+    assert O.hash_state_dict_keys(shapes) == "9269f8db9040a9d860eaca435be61814"
+    vace = VaceWanModel(vace_layers=c["vace_layers"], dim=c["dim"], num_heads=c["num_heads"], ffn_dim=c["ffn_dim"],
+                        device="meta")
+    vs = {k: tuple(v.shape) for k, v in vace.state_dict().items()}
+    both = dict(shapes)
+    both.update(vs)
+    assert O.hash_state_dict_keys(both) == "a61453409b67cd3246cf0c3bebad47ba"
+
+
+def test_sigma_schedule_closed_form():
+    for n in (2, 4, 50):
+        sig, ts = O.set_timesteps(n, shift=5.0)
+        for i in range(n):
+            s = 1.0 - i / n
+            assert math.isclose(float(sig[i]), 5 * s / (1 + 4 * s), rel_tol=0, abs_tol=2e-7)
+        assert torch.allclose(ts, sig * 1000)
+        assert float(O.euler_delta(sig, n - 1)) == -float(sig[-1])
+
+
+def test_sinusoid_and_rope_tables():
+    t = torch.tensor([1000.0]).to(torch.bfloat16)
+    e = O.sinusoidal_embedding_1d(256, t)
+    assert e.shape == (1, 256) and e.dtype == torch.bfloat16
+    assert float(e[0, 0]) == 1.0 or abs(float(e[0, 0]) - math.cos(1000.0)) < 1e-2
+    tf, th, tw = O.rope_tables(128)
+    assert tf.shape == (1024, 22) and th.shape == (1024, 21) and tw.shape == (1024, 21)
+    f = O.rope_freqs(2, 3, 4)
+    assert f.shape == (24, 1, 64)
+    # token (f=1,h=2,w=3) -> pairs 0..21 use position 1, 22..42 position 2, 43..63 position 3
+    tok = 1 * 12 + 2 * 4 + 3
+    assert torch.allclose(f[tok, 0, :22], tf[1]) and torch.allclose(f[tok, 0, 22:43], th[2])
+    assert torch.allclose(f[tok, 0, 43:], tw[3])
+
+
+def test_unpatchify_inverts_patchify_layout():
+    lat = torch.randn(2, 16, 3, 8, 6).to(torch.bfloat16)
+    D = 64
+    eye = torch.eye(D).reshape(D, 16, 1, 2, 2).to(torch.bfloat16)   # identity conv: token = im2col
+    tok, grid = O.patchify(lat, eye, torch.zeros(D, dtype=torch.bfloat16))
+    # im2col column order c*4+kh*2+kw; head/unpatchify order (y*2+z)*16+c
+    perm = torch.tensor([c * 4 + y * 2 + z for y in range(2) for z in range(2) for c in range(16)])
+    back = O.unpatchify(tok[..., perm], grid, 16)
+    assert torch.equal(back, lat)

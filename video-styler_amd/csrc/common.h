@@ -1,0 +1,52 @@
+// Shared device helpers for the gfx950 kernels of libvstyler.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/vstyler.h"
+
+typedef uint16_t bf16_t;  // raw bf16 bits in global memory
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+#define LDS_AS __attribute__((address_space(3)))
+#define GLB_AS __attribute__((address_space(1)))
+
+__device__ __forceinline__ float bf2f(uint32_t h) { return __uint_as_float(h << 16); }
+__device__ __forceinline__ float bflo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bfhi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// round-to-nearest-even fp32 -> bf16 (hipcc lowers the __bf16 cast to v_cvt_pk_bf16_f32 on gfx950)
+__device__ __forceinline__ uint32_t f2bf(float f) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)f);
+}
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) { return f2bf(lo) | (f2bf(hi) << 16); }
+// materialise a bf16 rounding point inside fp32 arithmetic
+__device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
+
+__device__ __forceinline__ float gelu_tanh_f(float x) {
+    // 0.5*x*(1+tanh(sqrt(2/pi)*(x+0.044715x^3)))  (torch GELU approximate='tanh')
+    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+    float u = k0 * (x + k1 * x * x * x);
+    return 0.5f * x * (1.0f + tanhf(u));
+}
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
+
+// Bijective XCD-aware remap of a linear workgroup id (MI355X deals workgroups round-robin over
+// 8 XCDs; this gives each XCD a contiguous chunk of the logical id space so that neighbouring
+// tiles share that XCD's L2).  cdna_hip_programming.md §5 "XCD swizzle must be bijective".
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    const int nx = 8;
+    int q = nwg / nx, r = nwg % nx;
+    int xcd = orig % nx, loc = orig / nx;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+#define VS_CHECK_LAUNCH()                                            \
+    do {                                                             \
+        if (hipGetLastError() != hipSuccess) return VS_E_LAUNCH;     \
+    } while (0)

@@ -1,0 +1,417 @@
+// HBM-bound row/elementwise kernels of the Wan2.1 DiT path, gfx950.
+// All loads/stores are 16-B vectorised (8 bf16 per lane); normalisations keep the row in
+// registers between the reduction and the write (one HBM read + one write per element).
+#include "common.h"
+
+namespace {
+
+constexpr int RT = 256;     // threads per row-kernel block
+constexpr int MAXCH = 3;    // 8-element chunks per thread -> dim <= 6144
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < RT / 64; ++i) t += red[i];
+    return t;
+}
+
+__device__ __forceinline__ void unpack8(const u32x4_t& w, float* v) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[2 * i] = bflo(w[i]);
+        v[2 * i + 1] = bfhi(w[i]);
+    }
+}
+__device__ __forceinline__ u32x4_t pack8(const float* v) {
+    u32x4_t w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = pack2(v[2 * i], v[2 * i + 1]);
+    return w;
+}
+
+// LayerNorm (fp32, eps) [affine] -> bf16, then optional modulate  (layers.py:89-91,
+// wan_video_dit.py:64-65): out = bf16(bf16(n * bf16(1 + scale)) + shift)
+__global__ __launch_bounds__(RT) void ln_modulate_kernel(
+    const bf16_t* __restrict__ x, long long ldx, bf16_t* __restrict__ out, long long ldo, int dim,
+    int rpb, const bf16_t* __restrict__ shift, const bf16_t* __restrict__ scale, long long mbs,
+    const bf16_t* __restrict__ w, const bf16_t* __restrict__ bb, float eps) {
+    __shared__ float red[RT / 64];
+    const long long row = blockIdx.x;
+    const int nch = dim >> 3;
+    const bf16_t* xr = x + row * ldx;
+    float v[MAXCH][8];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXCH; ++c) {
+        const int ch = threadIdx.x + c * RT;
+        if (ch < nch) {
+            unpack8(*reinterpret_cast<const u32x4_t*>(xr + ch * 8), v[c]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s += v[c][e];
+        }
+    }
+    const float mean = block_sum(s, red) / dim;
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXCH; ++c) {
+        const int ch = threadIdx.x + c * RT;
+        if (ch < nch) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float d = v[c][e] - mean;
+                q += d * d;
+            }
+        }
+    }
+    const float rstd = rsqrtf(block_sum(q, red) / dim + eps);
+    const long long bidx = row / rpb;
+    bf16_t* orow = out + row * ldo;
+#pragma unroll
+    for (int c = 0; c < MAXCH; ++c) {
+        const int ch = threadIdx.x + c * RT;
+        if (ch >= nch) continue;
+        float y[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) y[e] = (v[c][e] - mean) * rstd;
+        if (w) {
+            float wv[8], bv[8];
+            unpack8(*reinterpret_cast<const u32x4_t*>(w + ch * 8), wv);
+            unpack8(*reinterpret_cast<const u32x4_t*>(bb + ch * 8), bv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[e] = y[e] * wv[e] + bv[e];
+        }
+        if (shift) {
+            float sh[8], sc[8];
+            unpack8(*reinterpret_cast<const u32x4_t*>(shift + bidx * mbs + ch * 8), sh);
+            unpack8(*reinterpret_cast<const u32x4_t*>(scale + bidx * mbs + ch * 8), sc);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[e] = rbf(rbf(rbf(y[e]) * rbf(1.f + sc[e])) + sh[e]);
+        }
+        *reinterpret_cast<u32x4_t*>(orow + ch * 8) = pack8(y);
+    }
+}
+
+// RMSNorm over the full row (wan_video_dit.py:106-111) + interleaved 3-D RoPE (:92-97)
+__global__ __launch_bounds__(RT) void rmsnorm_rope_kernel(
+    bf16_t* __restrict__ x, long long ldx, int dim, int hd, const bf16_t* __restrict__ w, float eps,
+    const float2* __restrict__ rope, int rope_len, int gf, int gh, int gw, int rpb, int tok_off) {
+    __shared__ float red[RT / 64];
+    const long long row = blockIdx.x;
+    const int nch = dim >> 3;
+    bf16_t* xr = x + row * ldx;
+    float v[MAXCH][8];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXCH; ++c) {
+        const int ch = threadIdx.x + c * RT;
+        if (ch < nch) {
+            unpack8(*reinterpret_cast<const u32x4_t*>(xr + ch * 8), v[c]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s += v[c][e] * v[c][e];
+        }
+    }
+    const float r = rsqrtf(block_sum(s, red) / dim + eps);
+    int pf = 0, ph = 0, pw = 0;
+    if (rope) {
+        const int t = (int)(row % rpb) + tok_off;
+        pw = t % gw;
+        ph = (t / gw) % gh;
+        pf = t / (gw * gh);
+    }
+    const int half = hd >> 1;
+    const int tdim = half - 2 * (hd / 3 / 2);   // 22 temporal pairs for hd=128
+    const int hdim = hd / 3 / 2;                 // 21
+#pragma unroll
+    for (int c = 0; c < MAXCH; ++c) {
+        const int ch = threadIdx.x + c * RT;
+        if (ch >= nch) continue;
+        float wv[8], y[8];
+        unpack8(*reinterpret_cast<const u32x4_t*>(w + ch * 8), wv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) y[e] = rbf(rbf(v[c][e] * r) * wv[e]);
+        if (rope) {
+            const int pair0 = ((ch * 8) % hd) >> 1;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int j = pair0 + e;
+                const int pos = j < tdim ? pf : (j < tdim + hdim ? ph : pw);
+                const float2 cs = rope[(long long)pos * half + j];
+                const float a = y[2 * e], b = y[2 * e + 1];
+                y[2 * e] = a * cs.x - b * cs.y;
+                y[2 * e + 1] = a * cs.y + b * cs.x;
+            }
+        }
+        *reinterpret_cast<u32x4_t*>(xr + ch * 8) = pack8(y);
+    }
+    (void)rope_len;
+}
+
+// Conv3d (1,2,2) im2col: one thread per (token, channel) writes 4 contiguous columns
+__global__ void patchify_kernel(const bf16_t* __restrict__ lat, bf16_t* __restrict__ tok, int C,
+                                int T, int H, int W, long long total) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int h2 = H >> 1, w2 = W >> 1;
+    const int c = (int)(i % C);
+    const long long t = i / C;                 // global token (b, f, hh, ww)
+    const int ww = (int)(t % w2);
+    const int hh = (int)((t / w2) % h2);
+    const int f = (int)((t / ((long long)w2 * h2)) % T);
+    const long long b = t / ((long long)w2 * h2 * T);
+    const bf16_t* src = lat + (((b * C + c) * T + f) * H + 2 * hh) * (long long)W + 2 * ww;
+    const uint32_t top = *reinterpret_cast<const uint32_t*>(src);
+    const uint32_t bot = *reinterpret_cast<const uint32_t*>(src + W);
+    u32x2_t o;
+    o[0] = top;
+    o[1] = bot;
+    *reinterpret_cast<u32x2_t*>(tok + t * (4LL * C) + 4 * c) = o;
+}
+
+// unpatchify: out[b][c][f][2hh+y][2ww+z] = tok[(b,f,hh,ww)][(2y+z)*C + c]
+__global__ void unpatchify_kernel(const bf16_t* __restrict__ tok, bf16_t* __restrict__ lat, int C,
+                                  int T, int H, int W, long long total) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int h2 = H >> 1, w2 = W >> 1;
+    const int ww = (int)(i % w2);
+    const int hh = (int)((i / w2) % h2);
+    const int f = (int)((i / ((long long)w2 * h2)) % T);
+    const int c = (int)((i / ((long long)w2 * h2 * T)) % C);
+    const long long b = i / ((long long)w2 * h2 * T * C);
+    const long long t = ((b * T + f) * h2 + hh) * (long long)w2 + ww;
+    const bf16_t* src = tok + t * (4LL * C) + c;
+    bf16_t* dst = lat + (((b * C + c) * T + f) * H + 2 * hh) * (long long)W + 2 * ww;
+    const uint32_t top = (uint32_t)src[0] | ((uint32_t)src[C] << 16);
+    const uint32_t bot = (uint32_t)src[2 * C] | ((uint32_t)src[3 * C] << 16);
+    *reinterpret_cast<uint32_t*>(dst) = top;
+    *reinterpret_cast<uint32_t*>(dst + W) = bot;
+}
+
+__global__ void cfg_euler_kernel(const bf16_t* __restrict__ vp, const bf16_t* __restrict__ vn,
+                                 bf16_t* __restrict__ x, long long n8, float g, float ds, int use_cfg) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= n8) return;
+    float a[8], b[8], xv[8];
+    unpack8(reinterpret_cast<const u32x4_t*>(vp)[i], a);
+    unpack8(reinterpret_cast<const u32x4_t*>(x)[i], xv);
+    if (use_cfg) unpack8(reinterpret_cast<const u32x4_t*>(vn)[i], b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        float v = a[e];
+        if (use_cfg) v = rbf(b[e] + rbf(g * rbf(a[e] - b[e])));
+        xv[e] = xv[e] + rbf(v * ds);
+    }
+    reinterpret_cast<u32x4_t*>(x)[i] = pack8(xv);
+}
+
+__global__ void time_sinusoid_kernel(const bf16_t* __restrict__ t, bf16_t* __restrict__ out, int dim) {
+    const int b = blockIdx.x;
+    const int half = dim >> 1;
+    const double pos = (double)bf2f(t[b]);
+    for (int i = threadIdx.x; i < half; i += blockDim.x) {
+        const double ang = pos * pow(10000.0, -(double)i / (double)half);
+        out[(long long)b * dim + i] = (bf16_t)f2bf((float)cos(ang));
+        out[(long long)b * dim + half + i] = (bf16_t)f2bf((float)sin(ang));
+    }
+}
+
+__global__ void mod_add_kernel(const bf16_t* __restrict__ p, const bf16_t* __restrict__ tv,
+                               bf16_t* __restrict__ out, int rows, int dim, long long tbs,
+                               long long trs, long long total) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int d = (int)(i % dim);
+    const int r = (int)((i / dim) % rows);
+    const long long b = i / ((long long)dim * rows);
+    const float v = bf2f(p[(long long)r * dim + d]) + bf2f(tv[b * tbs + r * trs + d]);
+    out[i] = (bf16_t)f2bf(v);
+}
+
+__global__ void axpy_kernel(bf16_t* __restrict__ x, const bf16_t* __restrict__ y, float s, long long n8) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= n8) return;
+    float a[8], b[8];
+    unpack8(reinterpret_cast<const u32x4_t*>(x)[i], a);
+    unpack8(reinterpret_cast<const u32x4_t*>(y)[i], b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = a[e] + rbf(b[e] * s);
+    reinterpret_cast<u32x4_t*>(x)[i] = pack8(a);
+}
+
+
+// Ulysses sequence-parallel row permutations (8 bf16 = 16 B per thread).  Canonical index
+// (j, b, t, c): rank-chunk j, batch b, local token t, column c within a rank's head group.
+//   packed: j*jstride + (b*Sl + t)*cpr + c         (all_to_all_single chunk j)
+//   local : (b*Sl + t)*ld + j*cpr + c             (token-sharded activations, all heads)
+//   full  : (b*P*Sl + j*Sl + t)*cpr + c            (head-sharded, full sequence)
+// mode 0 local->packed, 1 packed->local, 2 packed->full, 3 full->packed.
+__global__ void ulysses_permute_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst, int B,
+                                       int Sl, int P, int cpr, long long ld, long long jstride, int mode,
+                                       long long total8) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= total8) return;
+    const int c8 = cpr >> 3;
+    const int c = (int)(i % c8) * 8;
+    long long r = i / c8;
+    const int t = (int)(r % Sl);
+    r /= Sl;
+    const int b = (int)(r % B);
+    const int j = (int)(r / B);
+    const long long packed = j * jstride + ((long long)b * Sl + t) * cpr + c;
+    const long long local = ((long long)b * Sl + t) * ld + (long long)j * cpr + c;
+    const long long full = ((long long)b * P * Sl + (long long)j * Sl + t) * cpr + c;
+    long long so, d;
+    switch (mode) {
+        case 0: so = local; d = packed; break;
+        case 1: so = packed; d = local; break;
+        case 2: so = packed; d = full; break;
+        default: so = full; d = packed; break;
+    }
+    *reinterpret_cast<u32x4_t*>(dst + d) = *reinterpret_cast<const u32x4_t*>(src + so);
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+unsigned nblk(long long n, int t) { return (unsigned)((n + t - 1) / t); }
+
+}  // namespace
+
+extern "C" int vs_layernorm_modulate(const void* x, long long ldx, void* out, long long ldo,
+                                     int rows, int dim, int rows_per_batch, const void* shift,
+                                     const void* scale, long long mod_bstride, const void* weight,
+                                     const void* bias, float eps, void* stream) {
+    if (!x || !out || rows <= 0 || dim <= 0 || dim % 8 || dim > MAXCH * RT * 8) return VS_E_INVALID;
+    if (ldx < dim || ldo < dim || (ldx & 7) || (ldo & 7) || !al16(x) || !al16(out)) return VS_E_INVALID;
+    if ((shift == nullptr) != (scale == nullptr)) return VS_E_INVALID;
+    if ((weight == nullptr) != (bias == nullptr)) return VS_E_INVALID;
+    if (shift && (!al16(shift) || !al16(scale) || (mod_bstride & 7))) return VS_E_INVALID;
+    if (weight && (!al16(weight) || !al16(bias))) return VS_E_INVALID;
+    if (rows_per_batch <= 0) rows_per_batch = rows;
+    hipLaunchKernelGGL(ln_modulate_kernel, dim3(rows), dim3(RT), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, ldx, (bf16_t*)out, ldo, dim, rows_per_batch,
+                       (const bf16_t*)shift, (const bf16_t*)scale, mod_bstride,
+                       (const bf16_t*)weight, (const bf16_t*)bias, eps);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_rmsnorm_rope(void* x, long long ldx, int rows, int dim, int head_dim,
+                               const void* weight, float eps, const void* rope, int rope_len,
+                               int gf, int gh, int gw, int rows_per_batch, int token_offset,
+                               void* stream) {
+    if (!x || !weight || rows <= 0 || dim <= 0 || dim % 8 || dim > MAXCH * RT * 8) return VS_E_INVALID;
+    if (ldx < dim || (ldx & 7) || !al16(x) || !al16(weight)) return VS_E_INVALID;
+    if (rope) {
+        if (head_dim != 128 || dim % head_dim) return VS_E_UNSUPPORTED;
+        if (gf <= 0 || gh <= 0 || gw <= 0 || gf > rope_len || gh > rope_len || gw > rope_len)
+            return VS_E_INVALID;
+        if (rows_per_batch <= 0 || token_offset < 0 ||
+            (long long)token_offset + rows_per_batch > (long long)gf * gh * gw)
+            return VS_E_INVALID;
+    }
+    if (rows_per_batch <= 0) rows_per_batch = rows;
+    hipLaunchKernelGGL(rmsnorm_rope_kernel, dim3(rows), dim3(RT), 0, (hipStream_t)stream,
+                       (bf16_t*)x, ldx, dim, head_dim, (const bf16_t*)weight, eps,
+                       (const float2*)rope, rope_len, gf, gh, gw, rows_per_batch, token_offset);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_patchify(const void* lat, void* tokens, int batch, int channels, int frames,
+                           int height, int width, void* stream) {
+    if (!lat || !tokens || batch <= 0 || channels <= 0 || frames <= 0 || height <= 0 || width <= 0)
+        return VS_E_INVALID;
+    if (height % 2 || width % 2 || (reinterpret_cast<uintptr_t>(lat) & 3) || (reinterpret_cast<uintptr_t>(tokens) & 7))
+        return VS_E_INVALID;
+    const long long total = (long long)batch * frames * (height / 2) * (width / 2) * channels;
+    hipLaunchKernelGGL(patchify_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)lat, (bf16_t*)tokens, channels, frames, height, width, total);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_unpatchify(const void* tokens, void* lat, int batch, int channels, int frames,
+                             int height, int width, void* stream) {
+    if (!lat || !tokens || batch <= 0 || channels <= 0 || frames <= 0 || height <= 0 || width <= 0)
+        return VS_E_INVALID;
+    if (height % 2 || width % 2 || (reinterpret_cast<uintptr_t>(lat) & 3)) return VS_E_INVALID;
+    const long long total = (long long)batch * channels * frames * (height / 2) * (width / 2);
+    hipLaunchKernelGGL(unpatchify_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)tokens, (bf16_t*)lat, channels, frames, height, width, total);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_cfg_euler(const void* v_pos, const void* v_neg, void* x, long long n,
+                            float cfg_scale, float dsigma, int use_cfg, void* stream) {
+    if (!v_pos || !x || n <= 0 || n % 8 || (use_cfg && !v_neg)) return VS_E_INVALID;
+    if (!al16(v_pos) || !al16(x) || (use_cfg && !al16(v_neg))) return VS_E_INVALID;
+    const long long n8 = n / 8;
+    hipLaunchKernelGGL(cfg_euler_kernel, dim3(nblk(n8, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)v_pos, (const bf16_t*)v_neg, (bf16_t*)x, n8, cfg_scale,
+                       dsigma, use_cfg);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_time_sinusoid(const void* t, void* out, int batch, int dim, void* stream) {
+    if (!t || !out || batch <= 0 || dim <= 0 || dim % 2) return VS_E_INVALID;
+    hipLaunchKernelGGL(time_sinusoid_kernel, dim3(batch), dim3(128), 0, (hipStream_t)stream,
+                       (const bf16_t*)t, (bf16_t*)out, dim);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_mod_add(const void* param, const void* tv, void* out, int batch, int rows,
+                          int dim, long long tv_bstride, long long tv_rstride, void* stream) {
+    if (!param || !tv || !out || batch <= 0 || rows <= 0 || dim <= 0) return VS_E_INVALID;
+    const long long total = (long long)batch * rows * dim;
+    hipLaunchKernelGGL(mod_add_kernel, dim3(nblk(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)param, (const bf16_t*)tv, (bf16_t*)out, rows, dim,
+                       tv_bstride, tv_rstride, total);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_axpy(void* x, const void* y, float scale, long long n, void* stream) {
+    if (!x || !y || n <= 0 || n % 8 || !al16(x) || !al16(y)) return VS_E_INVALID;
+    const long long n8 = n / 8;
+    hipLaunchKernelGGL(axpy_kernel, dim3(nblk(n8, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (bf16_t*)x, (const bf16_t*)y, scale, n8);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+
+extern "C" int vs_ulysses_permute(const void* src, void* dst, int batch, int s_local, int world,
+                                  int cols_per_rank, long long ld_local, long long jstride, int mode,
+                                  void* stream) {
+    if (!src || !dst || batch <= 0 || s_local <= 0 || world <= 0 || cols_per_rank <= 0) return VS_E_INVALID;
+    if (cols_per_rank % 8 || (ld_local & 7) || (jstride & 7) || mode < 0 || mode > 3) return VS_E_INVALID;
+    if ((mode <= 1) && ld_local < (long long)world * cols_per_rank) return VS_E_INVALID;
+    if (jstride < (long long)batch * s_local * cols_per_rank) return VS_E_INVALID;
+    if (!al16(src) || !al16(dst)) return VS_E_INVALID;
+    const long long total8 = (long long)world * batch * s_local * (cols_per_rank / 8);
+    hipLaunchKernelGGL(ulysses_permute_kernel, dim3(nblk(total8, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)src, (bf16_t*)dst, batch, s_local, world, cols_per_rank, ld_local,
+                       jstride, mode, total8);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" const char* vs_strerror(int code) {
+    switch (code) {
+        case VS_OK: return "VS_OK";
+        case VS_E_INVALID: return "VS_E_INVALID: invalid shape, stride, alignment or pointer";
+        case VS_E_LAUNCH: return "VS_E_LAUNCH: kernel launch failed";
+        case VS_E_UNSUPPORTED: return "VS_E_UNSUPPORTED: configuration not implemented";
+        default: return "unknown vstyler error";
+    }
+}
+
+extern "C" int vs_abi_version(void) { return 1; }

@@ -1,0 +1,75 @@
+"""ctypes binding of libvstyler.so (the C ABI declared in include/vstyler.h).
+
+The product path has no CPU fallback: if the library is missing every op raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("VSTYLER_LIB", os.path.join(_HERE, "lib", "libvstyler.so"))
+
+VS_EPI_BIAS, VS_EPI_GELU, VS_EPI_SILU, VS_EPI_GATE_RES, VS_EPI_RES = range(5)
+
+
+class VsEpilogue(ctypes.Structure):
+    _fields_ = [
+        ("bias", ctypes.c_void_p),
+        ("residual", ctypes.c_void_p),
+        ("ld_res", ctypes.c_longlong),
+        ("gate", ctypes.c_void_p),
+        ("gate_bstride", ctypes.c_longlong),
+        ("hint", ctypes.c_void_p),
+        ("ld_hint", ctypes.c_longlong),
+        ("hint_scale", ctypes.c_float),
+        ("alpha", ctypes.c_float),
+        ("rows_per_batch", ctypes.c_int),
+        ("reserved", ctypes.c_int),
+    ]
+
+
+_P, _LL, _I, _F = ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_float
+
+# name -> argtypes (restype is int unless listed in _RESTYPES)
+SIGNATURES = {
+    "vs_abi_version": [],
+    "vs_strerror": [_I],
+    "vs_gemm": [_P, _LL, _P, _LL, _P, _LL, _I, _I, _I, _I, ctypes.POINTER(VsEpilogue),
+                _P, _LL, _P, _LL, _I, _P],
+    "vs_attn_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _LL, _LL, _LL, _LL, _LL, _LL, _LL, _LL,
+                    _F, _P],
+    "vs_layernorm_modulate": [_P, _LL, _P, _LL, _I, _I, _I, _P, _P, _LL, _P, _P, _F, _P],
+    "vs_rmsnorm_rope": [_P, _LL, _I, _I, _I, _P, _F, _P, _I, _I, _I, _I, _I, _I, _P],
+    "vs_patchify": [_P, _P, _I, _I, _I, _I, _I, _P],
+    "vs_unpatchify": [_P, _P, _I, _I, _I, _I, _I, _P],
+    "vs_cfg_euler": [_P, _P, _P, _LL, _F, _F, _I, _P],
+    "vs_time_sinusoid": [_P, _P, _I, _I, _P],
+    "vs_mod_add": [_P, _P, _P, _I, _I, _I, _LL, _LL, _P],
+    "vs_axpy": [_P, _P, _F, _LL, _P],
+    "vs_ulysses_permute": [_P, _P, _I, _I, _I, _I, _LL, _LL, _I, _P],
+}
+_RESTYPES = {"vs_strerror": ctypes.c_char_p}
+
+_lib = None
+
+
+def load():
+    """Load libvstyler.so once; raise (never fall back) if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libvstyler.so not found at {LIB_PATH}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (or make -C video-styler_amd/csrc)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        _lib = lib
+    return _lib
+
+
+def check(code):
+    if code != 0:
+        msg = load().vs_strerror(code).decode()
+        raise RuntimeError(f"vstyler kernel error {code}: {msg}")

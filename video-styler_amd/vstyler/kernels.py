@@ -1,0 +1,178 @@
+"""Typed wrappers over the C ABI: torch tensors in, launches on the current HIP stream.
+
+PyTorch is used only for device memory and streams; every computation below is a kernel of
+libvstyler.so.  Wrappers validate dtype/device/layout and raise ValueError before launching.
+"""
+import torch
+
+from . import _lib
+from ._lib import VS_EPI_BIAS, VS_EPI_GELU, VS_EPI_SILU, VS_EPI_GATE_RES, VS_EPI_RES, VsEpilogue
+
+BF16 = torch.bfloat16
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _req(t, name):
+    if t.dtype != BF16:
+        raise ValueError(f"{name}: expected bfloat16, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: expected a device (cuda/hip) tensor")
+    return t
+
+
+def _rows(t, name):
+    """(rows, cols, row_stride) of a 2-D view whose last dim is contiguous."""
+    _req(t, name)
+    if t.dim() < 2:
+        raise ValueError(f"{name}: expected >=2-D tensor")
+    if t.stride(-1) != 1:
+        raise ValueError(f"{name}: last dim must be contiguous")
+    if t.dim() > 2:
+        # all leading dims must collapse into one row index
+        rows = 1
+        for i in range(t.dim() - 1):
+            rows *= t.shape[i]
+        for i in range(t.dim() - 2):
+            if t.stride(i) != t.stride(i + 1) * t.shape[i + 1]:
+                raise ValueError(f"{name}: leading dims not collapsible")
+        return rows, t.shape[-1], t.stride(-2)
+    return t.shape[0], t.shape[1], t.stride(0)
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def gemm(a, w, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, gate_bstride=0,
+         hint=None, hint_scale=1.0, alpha=1.0, rows_per_batch=0, a2=None, w2=None):
+    """out[M,N] = epilogue(a[M,K] @ w[N,K]^T (+ a2 @ w2^T)) (see include/vstyler.h vs_gemm)."""
+    M, K, lda = _rows(a, "a")
+    N, Kw, ldw = _rows(w, "w")
+    Mo, No, ldc = _rows(out, "out")
+    if Kw != K or Mo != M or No != N:
+        raise ValueError(f"gemm shape mismatch a={tuple(a.shape)} w={tuple(w.shape)} out={tuple(out.shape)}")
+    ep = VsEpilogue()
+    ep.bias = _ptr(bias)
+    ep.hint_scale = float(hint_scale)
+    ep.alpha = float(alpha)
+    ep.rows_per_batch = int(rows_per_batch)
+    if residual is not None:
+        _, Nr, ldr = _rows(residual, "residual")
+        ep.residual, ep.ld_res = residual.data_ptr(), ldr
+    if gate is not None:
+        ep.gate, ep.gate_bstride = gate.data_ptr(), int(gate_bstride)
+    if hint is not None:
+        _, _, ldh = _rows(hint, "hint")
+        ep.hint, ep.ld_hint = hint.data_ptr(), ldh
+    k2, lda2, ldw2 = 0, 0, 0
+    if a2 is not None:
+        _, k2, lda2 = _rows(a2, "a2")
+        _, _, ldw2 = _rows(w2, "w2")
+    _lib.check(_lib.load().vs_gemm(a.data_ptr(), lda, w.data_ptr(), ldw, out.data_ptr(), ldc, M, N, K,
+                                   int(epilogue), ep, _ptr(a2), lda2, _ptr(w2), ldw2, k2, _stream(a)))
+    return out
+
+
+def attention(q, k, v, out, num_heads, batch, scale=None):
+    """q/out: [batch*Sq, >=H*128] rows, k/v: [batch*Skv, ...] (views with row strides allowed)."""
+    Mq, _, ldq = _rows(q, "q")
+    Mk, _, ldk = _rows(k, "k")
+    Mv, _, ldv = _rows(v, "v")
+    Mo, _, ldo = _rows(out, "out")
+    if Mq % batch or Mk % batch or Mk != Mv or Mo != Mq:
+        raise ValueError("attention: row counts do not match batch")
+    sq, skv = Mq // batch, Mk // batch
+    hd = 128
+    if scale is None:
+        scale = hd ** -0.5
+    _lib.check(_lib.load().vs_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), batch, sq,
+                                       skv, num_heads, hd, ldq, ldk, ldv, ldo, sq * ldq, skv * ldk,
+                                       skv * ldv, sq * ldo, float(scale), _stream(q)))
+    return out
+
+
+def layernorm_modulate(x, out, eps=1e-6, shift=None, scale=None, mod_bstride=0, rows_per_batch=0,
+                       weight=None, bias=None):
+    M, D, ldx = _rows(x, "x")
+    Mo, Do, ldo = _rows(out, "out")
+    if Mo != M or Do != D:
+        raise ValueError("layernorm_modulate: shape mismatch")
+    _lib.check(_lib.load().vs_layernorm_modulate(x.data_ptr(), ldx, out.data_ptr(), ldo, M, D, int(rows_per_batch),
+                                                 _ptr(shift), _ptr(scale), int(mod_bstride), _ptr(weight),
+                                                 _ptr(bias), float(eps), _stream(x)))
+    return out
+
+
+def rmsnorm_rope(x, weight, eps=1e-6, rope=None, grid=(1, 1, 1), rows_per_batch=0, token_offset=0, head_dim=128):
+    M, D, ldx = _rows(x, "x")
+    rlen = 0 if rope is None else rope.shape[0]
+    if rope is not None and (rope.dtype != torch.float32 or rope.shape[1] != head_dim // 2 or rope.shape[2] != 2):
+        raise ValueError("rope table must be float32 [len, head_dim/2, 2]")
+    gf, gh, gw = grid
+    _lib.check(_lib.load().vs_rmsnorm_rope(x.data_ptr(), ldx, M, D, head_dim, weight.data_ptr(), float(eps),
+                                           _ptr(rope), rlen, gf, gh, gw, int(rows_per_batch), int(token_offset),
+                                           _stream(x)))
+    return x
+
+
+def patchify(lat, out):
+    _req(lat, "lat")
+    B, C, T, H, W = lat.shape
+    if not lat.is_contiguous() or not out.is_contiguous() or out.numel() != lat.numel():
+        raise ValueError("patchify: contiguous tensors of equal numel required")
+    _lib.check(_lib.load().vs_patchify(lat.data_ptr(), out.data_ptr(), B, C, T, H, W, _stream(lat)))
+    return out
+
+
+def unpatchify(tokens, out):
+    _req(out, "out")
+    B, C, T, H, W = out.shape
+    if not tokens.is_contiguous() or not out.is_contiguous() or out.numel() != tokens.numel():
+        raise ValueError("unpatchify: contiguous tensors of equal numel required")
+    _lib.check(_lib.load().vs_unpatchify(tokens.data_ptr(), out.data_ptr(), B, C, T, H, W, _stream(out)))
+    return out
+
+
+def cfg_euler(v_pos, v_neg, x, cfg_scale, dsigma):
+    for t, n in ((v_pos, "v_pos"), (x, "x")):
+        _req(t, n)
+        if not t.is_contiguous():
+            raise ValueError(f"{n} must be contiguous")
+    use_cfg = v_neg is not None
+    _lib.check(_lib.load().vs_cfg_euler(v_pos.data_ptr(), _ptr(v_neg), x.data_ptr(), x.numel(), float(cfg_scale),
+                                        float(dsigma), int(use_cfg), _stream(x)))
+    return x
+
+
+def time_sinusoid(t, out):
+    _lib.check(_lib.load().vs_time_sinusoid(t.data_ptr(), out.data_ptr(), t.numel(), out.shape[-1], _stream(t)))
+    return out
+
+
+def mod_add(param, tv, out, tv_bstride, tv_rstride):
+    """out[b][r][d] = bf16(param[r][d] + tv[b*bs + r*rs + d]); out is [B, R, D] contiguous."""
+    B, R, D = out.shape
+    _lib.check(_lib.load().vs_mod_add(param.data_ptr(), tv.data_ptr(), out.data_ptr(), B, R, D, int(tv_bstride),
+                                      int(tv_rstride), _stream(out)))
+    return out
+
+
+def axpy(x, y, scale):
+    _lib.check(_lib.load().vs_axpy(x.data_ptr(), y.data_ptr(), float(scale), x.numel(), _stream(x)))
+    return x
+
+
+def ulysses_permute(src, dst, batch, s_local, world, cols_per_rank, ld_local, jstride, mode):
+    """Row permutation between token-sharded / all_to_all-packed / head-sharded layouts."""
+    _lib.check(_lib.load().vs_ulysses_permute(src.data_ptr(), dst.data_ptr(), int(batch), int(s_local), int(world),
+                                              int(cols_per_rank), int(ld_local), int(jstride), int(mode),
+                                              _stream(src)))
+    return dst
+
+
+__all__ = ["ulysses_permute", "gemm", "attention", "layernorm_modulate", "rmsnorm_rope", "patchify", "unpatchify", "cfg_euler",
+           "time_sinusoid", "mod_add", "axpy", "VS_EPI_BIAS", "VS_EPI_GELU", "VS_EPI_SILU", "VS_EPI_GATE_RES",
+           "VS_EPI_RES"]

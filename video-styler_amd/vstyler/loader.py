@@ -1,0 +1,98 @@
+"""Checkpoint loading with the reference's model detection (md5 of sorted 'key:shape' strings).
+
+Reference: diffsynth/models/utils.py:65-88 (readers), :148-182 (hash), diffsynth/models/
+model_manager.py:162-196 (detector), configs/model_config.py:142-179 (hash table),
+wan_video_dit.py:506-536 / wan_video_vace.py:98-113 (hash -> config).  Serialized files are read
+with safetensors or torch.load(weights_only=True) only.
+"""
+import hashlib
+import os
+
+import torch
+
+from .models import VaceWanModel, WanModel
+
+WAN_DIT_CONFIGS = {
+    "9269f8db9040a9d860eaca435be61814": dict(dim=1536, ffn_dim=8960, num_heads=12, num_layers=30),   # 1.3B
+    "aafcfd9672c3a2456dc46e1cb6e52c70": dict(dim=5120, ffn_dim=13824, num_heads=40, num_layers=40),  # 14B
+}
+WAN_COMMON = dict(in_dim=16, out_dim=16, text_dim=4096, freq_dim=256, eps=1e-6, patch_size=(1, 2, 2))
+VACE_14B_HASH = "3b2726384e4f64837bdf216eea3f310d"
+VACE_14B = dict(vace_layers=(0, 5, 10, 15, 20, 25, 30, 35), vace_in_dim=96, patch_size=(1, 2, 2),
+                dim=5120, num_heads=40, ffn_dim=13824, eps=1e-6)
+VACE_DEFAULT = dict(vace_layers=tuple(range(0, 30, 2)), vace_in_dim=96, patch_size=(1, 2, 2),
+                    dim=1536, num_heads=12, ffn_dim=8960, eps=1e-6)   # VaceWanModel() defaults
+
+
+def hash_state_dict_keys(state_dict, with_shape=True):
+    """models/utils.py:148-182."""
+    keys = []
+    for key, value in state_dict.items():
+        if isinstance(key, str) and isinstance(value, torch.Tensor):
+            if with_shape:
+                keys.append(key + ":" + "_".join(map(str, list(value.shape))))
+            keys.append(key)
+    keys.sort()
+    return hashlib.md5(",".join(keys).encode("UTF-8")).hexdigest()
+
+
+def load_state_dict(path, device="cpu", torch_dtype=None):
+    if isinstance(path, (list, tuple)):
+        sd = {}
+        for p in path:
+            sd.update(load_state_dict(p, device, torch_dtype))
+        return sd
+    if os.path.isdir(path):
+        sd = {}
+        for name in sorted(os.listdir(path)):
+            if name.split(".")[-1] in ("safetensors", "bin", "ckpt", "pth", "pt"):
+                sd.update(load_state_dict(os.path.join(path, name), device, torch_dtype))
+        return sd
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        sd = load_file(path, device=str(device))
+    else:
+        sd = torch.load(path, map_location=device, weights_only=True)
+    if torch_dtype is not None:
+        sd = {k: (v.to(torch_dtype) if isinstance(v, torch.Tensor) and v.is_floating_point() else v)
+              for k, v in sd.items()}
+    return sd
+
+
+def build_dit(state_dict, device):
+    sd = {k: v for k, v in state_dict.items() if not k.startswith("vace")}
+    h = hash_state_dict_keys(sd)
+    if h not in WAN_DIT_CONFIGS:
+        return None
+    cfg = dict(WAN_COMMON, **WAN_DIT_CONFIGS[h])
+    model = WanModel(device=device, **cfg)
+    model.load_state_dict({k: v.to(torch.bfloat16) for k, v in sd.items()}, strict=True)
+    return model
+
+
+def build_vace(state_dict, device):
+    sd = {k: v for k, v in state_dict.items() if k.startswith("vace")}
+    if not sd:
+        return None
+    cfg = VACE_14B if hash_state_dict_keys(sd) == VACE_14B_HASH else VACE_DEFAULT
+    model = VaceWanModel(device=device, **cfg)
+    model.load_state_dict({k: v.to(torch.bfloat16) for k, v in sd.items()}, strict=True)
+    return model
+
+
+def load_models(paths, device="cuda"):
+    """Returns {'wan_video_dit': WanModel, 'wan_video_vace': VaceWanModel, ...} for the files given."""
+    out = {}
+    for path in paths:
+        sd = load_state_dict(path, device="cpu")
+        if "model_state" in sd:       # Wan VAE .pth layout (wan_video_vae.py:1262-1263)
+            raise NotImplementedError("Wan2.1 VAE checkpoint: VAE kernels are not built in this round")
+        dit = build_dit(sd, device)
+        if dit is not None:
+            out["wan_video_dit"] = dit
+            vace = build_vace(sd, device)
+            if vace is not None:
+                out["wan_video_vace"] = vace
+            continue
+        raise NotImplementedError(f"unrecognised checkpoint {path} (hash {hash_state_dict_keys(sd)})")
+    return out

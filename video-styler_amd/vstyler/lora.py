@@ -1,0 +1,90 @@
+"""LoRA for the VACE/DiT linears.
+
+merge_lora   : GeneralLoRALoader.load (diffsynth/lora/__init__.py:11-45): W <- W + alpha*(B@A),
+               computed by the MFMA GEMM with the VS_EPI_RES epilogue (bf16 mm, *alpha, + W).
+hotload_lora : AutoWrappedLinear hot-load (vram_management/layers.py:180-182, pipeline
+               wan_video_new.py:96-103): y = W x + b + B (alpha A x), fused into the main GEMM as a
+               second K phase (the "LoRA-fused linear" of BASELINE config 3).
+"""
+import torch
+
+from . import kernels as K
+from .models import Linear
+
+BF16 = torch.bfloat16
+
+
+def load_lora_state_dict(lora_config, device):
+    from .loader import load_state_dict
+    if isinstance(lora_config, str):
+        path = lora_config
+    else:
+        lora_config.download_if_necessary()
+        path = lora_config.path
+    return load_state_dict(path, device=device, torch_dtype=BF16)
+
+
+def get_name_dict(lora_state_dict):
+    """lora/__init__.py:11-25: '<prefix>.<name>.lora_B[.default].weight' -> module name."""
+    names = {}
+    for key in lora_state_dict:
+        if ".lora_B." not in key:
+            continue
+        keys = key.split(".")
+        if len(keys) > keys.index("lora_B") + 2:
+            keys.pop(keys.index("lora_B") + 1)
+        keys.pop(keys.index("lora_B"))
+        if keys[0] == "diffusion_model":
+            keys.pop(0)
+        keys.pop(-1)
+        names[".".join(keys)] = (key, key.replace(".lora_B.", ".lora_A."))
+    return names
+
+
+def _padded(t, rows=None, cols=None):
+    """zero-pad a 2-D bf16 matrix so its K dim is a multiple of 64 (exact for a low-rank product)."""
+    r, c = t.shape
+    rr = rows or r
+    cc = cols or c
+    if (rr, cc) == (r, c) and t.is_contiguous():
+        return t
+    out = torch.zeros((rr, cc), dtype=t.dtype, device=t.device)
+    out[:r, :c] = t
+    return out
+
+
+def merge_lora(model, lora, alpha=1.0):
+    updated = 0
+    names = get_name_dict(lora)
+    for name, module in model.named_modules():
+        if name in names and isinstance(module, Linear):
+            up = lora[names[name][0]].to(device=module.weight.device, dtype=BF16)     # B: [out, r]
+            down = lora[names[name][1]].to(device=module.weight.device, dtype=BF16)   # A: [r, in]
+            if up.dim() == 4:
+                up, down = up[:, :, 0, 0], down[:, :, 0, 0]
+            r = up.shape[1]
+            rp = (r + 63) // 64 * 64
+            b_mat = _padded(up, cols=rp)                          # [out, rp]
+            a_t = _padded(down.t().contiguous(), cols=rp)         # [in, rp]
+            w = module.weight
+            K.gemm(b_mat, a_t, w, epilogue=K.VS_EPI_RES, residual=w, alpha=float(alpha))
+            updated += 1
+    print(f"{updated} tensors are updated by LoRA.")
+    return updated
+
+
+def hotload_lora(model, lora, alpha=1.0):
+    """Attach (alpha*A, B) pairs to each matching Linear; the GEMM adds them as a fused K phase."""
+    updated = 0
+    for name, module in model.named_modules():
+        if not isinstance(module, Linear):
+            continue
+        ka, kb = f"{name}.lora_A.default.weight", f"{name}.lora_B.default.weight"
+        if ka in lora and kb in lora:
+            a = (lora[ka].to(device=module.weight.device, dtype=BF16) * alpha).to(BF16)   # [r, in]
+            b = lora[kb].to(device=module.weight.device, dtype=BF16)                       # [out, r]
+            rp = (a.shape[0] + 63) // 64 * 64
+            module.lora_A = _padded(a, rows=rp)          # [rp, in]
+            module.lora_B = _padded(b, cols=rp)          # [out, rp]
+            updated += 1
+    return updated

@@ -1,0 +1,335 @@
+"""Wan2.1 DiT + VACE branch on MI355X.
+
+Parameter containers keep the reference's module names and shapes (so a reference state dict
+loads by name and reproduces the reference's md5 key-layout hash, models/utils.py:148-182); the
+forward passes are sequences of libvstyler kernels (vstyler.kernels), never torch math.
+
+Reference: diffsynth/models/wan_video_dit.py (DiTBlock :196-230, Head :253-269, WanModel
+:272-352), diffsynth/models/wan_video_vace.py (:5-87), model_fn_wan_video
+(diffsynth/pipelines/wan_video_new.py:1260-1468).
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from . import kernels as K
+
+BF16 = torch.bfloat16
+
+
+def _param(*shape, device=None, dtype=BF16):
+    return nn.Parameter(torch.empty(*shape, device=device, dtype=dtype), requires_grad=False)
+
+
+class Linear(nn.Module):
+    """Weight [out, in] + bias, bf16 (the nn.Linear layout the MFMA GEMM reads K-contiguous)."""
+
+    def __init__(self, in_features, out_features, bias=True, device=None, dtype=BF16):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.weight = _param(out_features, in_features, device=device, dtype=dtype)
+        self.bias = _param(out_features, device=device, dtype=dtype) if bias else None
+
+
+def linear(lin, x, out, ws, **epi):
+    """Linear through vs_gemm; a hot-loaded LoRA (lin.lora_A = alpha*A, lin.lora_B = B) is fused as
+    the GEMM's second K phase (AutoWrappedLinear, vram_management/layers.py:173-188)."""
+    la = getattr(lin, "lora_A", None)
+    a2 = w2 = None
+    if la is not None:
+        t = ws.get("lora_t", (x.shape[0], la.shape[0]))
+        K.gemm(x, la, t)
+        a2, w2 = t, lin.lora_B
+    return K.gemm(x, lin.weight, out, bias=lin.bias, a2=a2, w2=w2, **epi)
+
+
+class PatchEmbed(nn.Module):
+    """Conv3d(in, dim, k=s=(1,2,2)) parameters (wan_video_dit.py:306-307)."""
+
+    def __init__(self, in_dim, dim, device=None):
+        super().__init__()
+        self.in_dim, self.dim = in_dim, dim
+        self.weight = _param(dim, in_dim, 1, 2, 2, device=device)
+        self.bias = _param(dim, device=device)
+
+    def forward(self, lat, ws, tag):
+        B, C, T, H, W = lat.shape
+        S = T * (H // 2) * (W // 2)
+        cols = ws.get(tag + ".cols", (B * S, C * 4))
+        K.patchify(lat.contiguous(), cols)
+        out = ws.get(tag + ".out", (B * S, self.dim))
+        K.gemm(cols, self.weight.view(self.dim, C * 4), out, bias=self.bias)
+        return out, (T, H // 2, W // 2)
+
+
+class RMSNormW(nn.Module):
+    def __init__(self, dim, device=None):
+        super().__init__()
+        self.weight = _param(dim, device=device)
+
+
+class LayerNormAffine(nn.Module):
+    def __init__(self, dim, device=None):
+        super().__init__()
+        self.weight = _param(dim, device=device)
+        self.bias = _param(dim, device=device)
+
+
+class AttentionParams(nn.Module):
+    def __init__(self, dim, num_heads, device=None):
+        super().__init__()
+        self.dim, self.num_heads = dim, num_heads
+        self.q = Linear(dim, dim, device=device)
+        self.k = Linear(dim, dim, device=device)
+        self.v = Linear(dim, dim, device=device)
+        self.o = Linear(dim, dim, device=device)
+        self.norm_q = RMSNormW(dim, device=device)
+        self.norm_k = RMSNormW(dim, device=device)
+
+
+class Sequential3(nn.Module):
+    """Holds modules at indices 0 and 2 (Linear, act, Linear) to keep the reference's key names."""
+
+    def __init__(self, first, last):
+        super().__init__()
+        self.add_module("0", first)
+        self.add_module("2", last)
+
+    def __getitem__(self, i):
+        return getattr(self, str(i))
+
+
+class Workspace:
+    """Scratch buffers reused across blocks/steps (allocated once per shape; kernels never allocate)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs = {}
+
+    def get(self, name, shape, dtype=BF16):
+        shape = tuple(int(s) for s in shape)
+        t = self.bufs.get(name)
+        if t is None or t.shape != shape or t.dtype != dtype:
+            t = torch.empty(shape, device=self.device, dtype=dtype)
+            self.bufs[name] = t
+        return t
+
+
+class RunCtx:
+    """Per-forward constants shared by all blocks: batch/token geometry, RoPE table, SP info."""
+
+    def __init__(self, batch, seq, grid, rope, ctx, ctx_len, ws, sp=None, token_offset=0):
+        self.batch, self.seq, self.grid, self.rope = batch, seq, grid, rope
+        self.ctx, self.ctx_len, self.ws = ctx, ctx_len, ws
+        self.sp = sp                    # vstyler.usp.UlyssesGroup or None
+        self.token_offset = token_offset
+
+
+class DiTBlock(nn.Module):
+    """wan_video_dit.py:196-230 parameters; forward = fused kernel sequence on [B*S, D] rows."""
+
+    def __init__(self, dim, num_heads, ffn_dim, eps=1e-6, device=None):
+        super().__init__()
+        self.dim, self.num_heads, self.ffn_dim, self.eps = dim, num_heads, ffn_dim, eps
+        self.self_attn = AttentionParams(dim, num_heads, device)
+        self.cross_attn = AttentionParams(dim, num_heads, device)
+        self.norm3 = LayerNormAffine(dim, device)
+        self.ffn = Sequential3(Linear(dim, ffn_dim, device=device), Linear(ffn_dim, dim, device=device))
+        self.modulation = _param(1, 6, dim, device=device)
+
+    def forward(self, x, t_mod, rc, hint=None, hint_scale=1.0):
+        """x: [B*S, D] updated in place.  t_mod: [B, 6, D].  hint: [B*S, D] added after the block."""
+        B, S, D, eps, ws = rc.batch, rc.seq, self.dim, self.eps, rc.ws
+        M = B * S
+        mod = ws.get("mod", (B, 6, D))
+        K.mod_add(self.modulation.view(6, D), t_mod, mod, 6 * D, D)   # :218-219
+        sh_msa, sc_msa, g_msa, sh_mlp, sc_mlp, g_mlp = (mod[:, i] for i in range(6))
+        h = ws.get("h", (M, D))
+        # --- self-attention (wan_video_dit.py:225-226, :140-147)
+        K.layernorm_modulate(x, h, eps, shift=sh_msa, scale=sc_msa, mod_bstride=6 * D, rows_per_batch=S)
+        sa = self.self_attn
+        q, k, v, o = (ws.get(n, (M, D)) for n in ("q", "k", "v", "o"))
+        linear(sa.q, h, q, ws)
+        linear(sa.k, h, k, ws)
+        linear(sa.v, h, v, ws)
+        K.rmsnorm_rope(q, sa.norm_q.weight, eps, rope=rc.rope, grid=rc.grid, rows_per_batch=S,
+                       token_offset=rc.token_offset)
+        K.rmsnorm_rope(k, sa.norm_k.weight, eps, rope=rc.rope, grid=rc.grid, rows_per_batch=S,
+                       token_offset=rc.token_offset)
+        if rc.sp is not None:
+            rc.sp.attention(q, k, v, o, self.num_heads, B)
+        else:
+            K.attention(q, k, v, o, self.num_heads, B)
+        linear(sa.o, o, x, ws, epilogue=K.VS_EPI_GATE_RES, residual=x, gate=g_msa,
+               gate_bstride=6 * D, rows_per_batch=S)
+        # --- cross-attention (wan_video_dit.py:227, :171-186)
+        K.layernorm_modulate(x, h, eps, weight=self.norm3.weight, bias=self.norm3.bias)
+        ca = self.cross_attn
+        L = rc.ctx_len
+        kc, vc = ws.get("kc", (B * L, D)), ws.get("vc", (B * L, D))
+        linear(ca.q, h, q, ws)
+        K.rmsnorm_rope(q, ca.norm_q.weight, eps)
+        linear(ca.k, rc.ctx, kc, ws)
+        K.rmsnorm_rope(kc, ca.norm_k.weight, eps)
+        linear(ca.v, rc.ctx, vc, ws)
+        K.attention(q, kc, vc, o, self.num_heads, B)
+        linear(ca.o, o, x, ws, epilogue=K.VS_EPI_RES, residual=x)
+        # --- FFN (wan_video_dit.py:228-229) + VACE hint (wan_video_new.py:1450)
+        K.layernorm_modulate(x, h, eps, shift=sh_mlp, scale=sc_mlp, mod_bstride=6 * D, rows_per_batch=S)
+        f = ws.get("f", (M, self.ffn_dim))
+        linear(self.ffn[0], h, f, ws, epilogue=K.VS_EPI_GELU)
+        linear(self.ffn[2], f, x, ws, epilogue=K.VS_EPI_GATE_RES, residual=x,
+               gate=g_mlp, gate_bstride=6 * D, rows_per_batch=S, hint=hint, hint_scale=hint_scale)
+        return x
+
+
+class Head(nn.Module):
+    """wan_video_dit.py:253-269."""
+
+    def __init__(self, dim, out_dim, patch_size, eps, device=None):
+        super().__init__()
+        self.dim, self.out_dim, self.eps = dim, out_dim, eps
+        self.head = Linear(dim, out_dim * math.prod(patch_size), device=device)
+        self.modulation = _param(1, 2, dim, device=device)
+
+    def forward(self, x, t, rc):
+        B, S, D, ws = rc.batch, rc.seq, self.dim, rc.ws
+        hm = ws.get("head_mod", (B, 2, D))
+        K.mod_add(self.modulation.view(2, D), t, hm, D, 0)           # :267 (per-batch t row)
+        h = ws.get("h", (B * S, D))
+        K.layernorm_modulate(x, h, self.eps, shift=hm[:, 0], scale=hm[:, 1], mod_bstride=2 * D,
+                             rows_per_batch=S)
+        out = ws.get("head_out", (B * S, self.head.out_features))
+        K.gemm(h, self.head.weight, out, bias=self.head.bias)
+        return out
+
+
+def rope_table(head_dim=128, end=1024, theta=10000.0, device=None):
+    """float32 [end, head_dim/2, 2] (cos, sin) of the 3-D RoPE (wan_video_dit.py:75-89), from fp64."""
+    def freqs(dim):
+        return 1.0 / (theta ** (torch.arange(0, dim, 2)[: dim // 2].double() / dim))
+    f = torch.cat([freqs(head_dim - 2 * (head_dim // 3)), freqs(head_dim // 3), freqs(head_dim // 3)])
+    ang = torch.outer(torch.arange(end).double(), f)
+    tab = torch.stack([torch.cos(ang), torch.sin(ang)], dim=-1).float()
+    return tab.to(device)
+
+
+class WanModel(nn.Module):
+    """wan_video_dit.py:272-337 (has_image_input=False path used by Wan2.1-VACE / T2V)."""
+
+    def __init__(self, dim, in_dim, ffn_dim, out_dim, text_dim, freq_dim, eps, patch_size, num_heads,
+                 num_layers, has_image_input=False, device=None, **kwargs):
+        super().__init__()
+        if has_image_input:
+            raise NotImplementedError("image-conditioned Wan (I2V/FLF2V) is outside the Ditto hot path")
+        if dim // num_heads != 128:
+            raise NotImplementedError("head_dim must be 128 (all Wan2.1 models)")
+        self.dim, self.in_dim, self.ffn_dim, self.out_dim = dim, in_dim, ffn_dim, out_dim
+        self.text_dim, self.freq_dim, self.eps, self.num_heads = text_dim, freq_dim, eps, num_heads
+        self.patch_size = tuple(patch_size)
+        self.has_image_input = False
+        self.seperated_timestep = False
+        self.require_vae_embedding = True
+        self.require_clip_embedding = True
+        self.fuse_vae_embedding_in_latents = False
+        self.patch_embedding = PatchEmbed(in_dim, dim, device)
+        self.text_embedding = Sequential3(Linear(text_dim, dim, device=device), Linear(dim, dim, device=device))
+        self.time_embedding = Sequential3(Linear(freq_dim, dim, device=device), Linear(dim, dim, device=device))
+        self.time_projection = nn.Module()
+        self.time_projection.add_module("1", Linear(dim, 6 * dim, device=device))
+        self.blocks = nn.ModuleList([DiTBlock(dim, num_heads, ffn_dim, eps, device) for _ in range(num_layers)])
+        self.head = Head(dim, out_dim, patch_size, eps, device)
+        self._rope = None
+
+    def rope(self, device):
+        if self._rope is None or self._rope.device != torch.device(device):
+            self._rope = rope_table(self.dim // self.num_heads, device=device)
+        return self._rope
+
+    def time_embed(self, timestep, ws):
+        """t [B,D], t_mod [B,6,D] (wan_video_new.py:1351-1352)."""
+        B, D = timestep.shape[0], self.dim
+        s = ws.get("sinus", (B, self.freq_dim))
+        K.time_sinusoid(timestep.contiguous(), s)
+        u = ws.get("t_u", (B, D))
+        K.gemm(s, self.time_embedding[0].weight, u, epilogue=K.VS_EPI_SILU, bias=self.time_embedding[0].bias)
+        t = ws.get("t", (B, D))
+        K.gemm(u, self.time_embedding[2].weight, t, bias=self.time_embedding[2].bias)
+        st = ws.get("t_silu", (B, D))
+        K.gemm(u, self.time_embedding[2].weight, st, epilogue=K.VS_EPI_SILU, bias=self.time_embedding[2].bias)
+        tm = ws.get("t_mod", (B, 6 * D))
+        proj = getattr(self.time_projection, "1")
+        K.gemm(st, proj.weight, tm, bias=proj.bias)
+        return t, tm.view(B, 6, D)
+
+    def text_embed(self, context, ws):
+        """[B*L, text_dim] -> [B*L, D] (wan_video_dit.py:308-312)."""
+        BL = context.shape[0] * context.shape[1]
+        c = context.reshape(BL, self.text_dim).contiguous()
+        h = ws.get("ctx_h", (BL, self.dim))
+        K.gemm(c, self.text_embedding[0].weight, h, epilogue=K.VS_EPI_GELU, bias=self.text_embedding[0].bias)
+        out = ws.get("ctx", (BL, self.dim))
+        K.gemm(h, self.text_embedding[2].weight, out, bias=self.text_embedding[2].bias)
+        return out
+
+
+class VaceWanAttentionBlock(DiTBlock):
+    """wan_video_vace.py:5-24."""
+
+    def __init__(self, dim, num_heads, ffn_dim, eps=1e-6, block_id=0, device=None):
+        super().__init__(dim, num_heads, ffn_dim, eps, device)
+        self.block_id = block_id
+        if block_id == 0:
+            self.before_proj = Linear(dim, dim, device=device)
+        self.after_proj = Linear(dim, dim, device=device)
+
+
+class VaceWanModel(nn.Module):
+    """wan_video_vace.py:27-87; the hints are computed on the (possibly SP-sharded) token rows."""
+
+    def __init__(self, vace_layers=tuple(range(0, 30, 2)), vace_in_dim=96, patch_size=(1, 2, 2),
+                 has_image_input=False, dim=1536, num_heads=12, ffn_dim=8960, eps=1e-6, device=None):
+        super().__init__()
+        self.vace_layers = tuple(vace_layers)
+        self.vace_in_dim = vace_in_dim
+        self.vace_layers_mapping = {i: n for n, i in enumerate(self.vace_layers)}
+        self.vace_blocks = nn.ModuleList([
+            VaceWanAttentionBlock(dim, num_heads, ffn_dim, eps, block_id=i, device=device) for i in self.vace_layers])
+        self.vace_patch_embedding = PatchEmbed(vace_in_dim, dim, device)
+        self.dim = dim
+
+    def forward(self, x, vace_cols_out, t_mod, rc):
+        """x: patch-embedded main tokens [B*S, D]; vace_cols_out: patch-embedded control tokens
+        [B*S, D] (overwritten, becomes c).  Returns the list of hint buffers [B*S, D]."""
+        ws, D = rc.ws, self.dim
+        M = rc.batch * rc.seq
+        c = vace_cols_out
+        hints = []
+        for n, blk in enumerate(self.vace_blocks):
+            if n == 0:
+                c0 = ws.get("vace_c", (M, D))
+                linear(blk.before_proj, c, c0, ws, epilogue=K.VS_EPI_RES, residual=x)
+                c = c0
+            blk(c, t_mod, rc)
+            hint = ws.get(f"vace_hint{n}", (M, D))
+            linear(blk.after_proj, c, hint, ws)
+            hints.append(hint)
+        return hints
+
+
+def init_random_(module, seed=5, std=0.02):
+    """Synthetic on-device init of SURVEY.md §8(d) (used by bench.py / smoke; real checkpoints load
+    by name): N(0,std) weights, 0.01*N biases, modulation randn/sqrt(D), norm weights 1+0.1*N."""
+    g = torch.Generator(device=next(module.parameters()).device).manual_seed(seed)
+    with torch.no_grad():
+        for name, p in module.named_parameters():
+            if name.endswith("modulation"):
+                p.copy_(torch.randn(p.shape, generator=g, device=p.device) / p.shape[-1] ** 0.5)
+            elif "norm" in name and name.endswith("weight"):
+                p.copy_(1 + 0.1 * torch.randn(p.shape, generator=g, device=p.device))
+            elif name.endswith("bias"):
+                p.copy_(0.01 * torch.randn(p.shape, generator=g, device=p.device))
+            else:
+                p.normal_(0.0, std, generator=g)
+    return module

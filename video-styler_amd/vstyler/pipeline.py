@@ -1,0 +1,291 @@
+"""WanVideoPipeline / model_fn_wan_video with the reference call surface
+(diffsynth/pipelines/wan_video_new.py:32-560, 1260-1468), running on libvstyler kernels.
+
+Differences from the reference that are performance-only (same per-sample arithmetic):
+  * CFG runs as one batch-2 forward (posi, nega) instead of two batch-1 forwards; the per-batch
+    head modulation (mod + t[b]) equals the reference's batch-1 broadcast (wan_video_dit.py:267);
+  * sigma table on the host, Euler+CFG fused into one kernel (no per-step host sync);
+  * Ulysses SP shards the VACE branch too (the reference runs VACE unsharded).
+"""
+import os
+from dataclasses import dataclass
+from typing import Optional, Union
+
+import torch
+
+from . import kernels as K
+from .flow_match import FlowMatchScheduler
+from .models import RunCtx, Workspace, WanModel, VaceWanModel
+
+BF16 = torch.bfloat16
+
+_WS = {}
+
+
+def _workspace(device):
+    key = str(torch.device(device))
+    if key not in _WS:
+        _WS[key] = Workspace(device)
+    return _WS[key]
+
+
+_UNSUPPORTED = ("clip_feature", "y", "reference_latents", "audio_embeds", "motion_latents", "s2v_pose_latents",
+                "motion_bucket_id", "pose_latents", "face_pixel_values", "control_camera_latents_input",
+                "sliding_window_size", "tea_cache")
+
+
+def model_fn_wan_video(dit: WanModel, motion_controller=None, vace: VaceWanModel = None, animate_adapter=None,
+                       latents: torch.Tensor = None, timestep: torch.Tensor = None, context: torch.Tensor = None,
+                       vace_context=None, vace_scale=1.0, use_unified_sequence_parallel: bool = False,
+                       sp_group=None, **kwargs):
+    """One DiT(+VACE) forward (wan_video_new.py:1338-1468) -> [B,16,T,H,W] bf16 velocity.
+
+    `context` is [B, L, text_dim]; latents/timestep/vace_context with batch 1 are broadcast to B
+    (the cfg_merge convention of wan_video_new.py:1361-1364)."""
+    for name in _UNSUPPORTED:
+        if kwargs.get(name) is not None:
+            raise NotImplementedError(f"model_fn_wan_video: '{name}' is outside the Ditto hot path")
+    device = latents.device
+    ws = _workspace(device)
+    B, L = context.shape[0], context.shape[1]
+    if latents.shape[0] != B:
+        latents = latents.expand(B, *latents.shape[1:])
+    latents = latents.to(BF16).contiguous()
+    timestep = timestep.reshape(-1).to(device=device, dtype=BF16)
+    if timestep.shape[0] != B:
+        timestep = timestep.expand(B).contiguous()
+
+    t, t_mod = dit.time_embed(timestep, ws)
+    ctx = dit.text_embed(context.to(BF16), ws)
+    x, grid = dit.patch_embedding(latents, ws, "x")
+    S = grid[0] * grid[1] * grid[2]
+
+    sp = None
+    if use_unified_sequence_parallel:
+        sp = sp_group
+        if sp is None:
+            from .usp import get_default_group
+            sp = get_default_group()
+        if sp is not None and sp.world_size == 1:
+            sp = None
+    rc = RunCtx(B, S, grid, dit.rope(device), ctx, L, ws)
+
+    vace_x = None
+    if vace_context is not None and vace is not None:
+        vc = vace_context.to(BF16)
+        if vc.shape[0] != B:
+            vc = vc.expand(B, *vc.shape[1:])
+        vace_x, _ = vace.vace_patch_embedding(vc.contiguous(), ws, "vace")
+
+    if sp is not None:
+        x, vace_x, rc = sp.shard_tokens(x, vace_x, rc)
+
+    hints = vace(x, vace_x, t_mod, rc) if vace_x is not None else None
+    vmap = vace.vace_layers_mapping if hints is not None else {}
+    for i, blk in enumerate(dit.blocks):
+        hint = hints[vmap[i]] if i in vmap else None
+        blk(x, t_mod, rc, hint=hint, hint_scale=float(vace_scale))
+    out = dit.head(x, t, rc)
+    if sp is not None:
+        out = sp.gather_tokens(out, rc)
+    T, H2, W2 = grid
+    lat = torch.empty((B, dit.out_dim, T, 2 * H2, 2 * W2), device=device, dtype=BF16)
+    K.unpatchify(out, lat)
+    return lat
+
+
+@dataclass
+class ModelConfig:
+    """diffsynth/utils/__init__.py:158-218, offline: resolves local files only (no ModelScope)."""
+    path: Union[str, list, None] = None
+    model_id: str = None
+    origin_file_pattern: Union[str, list, None] = None
+    download_resource: str = "ModelScope"
+    offload_device: Optional[Union[str, torch.device]] = None
+    offload_dtype: Optional[torch.dtype] = None
+    local_model_path: str = None
+    skip_download: bool = False
+
+    def download_if_necessary(self, use_usp=False):
+        if self.path is not None:
+            return
+        if self.model_id is None:
+            raise ValueError('No valid model files. Please use `ModelConfig(path="xxx")` or '
+                             '`ModelConfig(model_id="xxx/yyy", origin_file_pattern="zzz")`.')
+        import glob
+        root = os.path.join(self.local_model_path or "./models", self.model_id)
+        pattern = self.origin_file_pattern or ""
+        if pattern == "" or pattern.endswith("/"):
+            self.path = os.path.join(root, pattern)
+            if not os.path.isdir(self.path):
+                raise FileNotFoundError(f"{self.path} not found (offline build: no ModelScope download)")
+            return
+        files = sorted(glob.glob(os.path.join(root, pattern)))
+        if not files:
+            raise FileNotFoundError(f"no local files match {os.path.join(root, pattern)} "
+                                    "(offline build: no ModelScope download)")
+        self.path = files[0] if len(files) == 1 else files
+
+
+class WanVideoPipeline:
+    """The Ditto drop-in (wan_video_new.py:32).  DiT/VACE/Euler/CFG on libvstyler kernels."""
+
+    def __init__(self, device="cuda", torch_dtype=BF16, tokenizer_path=None):
+        self.device = device
+        self.torch_dtype = torch_dtype
+        self.scheduler = FlowMatchScheduler(shift=5, sigma_min=0.0, extra_one_step=True)
+        self.text_encoder = None
+        self.prompter = None
+        self.image_encoder = None
+        self.dit: WanModel = None
+        self.dit2 = None
+        self.vae = None
+        self.vace: VaceWanModel = None
+        self.vace2 = None
+        self.motion_controller = None
+        self.animate_adapter = None
+        self.model_fn = model_fn_wan_video
+        self.height_division_factor = 16
+        self.width_division_factor = 16
+        self.time_division_factor = 4
+        self.time_division_remainder = 1
+        self.use_unified_sequence_parallel = False
+        self.sp_group = None
+        self.vram_management_enabled = False
+
+    # ---------------------------------------------------------------- loading
+    @staticmethod
+    def from_pretrained(torch_dtype=BF16, device="cuda", model_configs=(), tokenizer_config=None,
+                        audio_processor_config=None, redirect_common_files=True, use_usp=False):
+        """wan_video_new.py:341-413 (local files only)."""
+        from .loader import load_models
+        pipe = WanVideoPipeline(device=device, torch_dtype=torch_dtype)
+        if use_usp:
+            pipe.initialize_usp()
+            device = pipe.device
+        paths = []
+        for mc in model_configs:
+            mc.download_if_necessary(use_usp=use_usp)
+            paths.append(mc.path)
+        models = load_models(paths, device=device)
+        pipe.dit = models.get("wan_video_dit")
+        pipe.vace = models.get("wan_video_vace")
+        pipe.vae = models.get("wan_video_vae")
+        pipe.text_encoder = models.get("wan_video_text_encoder")
+        if use_usp:
+            pipe.enable_usp()
+        return pipe
+
+    def load_lora(self, module, lora_config=None, alpha=1, hotload=False, state_dict=None):
+        """wan_video_new.py:80-106."""
+        from .lora import load_lora_state_dict, merge_lora, hotload_lora
+        lora = state_dict if state_dict is not None else load_lora_state_dict(lora_config, self.device)
+        if hotload:
+            return hotload_lora(module, lora, alpha)
+        return merge_lora(module, lora, alpha)
+
+    def enable_vram_management(self, num_persistent_param_in_dit=None, vram_limit=None, vram_buffer=0.5):
+        """wan_video_new.py:124.  On MI355X (288 GB HBM) every weight stays resident, so there is no
+        offload state machine; LayerNorms already run in fp32 (WanAutoCastLayerNorm semantics)."""
+        self.vram_management_enabled = True
+
+    def initialize_usp(self):
+        from .usp import init_distributed
+        rank = init_distributed()
+        self.device = f"cuda:{rank}"
+
+    def enable_usp(self):
+        from .usp import get_default_group
+        self.sp_group = get_default_group()
+        self.use_unified_sequence_parallel = True
+
+    # ---------------------------------------------------------------- helpers
+    def check_resize_height_width(self, height, width, num_frames=None):
+        """utils/__init__.py:43-57."""
+        if height % self.height_division_factor != 0:
+            height = (height + self.height_division_factor - 1) // self.height_division_factor * self.height_division_factor
+        if width % self.width_division_factor != 0:
+            width = (width + self.width_division_factor - 1) // self.width_division_factor * self.width_division_factor
+        if num_frames is None:
+            return height, width
+        if num_frames % self.time_division_factor != self.time_division_remainder:
+            num_frames = (num_frames + self.time_division_factor - 1) // self.time_division_factor * \
+                self.time_division_factor + self.time_division_remainder
+        return height, width, num_frames
+
+    def generate_noise(self, shape, seed=None, rand_device="cpu", rand_torch_dtype=torch.float32):
+        """utils/__init__.py:117-122 (same CPU generator stream -> identical noise)."""
+        generator = None if seed is None else torch.Generator(rand_device).manual_seed(seed)
+        noise = torch.randn(shape, generator=generator, device=rand_device, dtype=rand_torch_dtype)
+        return noise.to(dtype=self.torch_dtype, device=self.device)
+
+    # ---------------------------------------------------------------- denoise
+    def denoise(self, latents, context_posi, context_nega, vace_context=None, vace_scale=1.0, cfg_scale=5.0,
+                num_inference_steps=50, sigma_shift=5.0, denoising_strength=1.0, progress_bar_cmd=None):
+        """The loop of wan_video_new.py:515-542 (cfg_merge batched), returns the final latents."""
+        self.scheduler.set_timesteps(num_inference_steps, denoising_strength=denoising_strength, shift=sigma_shift)
+        use_cfg = cfg_scale != 1.0
+        ctx = torch.cat([context_posi, context_nega], 0) if use_cfg else context_posi
+        latents = latents.to(device=self.device, dtype=BF16).contiguous().clone()
+        steps = range(len(self.scheduler.timesteps))
+        if progress_bar_cmd is not None:
+            steps = progress_bar_cmd(steps)
+        for i in steps:
+            timestep = self.scheduler.timesteps[i].reshape(1).to(dtype=BF16, device=self.device)
+            v = self.model_fn(dit=self.dit, vace=self.vace, latents=latents, timestep=timestep, context=ctx,
+                              vace_context=vace_context, vace_scale=vace_scale,
+                              use_unified_sequence_parallel=self.use_unified_sequence_parallel,
+                              sp_group=self.sp_group)
+            K.cfg_euler(v[0:1].contiguous(), v[1:2].contiguous() if use_cfg else None, latents, cfg_scale,
+                        self.scheduler.delta(i))
+        return latents
+
+    @torch.no_grad()
+    def __call__(self, prompt=None, negative_prompt="", input_image=None, end_image=None, input_video=None,
+                 denoising_strength=1.0, vace_video=None, vace_video_mask=None, vace_reference_image=None,
+                 vace_scale=1.0, seed=None, rand_device="cpu", height=480, width=832, num_frames=81,
+                 cfg_scale=5.0, cfg_merge=False, switch_DiT_boundary=0.875, num_inference_steps=50,
+                 sigma_shift=5.0, motion_bucket_id=None, tiled=True, tile_size=(30, 52), tile_stride=(15, 26),
+                 sliding_window_size=None, sliding_window_stride=None, tea_cache_l1_thresh=None,
+                 tea_cache_model_id="", progress_bar_cmd=None,
+                 # extensions of this build (the DiT path without T5/VAE):
+                 prompt_emb=None, negative_prompt_emb=None, vace_context=None, output_type="video", **kwargs):
+        """wan_video_new.py:416-560 for the Ditto path (T2V/VACE, no image/audio/camera inputs)."""
+        for name, val in (("input_image", input_image), ("end_image", end_image), ("input_video", input_video),
+                          ("motion_bucket_id", motion_bucket_id), ("sliding_window_size", sliding_window_size),
+                          ("tea_cache_l1_thresh", tea_cache_l1_thresh), ("vace_reference_image", vace_reference_image)):
+            if val is not None:
+                raise NotImplementedError(f"{name} is outside the Ditto hot path of this build")
+        height, width, num_frames = self.check_resize_height_width(height, width, num_frames)
+        T = (num_frames - 1) // 4 + 1
+        noise = self.generate_noise((1, 16, T, height // 8, width // 8), seed=seed, rand_device=rand_device)
+        if prompt_emb is None:
+            prompt_emb = self.encode_prompt(prompt)
+        if negative_prompt_emb is None and cfg_scale != 1.0:
+            negative_prompt_emb = self.encode_prompt(negative_prompt)
+        if vace_context is None and (vace_video is not None or vace_video_mask is not None):
+            vace_context = self.encode_vace(vace_video, vace_video_mask, height, width, num_frames, tiled,
+                                            tile_size, tile_stride)
+        latents = self.denoise(noise, prompt_emb.to(self.device), None if negative_prompt_emb is None else
+                               negative_prompt_emb.to(self.device),
+                               None if vace_context is None else vace_context.to(self.device), vace_scale,
+                               cfg_scale, num_inference_steps, sigma_shift, denoising_strength, progress_bar_cmd)
+        if output_type == "latents":
+            return latents
+        if self.vae is None:
+            raise NotImplementedError("VAE decode requires a loaded Wan2.1 VAE (not available in this build)")
+        video = self.vae.decode(latents, device=self.device, tiled=tiled, tile_size=tile_size, tile_stride=tile_stride)
+        return self.vae_output_to_video(video)
+
+    def encode_prompt(self, prompt):
+        if self.text_encoder is None or self.prompter is None:
+            raise NotImplementedError("T5 text encoder not loaded: pass prompt_emb=/negative_prompt_emb=")
+        return self.prompter.encode_prompt(prompt, device=self.device)
+
+    def encode_vace(self, vace_video, vace_video_mask, height, width, num_frames, tiled, tile_size, tile_stride):
+        if self.vae is None:
+            raise NotImplementedError("VACE video encoding requires the Wan2.1 VAE: pass vace_context=")
+        raise NotImplementedError("VAE encode path not built yet")
+
+    def vae_output_to_video(self, vae_output):
+        raise NotImplementedError("VAE output conversion not built yet")
