@@ -1,0 +1,221 @@
+"""Headline benchmark: denoising steps/s of Wan2.1-VACE-14B at 832x480x73 on MI355X.
+
+One step = the reference's CFG denoising step (wan_video_new.py:518-542): DiT(40 blocks) + VACE
+(8 blocks) forward for the positive AND negative prompt (run as one batch-2 forward), CFG combine
+and the Euler update.  Synthetic data: random-init weights (N(0,0.02), seed 5), seeded latents /
+contexts / VACE context of the real shapes (no checkpoints or datasets are reachable offline).
+
+  python bench.py [--gpus N --steps K --warmup W]        (N>1: torchrun, Ulysses SP over RCCL)
+
+Prints one JSON line with `roofline` (self-attention kernel, HIP-event timed inside the timed
+region) and, on rank 0 at N=1, `cpu_baseline` (the CPU oracle on a bounded token sample).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "video-styler_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+MODELS = {
+    "14B": dict(dim=5120, ffn_dim=13824, num_heads=40, num_layers=40, vace_layers=tuple(range(0, 40, 5))),
+    "1.3B": dict(dim=1536, ffn_dim=8960, num_heads=12, num_layers=30, vace_layers=tuple(range(0, 30, 2))),
+}
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def step_flops(m, S, L=512, B=2):
+    """Algorithmic FLOPs of one CFG step (SURVEY.md §8d / BASELINE.md §2)."""
+    D, F, nm, nv = m["dim"], m["ffn_dim"], m["num_layers"], len(m["vace_layers"])
+    blk = 12 * S * D * D + 4 * S * D * F + 4 * S * S * D + 4 * L * D * D + 4 * S * L * D
+    fwd = (nm + nv) * blk + (nv + 1) * 2 * S * D * D + 2 * S * D * (64 + 384 + 64) + 2 * L * D * (4096 + D)
+    return B * fwd
+
+
+def cpu_baseline(m, S, rows=1024, repeats=2):
+    """Oracle (PyTorch-CPU restatement) on a bounded sample: one DiT block's per-token work for
+    `rows` query tokens (their projections, norms, RoPE, attention against the full S-token K/V,
+    cross-attention, FFN), extrapolated x S/rows x (main+VACE blocks) x 2 (CFG)."""
+    from oracle import wan_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    torch.set_num_threads(threads)
+    D, F, H = m["dim"], m["ffn_dim"], m["num_heads"]
+    g = torch.Generator().manual_seed(0)
+    bf = torch.bfloat16
+
+    def w(*s):
+        return (0.02 * torch.randn(*s, generator=g)).to(bf)
+    Wb = {}
+    for a in ("self_attn.", "cross_attn."):
+        for l in "qkvo":
+            Wb[a + l + ".weight"], Wb[a + l + ".bias"] = w(D, D), w(D)
+        Wb[a + "norm_q.weight"], Wb[a + "norm_k.weight"] = 1 + w(D), 1 + w(D)
+    Wb["norm3.weight"], Wb["norm3.bias"] = 1 + w(D), w(D)
+    Wb["ffn.0.weight"], Wb["ffn.0.bias"], Wb["ffn.2.weight"], Wb["ffn.2.bias"] = w(F, D), w(F), w(D, F), w(D)
+    Wb["modulation"] = w(1, 6, D)
+    x = torch.randn(1, rows, D, generator=g).to(bf)
+    kfull = torch.randn(1, S, D, generator=g).to(bf)
+    vfull = torch.randn(1, S, D, generator=g).to(bf)
+    ctx = torch.randn(1, 512, D, generator=g).to(bf)
+    t_mod = w(1, 6, D)
+    freqs = O.rope_freqs(1, 1, rows)
+
+    def one():
+        mod = O.bf(Wb["modulation"].float() + t_mod.float())
+        sh, sc, ga, sh2, sc2, ga2 = mod.chunk(6, dim=1)
+        h = O.modulate(O.layer_norm(x), sh, sc)
+        q = O.rope_apply(O.rms_norm(O.linear(h, Wb["self_attn.q.weight"], Wb["self_attn.q.bias"]),
+                                    Wb["self_attn.norm_q.weight"]), freqs, H)
+        k = O.rope_apply(O.rms_norm(O.linear(h, Wb["self_attn.k.weight"], Wb["self_attn.k.bias"]),
+                                    Wb["self_attn.norm_k.weight"]), freqs, H)
+        v = O.linear(h, Wb["self_attn.v.weight"], Wb["self_attn.v.bias"])
+        kk = torch.cat([k, kfull[:, rows:]], 1)
+        vv = torch.cat([v, vfull[:, rows:]], 1)
+        o = O.attention(q, kk, vv, H)
+        y = O.gate_residual(x, ga, O.linear(o, Wb["self_attn.o.weight"], Wb["self_attn.o.bias"]))
+        y = O.add(y, O.cross_attention(O.layer_norm(y, 1e-6, Wb["norm3.weight"], Wb["norm3.bias"]), ctx, Wb,
+                                       "cross_attn.", H))
+        f = O.linear(O.gelu_tanh(O.linear(O.modulate(O.layer_norm(y), sh2, sc2), Wb["ffn.0.weight"],
+                                          Wb["ffn.0.bias"])), Wb["ffn.2.weight"], Wb["ffn.2.bias"])
+        return O.gate_residual(y, ga2, f)
+
+    one()
+    best = float("inf")
+    for _ in range(repeats):
+        t0 = time.perf_counter()
+        one()
+        best = min(best, time.perf_counter() - t0)
+    blocks = m["num_layers"] + len(m["vace_layers"])
+    sec_per_step = best * (S / rows) * blocks * 2
+    return {"value": 1.0 / sec_per_step, "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle DiT block, {rows} of {S} query tokens vs full {S}-token K/V, best of {repeats} "
+                      f"({best:.2f}s), extrapolated x{S}/{rows} tokens x{blocks} blocks x2 CFG "
+                      f"= {sec_per_step:.0f} s/step"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="14B", choices=list(MODELS))
+    ap.add_argument("--frames", type=int, default=73)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--width", type=int, default=832)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=1024)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        from vstyler.usp import init_distributed, get_default_group
+        local = init_distributed()
+        dev = torch.device(f"cuda:{local}")
+        sp = get_default_group()
+    else:
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        sp = None
+
+    from vstyler import model_fn_wan_video
+    from vstyler import kernels as K
+    from vstyler.flow_match import FlowMatchScheduler
+    from vstyler.models import TIMER, VaceWanModel, WanModel, init_random_
+
+    m = MODELS[args.model]
+    T = (args.frames - 1) // 4 + 1
+    Hl, Wl = args.height // 8, args.width // 8
+    S = T * (Hl // 2) * (Wl // 2)
+    dit = WanModel(dim=m["dim"], in_dim=16, ffn_dim=m["ffn_dim"], out_dim=16, text_dim=4096, freq_dim=256, eps=1e-6,
+                   patch_size=(1, 2, 2), num_heads=m["num_heads"], num_layers=m["num_layers"], device=dev)
+    vace = VaceWanModel(vace_layers=m["vace_layers"], dim=m["dim"], num_heads=m["num_heads"], ffn_dim=m["ffn_dim"],
+                        device=dev)
+    init_random_(dit, seed=5)
+    init_random_(vace, seed=6)
+
+    g = torch.Generator().manual_seed(1)
+    latents = torch.randn(1, 16, T, Hl, Wl, generator=g).to(torch.bfloat16).to(dev)
+    ctx = (0.1 * torch.randn(2, 512, 4096, generator=g))
+    ctx[0, 32:] = 0
+    ctx[1, 96:] = 0
+    ctx = ctx.to(torch.bfloat16).to(dev)
+    vc = torch.ones(1, 96, T, Hl, Wl)
+    vc[:, :32] = torch.randn(1, 32, T, Hl, Wl, generator=g)
+    vc = vc.to(torch.bfloat16).to(dev)
+    sched = FlowMatchScheduler(shift=5, sigma_min=0.0, extra_one_step=True)
+    n_total = args.warmup + args.steps
+    sched.set_timesteps(max(n_total, 2), shift=5.0)
+
+    def step(i):
+        t = sched.timesteps[i].reshape(1).to(torch.bfloat16).to(dev)
+        v = model_fn_wan_video(dit, vace=vace, latents=latents, timestep=t, context=ctx, vace_context=vc,
+                               use_unified_sequence_parallel=sp is not None, sp_group=sp)
+        K.cfg_euler(v[0:1].contiguous(), v[1:2].contiguous(), latents, 5.0, sched.delta(i))
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    TIMER.reset()
+    TIMER.enabled = True
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, n_total):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    TIMER.enabled = False
+    attn_ms, attn_n = TIMER.mean_ms("self_attn")
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = tt.item()
+
+    ms_per_step = 1000 * elapsed / args.steps
+    value = args.steps / elapsed
+    fl_step = step_flops(m, S)
+    # self-attention launch: 4*S_q*S_kv*d per head, B=2 (CFG); under SP a rank runs H/p heads
+    attn_flops = 4.0 * S * S * m["dim"] * 2 / world
+    achieved = attn_flops / (attn_ms / 1000) / 1e12
+    out = {
+        "metric": "denoising steps/sec, Wan2.1-VACE-14B 832x480x73" if args.model == "14B" else
+                  f"denoising steps/sec, Wan2.1-VACE-{args.model} {args.width}x{args.height}x{args.frames}",
+        "value": round(value, 5), "unit": "steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (random-init weights, seeded latents/contexts/VACE context)",
+        "config": {"workload": f"Wan2.1-VACE-{args.model} {args.width}x{args.height}x{args.frames}: "
+                               f"{m['num_layers']} DiT + {len(m['vace_layers'])} VACE blocks, CFG 5.0 as one "
+                               f"batch-2 forward + Euler",
+                   "model": f"Wan2.1-VACE-{args.model}", "global_batch": 1, "seq_len": S,
+                   "latent_shape": [1, 16, T, Hl, Wl], "parallelism": f"sp{world}" if world > 1 else "single",
+                   "lora": "merged (zero runtime cost, as the reference's GeneralLoRALoader)"},
+        "model_tflops_per_step": round(fl_step / 1e12, 1),
+        "mfu_bf16": round(fl_step * value / world / 1e12 / PEAK_BF16_TFLOPS, 4),
+        "roofline": {"kernel": "attn_fwd_d128 (self-attention)", "bound": "mfma",
+                     "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "avg_launch_ms": round(attn_ms, 3), "launches": attn_n,
+                     "flops_per_launch": attn_flops},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(m, S, rows=args.cpu_rows)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -116,6 +116,40 @@ class Workspace:
         return t
 
 
+class KernelTimer:
+    """Optional HIP-event bracketing of chosen launches (bench.py roofline): events are recorded on
+    the stream the kernel is launched on (torch's current stream), elapsed times read afterwards."""
+
+    def __init__(self):
+        self.enabled = False
+        self.events = {}
+
+    def start(self, name):
+        if not self.enabled:
+            return None
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        self.events.setdefault(name, []).append((e0, e1))
+        return e1
+
+    def stop(self, e1):
+        if e1 is not None:
+            e1.record()
+
+    def mean_ms(self, name):
+        ev = self.events.get(name, [])
+        if not ev:
+            return None
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in ev) / len(ev), len(ev)
+
+    def reset(self):
+        self.events = {}
+
+
+TIMER = KernelTimer()
+
+
 class RunCtx:
     """Per-forward constants shared by all blocks: batch/token geometry, RoPE table, SP info."""
 
@@ -160,7 +194,9 @@ class DiTBlock(nn.Module):
         if rc.sp is not None:
             rc.sp.attention(q, k, v, o, self.num_heads, B)
         else:
+            ev = TIMER.start("self_attn")
             K.attention(q, k, v, o, self.num_heads, B)
+            TIMER.stop(ev)
         linear(sa.o, o, x, ws, epilogue=K.VS_EPI_GATE_RES, residual=x, gate=g_msa,
                gate_bstride=6 * D, rows_per_batch=S)
         # --- cross-attention (wan_video_dit.py:227, :171-186)

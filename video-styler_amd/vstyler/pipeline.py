@@ -107,6 +107,12 @@ class ModelConfig:
     skip_download: bool = False
 
     def download_if_necessary(self, use_usp=False):
+        if isinstance(self.path, str) and any(ch in self.path for ch in "*?["):
+            import glob
+            files = sorted(glob.glob(self.path))
+            if not files:
+                raise FileNotFoundError(f"no local files match {self.path}")
+            self.path = files[0] if len(files) == 1 else files
         if self.path is not None:
             return
         if self.model_id is None:

@@ -110,7 +110,10 @@ class UlyssesGroup:
         for i in range(3):
             self._permute(recv[i * chunk:], full[i], B, Sl, cpr, D, 3 * chunk, 2)
         of = ws_.get("sp_out_full", (B * P * Sl, cpr))
+        from .models import TIMER
+        ev = TIMER.start("self_attn")
         K.attention(full[0], full[1], full[2], of, Hp, B)
+        TIMER.stop(ev)
         send2 = ws_.get("sp_send2", (P * chunk,))
         recv2 = ws_.get("sp_recv2", (P * chunk,))
         self._permute(of, send2, B, Sl, cpr, D, chunk, 3)
