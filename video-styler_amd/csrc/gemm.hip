@@ -8,6 +8,10 @@
 // (cross-attn, VACE before_proj), VACE hint add (wan_video_new.py:1450), LoRA merge
 // (lora/__init__.py:40-43) and the un-merged LoRA term (layers.py:180-182) as a second K phase.
 //
+// Two schedules share the epilogue:
+//  * gemm_bf16_tn_256 (large M*N, K >= 4096): 256x256 tile, 8 waves in a ping-pong pair per SIMD
+//    (see its header) -- the DiT projections and FFN;
+//  * gemm_bf16_tn (everything else): the structure described below.
 // Structure: 128x128x64 tile, 4 waves (2x2, 64x64 each), v_mfma_f32_16x16x32_bf16 computing the
 // transposed tile (W rows as the A operand) so every lane owns 4 consecutive output columns;
 // both operands are K-contiguous ([rows][K]) and staged by global_load_lds_dwordx4 (LDS-DMA,
@@ -15,6 +19,7 @@
 // (chunk ^ (row & 7)) applied on the global SOURCE address, which makes the fragment
 // ds_read_b128 conflict free; grouped (8 m-tiles) + XCD-aware tile order for L2 reuse.
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -44,6 +49,44 @@ __device__ __forceinline__ void load4(const bf16_t* p, float* v) {
     v[1] = bfhi(w[0]);
     v[2] = bflo(w[1]);
     v[3] = bfhi(w[1]);
+}
+
+__device__ __forceinline__ void epilogue_store(const f32x4_t& a, int m, int n, bf16_t* C, long long ldc,
+                                               const Epi& ep) {
+    const int bidx = m / ep.rows_per_batch;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (ep.bias) load4(ep.bias + n, bv);
+    float y[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = rbf(a[e] + bv[e]);
+    if (ep.mode == VS_EPI_GELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = gelu_tanh_f(y[e]);
+    } else if (ep.mode == VS_EPI_SILU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = silu_f(y[e]);
+    } else if (ep.mode == VS_EPI_GATE_RES) {
+        float rv[4], gv[4];
+        load4(ep.res + (long long)m * ep.ld_res + n, rv);
+        load4(ep.gate + (long long)bidx * ep.gate_bstride + n, gv);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = rbf(rv[e] + rbf(gv[e] * y[e]));
+        if (ep.hint) {
+            float hv[4];
+            load4(ep.hint + (long long)m * ep.ld_hint + n, hv);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) y[e] = y[e] + rbf(hv[e] * ep.hint_scale);
+        }
+    } else if (ep.mode == VS_EPI_RES) {
+        float rv[4];
+        load4(ep.res + (long long)m * ep.ld_res + n, rv);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = rv[e] + rbf(ep.alpha * y[e]);
+    }
+    u32x2_t w;
+    w[0] = pack2(y[0], y[1]);
+    w[1] = pack2(y[2], y[3]);
+    *reinterpret_cast<u32x2_t*>(C + (long long)m * ldc + n) = w;
 }
 
 __global__ __launch_bounds__(NTHR, 2) void gemm_bf16_tn(
@@ -140,44 +183,155 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_bf16_tn(
     for (int i = 0; i < 4; ++i) {
         const int m = m0 + wm * 64 + i * 16 + (lane & 15);
         if (m >= M) continue;
-        const int bidx = m / ep.rows_per_batch;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
             if (n >= N) continue;
-            float bv[4] = {0.f, 0.f, 0.f, 0.f};
-            if (ep.bias) load4(ep.bias + n, bv);
-            float y[4];
+            epilogue_store(acc[i][j], m, n, C, ldc, ep);
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// 256x256 tile, 8 waves, ping-pong schedule.  K is consumed in 32-wide half-steps through a
+// 4-slot LDS ring (4 x 32 KB, LDS-DMA filled three half-steps ahead).  Waves 0-3 (rows 0-127)
+// and waves 4-7 (rows 128-255) share SIMDs pairwise (w, w+4) and run one barrier-phase apart:
+// in every phase one wave of each SIMD executes its 32 MFMAs (setprio 1) while its partner reads
+// the next fragments from LDS and issues its LDS-DMA, so the matrix pipe alternates between the
+// two waves instead of idling at every barrier.  Counted vmcnt (never 0 in the main loop), raw
+// s_barrier.  64-B LDS rows, 16-B chunk swizzle c ^ ((3*(row>>2)) & 3) (conflict-free 16x16x32
+// fragment reads).
+// ---------------------------------------------------------------------------------------------
+constexpr int BT = 256, HK = 32, NTHR8 = 512, SLOT = 2 * BT * HK * 2;   // 32 KB per slot
+
+__device__ __forceinline__ int h_off(int row, int ch) {
+    return row * 64 + 16 * (ch ^ ((3 * (row >> 2)) & 3));
+}
+
+__device__ __forceinline__ void wait_barrier(int n_after) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (n_after >= 2)
+        asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (n_after == 1)
+        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+__global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
+    const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
+    bf16_t* C, long long ldc, int M, int N, int K, const bf16_t* __restrict__ A2, long long lda2,
+    const bf16_t* __restrict__ W2, long long ldw2, int K2, Epi ep, int ntm, int ntn) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int pid = xcd_remap(blockIdx.x, gridDim.x);
+    constexpr int GM = 4;
+    const int per_group = GM * ntn;
+    const int group = pid / per_group;
+    const int first_m = group * GM;
+    const int gsz = min(ntm - first_m, GM);
+    const int in_g = pid % per_group;
+    const int tm = first_m + in_g % gsz;
+    const int tn = in_g / gsz;
+    const int m0 = tm * BT, n0 = tn * BT;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;      // wm = ping-pong group
+
+    f32x4_t acc[8][4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) y[e] = rbf(acc[i][j][e] + bv[e]);
-            if (ep.mode == VS_EPI_GELU) {
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) y[e] = gelu_tanh_f(y[e]);
-            } else if (ep.mode == VS_EPI_SILU) {
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    // LDS-DMA: piece p (1 KB) = 16 rows x 64 B; lane L -> row 16p + L/4, physical chunk L%4,
+    // logical chunk (L%4) ^ ((3*((L/4)>>2))&3).  Per half-step 32 pieces (16 A, 16 W):
+    // wave w issues pieces 4w..4w+3 (waves 0-3: A, waves 4-7: W).
+    const int prow = lane >> 2;
+    const int pch = (lane & 3) ^ ((3 * (prow >> 2)) & 3);
+    const int nh1 = K / HK;
+    const int nh = nh1 + K2 / HK;
+    // operand this wave streams (group 0: activations A/A2 rows m0.., group 1: weights W/W2 rows n0..)
+    const bf16_t* Pm = wm == 0 ? A : W;
+    const bf16_t* Pl = wm == 0 ? A2 : W2;
+    const long long ldm = wm == 0 ? lda : ldw;
+    const long long ldl = wm == 0 ? lda2 : ldw2;
+    const int lim = (wm == 0 ? M : N) - 1;
+    const int r0 = wm == 0 ? m0 : n0;
+    const int dst_off = wm * (BT * 64) + wn * 4 * 1024;
+    const int rbase = r0 + wn * 64 + prow;
+    int issued = -1;                                // highest half-step this wave has issued
+    auto issue = [&](int h) {
+        char* dst = smem + (h & 3) * SLOT + dst_off;
+        const bool lora = h >= nh1;
+        const bf16_t* P = (lora ? Pl : Pm) + (lora ? h - nh1 : h) * HK + pch * 8;
+        const long long ld = lora ? ldl : ldm;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) y[e] = silu_f(y[e]);
-            } else if (ep.mode == VS_EPI_GATE_RES) {
-                float rv[4], gv[4];
-                load4(ep.res + (long long)m * ep.ld_res + n, rv);
-                load4(ep.gate + (long long)bidx * ep.gate_bstride + n, gv);
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_global_load_lds((const GLB_AS void*)(P + (long long)min(rbase + j * 16, lim) * ld),
+                                             (LDS_AS void*)(dst + j * 1024), 16, 0, 0);
+        issued = h;
+    };
+
+    const int frow = lane & 15, fch = lane >> 4;
+    bf16x8_t wf[4], af[8];
+    auto load_frags = [&](int h) {
+        const char* As = smem + (h & 3) * SLOT;
+        const char* Bs = As + BT * 64;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) y[e] = rbf(rv[e] + rbf(gv[e] * y[e]));
-                if (ep.hint) {
-                    float hv[4];
-                    load4(ep.hint + (long long)m * ep.ld_hint + n, hv);
+        for (int j = 0; j < 4; ++j)
+            wf[j] = *reinterpret_cast<const bf16x8_t*>(Bs + h_off(wn * 64 + j * 16 + frow, fch));
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) y[e] = y[e] + rbf(hv[e] * ep.hint_scale);
-                }
-            } else if (ep.mode == VS_EPI_RES) {
-                float rv[4];
-                load4(ep.res + (long long)m * ep.ld_res + n, rv);
+        for (int i = 0; i < 8; ++i)
+            af[i] = *reinterpret_cast<const bf16x8_t*>(As + h_off(wm * 128 + i * 16 + frow, fch));
+    };
+    auto mfmas = [&]() {
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) y[e] = rv[e] + rbf(ep.alpha * y[e]);
-            }
-            u32x2_t w;
-            w[0] = pack2(y[0], y[1]);
-            w[1] = pack2(y[2], y[3]);
-            *reinterpret_cast<u32x2_t*>(C + (long long)m * ldc + n) = w;
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], af[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+
+    // prologue: half-steps 0..2 in flight, then wait for half-step 0
+    issue(0);
+    if (nh > 1) issue(1);
+    if (nh > 2) issue(2);
+    wait_barrier(issued);                           // needed = 0
+    // Every wave runs the same body [L(h); barrier; C(h); barrier]; group 1 executes one extra
+    // barrier first, so its L phases coincide with group 0's C phases (s_barrier counts arrivals,
+    // not code positions) and group 0 balances the count at the end.  Global phase q = barriers
+    // passed since the prologue; the barrier into phase q+1 needs half-step (q+1)/2 on every wave.
+    int q = 0;
+    auto bar = [&]() {
+        wait_barrier(issued - min((q + 1) >> 1, nh - 1));
+        ++q;
+    };
+    if (wm == 1) bar();
+#pragma nounroll
+    for (int h = 0; h < nh; ++h) {
+        load_frags(h);
+        if (h + 3 < nh) issue(h + 3);
+        bar();
+        mfmas();
+        bar();
+    }
+    if (wm == 0) bar();
+
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+            if (n >= N) continue;
+            epilogue_store(acc[i][j], m, n, C, ldc, ep);
         }
     }
 }
@@ -221,6 +375,30 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
         return VS_E_INVALID;
     if (epilogue == VS_EPI_GATE_RES && !ep.gate) return VS_E_INVALID;
     if (ep.hint && ep.ld_hint < n) return VS_E_INVALID;
+    // 256x256 schedule once there are enough tiles to fill the chip, 128x128 otherwise
+    // (VSTYLER_GEMM_TILE=128|256 forces one for A/B measurements)
+    static int force = -1;
+    if (force < 0) {
+        const char* e = getenv("VSTYLER_GEMM_TILE");
+        force = e ? atoi(e) : 0;
+    }
+    const bool big = force ? force == 256
+                          : k >= 4096 && (long long)((m + BT - 1) / BT) * ((n + BT - 1) / BT) >= 240;
+    if (big) {
+        const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
+        static bool attr256 = false;
+        if (!attr256) {
+            (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_256,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 4 * SLOT);
+            attr256 = true;
+        }
+        hipLaunchKernelGGL(gemm_bf16_tn_256, dim3((unsigned)(tm * tn)), dim3(NTHR8), 4 * SLOT,
+                           (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw,
+                           (bf16_t*)c, ldc, m, n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2,
+                           k2, ep, tm, tn);
+        VS_CHECK_LAUNCH();
+        return VS_OK;
+    }
     const int ntm = (m + BM - 1) / BM, ntn = (n + BN - 1) / BN;
     const long long nwg = (long long)ntm * ntn;
     if (nwg > 0x7fffffff) return VS_E_INVALID;

@@ -49,6 +49,12 @@ class UlyssesGroup:
     def _permute(self, src, dst, batch, s_local, cpr, ld_local, jstride, mode):
         K.ulysses_permute(src, dst, batch, s_local, self.world_size, cpr, ld_local, jstride, mode)
 
+    def _attention(self, q, k, v, o, heads, batch):
+        from .models import TIMER
+        ev = TIMER.start("self_attn")
+        K.attention(q, k, v, o, heads, batch)
+        TIMER.stop(ev)
+
     def _all_to_all(self, recv, send):
         dist.all_to_all_single(recv, send, group=self.group)
 
@@ -110,10 +116,7 @@ class UlyssesGroup:
         for i in range(3):
             self._permute(recv[i * chunk:], full[i], B, Sl, cpr, D, 3 * chunk, 2)
         of = ws_.get("sp_out_full", (B * P * Sl, cpr))
-        from .models import TIMER
-        ev = TIMER.start("self_attn")
-        K.attention(full[0], full[1], full[2], of, Hp, B)
-        TIMER.stop(ev)
+        self._attention(full[0], full[1], full[2], of, Hp, B)
         send2 = ws_.get("sp_send2", (P * chunk,))
         recv2 = ws_.get("sp_recv2", (P * chunk,))
         self._permute(of, send2, B, Sl, cpr, D, chunk, 3)
