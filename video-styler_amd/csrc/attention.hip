@@ -27,10 +27,18 @@ constexpr int HD = 128;          // head dim
 constexpr int BQ = 256;          // query rows per workgroup
 constexpr int BKV = 64;          // keys per tile
 constexpr int NTHR = 512;
-constexpr int TILE = BKV * HD * 2;  // 16 KB per K (or V) tile
+constexpr int KROW = 272;        // LDS row pitch of the K tile (256 B + 16): row reads conflict-free
+constexpr int VROW = 320;        // LDS row pitch of the V tile (256 B + 64): transposed reads conflict-free
+constexpr int KT = BKV * KROW;   // 17408
+constexpr int VT = BKV * VROW;   // 20480
+constexpr int LDS_BYTES = 2 * (KT + VT);   // K ring 2 x 17408 + V ring 2 x 20480
+constexpr float RESCALE_THR = 8.0f;   // lazy rescale (exp2 domain): skip while the max grows <= 2^8
 
-__device__ __forceinline__ int lds_off(int row, int ch) {
-    return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+    // raw buffer descriptor; out-of-range loads return 0 (rows past Skv, masked anyway)
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
 }
 
 __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
@@ -43,7 +51,8 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     const int qb = g % nqb;
     const int bh = g / nqb;
     const int h = bh % H, b = bh / H;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, hh = lane >> 5;
     const int q0 = qb * BQ + wave * 32;
 
@@ -67,49 +76,62 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
         for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
     float m = -1e30f, l = 0.f;
 
-    // register staging: thread owns chunks tid and tid+512 (row = ci>>4, 16-B chunk = ci&15)
-    u32x4_t kst[2], vst[2];
-    auto load_tile = [&](int kv0) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int ci = tid + NTHR * j, row = ci >> 4, ch = ci & 15;
-            const long long kr = min(kv0 + row, Skv - 1);
-            kst[j] = *reinterpret_cast<const u32x4_t*>(Kb + kr * ldk + ch * 8);
-            vst[j] = *reinterpret_cast<const u32x4_t*>(Vb + kr * ldv + ch * 8);
-        }
+    // buffer descriptors over this (batch, head)'s K/V rows; per-lane byte offset constant, the
+    // tile's row offset goes to the scalar soffset
+    const unsigned kbytes = (unsigned)min((long long)(Skv - 1) * ldk * 2 + HD * 2, 0xffffffffLL);
+    const unsigned vbytes = (unsigned)min((long long)(Skv - 1) * ldv * 2 + HD * 2, 0xffffffffLL);
+    const __amdgpu_buffer_rsrc_t krs = make_rsrc(Kb, kbytes), vrs = make_rsrc(Vb, vbytes);
+    const int srow = tid >> 4, sch = tid & 15;            // chunk tid -> row srow (and srow+32)
+    const unsigned kvo0 = (unsigned)(srow * ldk * 2 + sch * 16), kvo1 = kvo0 + (unsigned)(32 * ldk * 2);
+    const unsigned vvo0 = (unsigned)(srow * ldv * 2 + sch * 16), vvo1 = vvo0 + (unsigned)(32 * ldv * 2);
+    const int kw = srow * KROW + sch * 16, vw = srow * VROW + sch * 16;
+
+    // K ring (2 slots) runs one tile ahead of the V ring (2 slots): iteration i reads K(i+1)
+    // (for the next S^T) and V(i) (for this tile's PV), and stages K(i+2), V(i+1).
+    i32x4_t kst[2], vst[2];
+    auto load_k = [&](int kv0) {
+        const int ks = kv0 * (int)ldk * 2;
+        kst[0] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo0, ks, 0);
+        kst[1] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo1, ks, 0);
     };
-    auto store_tile = [&](int buf) {
-        char* kb = smem + buf * 2 * TILE;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int ci = tid + NTHR * j, row = ci >> 4, ch = ci & 15;
-            *reinterpret_cast<u32x4_t*>(kb + lds_off(row, ch)) = kst[j];
-            *reinterpret_cast<u32x4_t*>(kb + TILE + lds_off(row, ch)) = vst[j];
-        }
+    auto load_v = [&](int kv0) {
+        const int vs = kv0 * (int)ldv * 2;
+        vst[0] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo0, vs, 0);
+        vst[1] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo1, vs, 0);
+    };
+    auto store_k = [&](int slot) {
+        char* base = smem + slot * KT;
+        *reinterpret_cast<i32x4_t*>(base + kw) = kst[0];
+        *reinterpret_cast<i32x4_t*>(base + kw + 32 * KROW) = kst[1];
+    };
+    auto store_v = [&](int slot) {
+        char* base = smem + 2 * KT + slot * VT;
+        *reinterpret_cast<i32x4_t*>(base + vw) = vst[0];
+        *reinterpret_cast<i32x4_t*>(base + vw + 32 * VROW) = vst[1];
     };
 
-    // per-lane constants of the transposed V read (ds_read_b64_tr_b16): group g4 of 16 lanes,
-    // lane 4*q4+p4 of the group addresses row q4 / columns 4*p4.. of a 4 x 16 block.
+    // per-lane LDS read bases (everything else is an immediate offset)
+    const int krd = r * KROW + 16 * hh;                   // + t*32*KROW + 32*ss
     const int g4 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-    const int vrow = 4 * (g4 >> 1) + q4;
-    const int vch = 2 * (g4 & 1) + (p4 >> 1);
-    const int vbyte = 8 * (p4 & 1);
+    const int vrd = (4 * (g4 >> 1) + q4) * VROW + 32 * (g4 & 1) + 8 * p4;   // + ks*16*VROW + 64*dt (+8 rows)
 
-    auto compute = [&](int buf, int kv0, bool mask) {
-        const char* kb = smem + buf * 2 * TILE;
-        const char* vb = kb + TILE;
-        f32x16_t s[2];
+    auto qk = [&](int slot, f32x16_t* s) {
+        const char* base = smem + slot * KT;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) s[t][i] = 0.f;
-            const int row = 32 * t + r;
 #pragma unroll
             for (int ss = 0; ss < 8; ++ss) {
-                const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kb + lds_off(row, 2 * ss + hh));
+                const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(base + krd + t * 32 * KROW + 32 * ss);
                 s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ss], s[t], 0, 0, 0);
             }
         }
+    };
+    // online softmax in the exp2 domain (c = scale*log2 e) with a lazy rescale: the reference max
+    // m only moves when some row's max exceeds it by more than RESCALE_THR, so P <= 2^THR.
+    // Runs after the previous tile's PV has been issued and before this tile's PV (T13 order).
+    auto softmax = [&](f32x16_t* s, int kv0, bool mask) {
         if (mask) {
 #pragma unroll
             for (int t = 0; t < 2; ++t)
@@ -119,46 +141,47 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
                     if (key >= Skv) s[t][i] = -INFINITY;
                 }
         }
-        // online softmax (scores scaled into the exp2 domain by c = scale*log2(e))
         float mx = s[0][0];
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[t][i]);
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
-        const float mnew = fmaxf(m, mx * c);
-        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-        m = mnew;
+        mx = fmaxf(mx, __shfl_xor(mx, 32)) * c;
+        if (__any(mx > m + RESCALE_THR)) {
+            const float mnew = fmaxf(m, mx);
+            const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+            m = mnew;
+            l *= alpha;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+        }
         float rs = 0.f;
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const float p = __builtin_amdgcn_exp2f(fmaf(s[t][i], c, -mnew));
+                const float p = __builtin_amdgcn_exp2f(fmaf(s[t][i], c, -m));
                 s[t][i] = p;
                 rs += p;
             }
-        l = l * alpha + rs;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
-
-        // O^T += V^T P over 4 k-steps of 16 keys
+        l += rs;
+    };
+    // O^T += V^T P over 4 k-steps of 16 keys
+    auto pv = [&](int slot, const f32x16_t* s) {
+        const char* base = smem + 2 * KT + slot * VT;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
             const int t = ks >> 1, u = ks & 1;
             bf16x8_t pf;
 #pragma unroll
             for (int j = 0; j < 8; ++j) pf[j] = (__bf16)s[t][8 * u + j];
-            const int row0 = 16 * ks + vrow;
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt) {
-                const int ch = 4 * dt + vch;
-                const i16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (LDS_AS i16x4_t*)(vb + lds_off(row0, ch) + vbyte));
-                const i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (LDS_AS i16x4_t*)(vb + lds_off(row0 + 8, ch) + vbyte));
+                const char* a0 = base + vrd + ks * 16 * VROW + 64 * dt;
+                const i16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_t*)(a0));
+                const i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_t*)(a0 + 8 * VROW));
                 const bf16x8_t vf = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, v0),
                                                             __builtin_bit_cast(bf16x4_t, v1), 0, 1, 2, 3,
                                                             4, 5, 6, 7);
@@ -168,16 +191,37 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     };
 
     const int nkv = (Skv + BKV - 1) / BKV;
-    load_tile(0);
-    store_tile(0);
-    __syncthreads();
-    for (int it = 0; it < nkv; ++it) {
-        const bool has_next = it + 1 < nkv;
-        if (has_next) load_tile((it + 1) * BKV);
-        compute(it & 1, it * BKV, (it + 1) * BKV > Skv);
-        if (has_next) store_tile((it + 1) & 1);
-        __syncthreads();
+    // prologue: K(0), K(1), V(0) in LDS; S(0) computed
+    load_k(0);
+    load_v(0);
+    store_k(0);
+    store_v(0);
+    if (nkv > 1) {
+        load_k(BKV);
+        store_k(1);
     }
+    __syncthreads();
+    f32x16_t sa[2], sb[2];
+    qk(0, sa);
+    __syncthreads();      // every wave has read K slot 0 before iteration 0 restages it with K(2)
+    // two named S states (no runtime-indexed register arrays): iterations alternate sa/sb
+    auto body = [&](int it, f32x16_t* cur, f32x16_t* nxt) {
+        const bool has1 = it + 1 < nkv, has2 = it + 2 < nkv;
+        if (has2) load_k((it + 2) * BKV);
+        if (has1) load_v((it + 1) * BKV);
+        if (has1) qk((it + 1) & 1, nxt);                // MFMAs independent of this softmax
+        softmax(cur, it * BKV, (it + 1) * BKV > Skv);
+        pv(it & 1, cur);
+        if (has2) store_k(it & 1);                      // K(it) slot is free
+        if (has1) store_v((it + 1) & 1);                // V(it-1) slot is free
+        __syncthreads();
+    };
+    int it = 0;
+    for (; it + 1 < nkv; it += 2) {
+        body(it, sa, sb);
+        body(it + 1, sb, sa);
+    }
+    if (it < nkv) body(it, sa, sb);
 
     const float lt = l + __shfl_xor(l, 32);
     const float inv = 1.f / lt;
@@ -211,17 +255,19 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
         return VS_E_INVALID;
     if ((ldq | ldk | ldv | ldo | bsq | bsk | bsv | bso) & 7) return VS_E_INVALID;
     if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o)) return VS_E_INVALID;
+    // buffer addressing: one (batch, head) K/V slab and a tile's row offset must fit 32 bits
+    if ((long long)skv * ldk * 2 >= (1LL << 31) || (long long)skv * ldv * 2 >= (1LL << 31)) return VS_E_UNSUPPORTED;
     const int nqb = (sq + BQ - 1) / BQ;
     const long long nwg = (long long)nqb * heads * batch;
     if (nwg > 0x7fffffff) return VS_E_INVALID;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)attn_fwd_d128, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            4 * TILE);
+                            LDS_BYTES);
         attr_set = true;
     }
     const float c = scale * 1.4426950408889634f;
-    hipLaunchKernelGGL(attn_fwd_d128, dim3((unsigned)nwg), dim3(NTHR), 4 * TILE,
+    hipLaunchKernelGGL(attn_fwd_d128, dim3((unsigned)nwg), dim3(NTHR), LDS_BYTES,
                        (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                        (bf16_t*)o, sq, skv, heads, ldq, ldk, ldv, ldo, bsq, bsk, bsv, bso, c, nqb);
     VS_CHECK_LAUNCH();
