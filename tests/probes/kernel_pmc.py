@@ -1,0 +1,21 @@
+"""Runs one kernel a few times for PMC collection: attn (14B self-attention) or gemm (FFN up)."""
+import os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "video-styler_amd"))
+import torch
+from vstyler import kernels as K
+which = sys.argv[1]
+g = torch.Generator(device="cuda").manual_seed(0)
+if which == "attn":
+    B, S, H = 2, 29640, 40
+    q, k, v = (torch.randn(B * S, H * 128, device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
+    o = torch.empty_like(q)
+    fn = lambda: K.attention(q, k, v, o, H, B)
+else:
+    M, N, Kd = 59280, 13824, 5120
+    a = torch.randn(M, Kd, device="cuda", generator=g).to(torch.bfloat16)
+    w = (0.05 * torch.randn(N, Kd, device="cuda", generator=g)).to(torch.bfloat16)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    fn = lambda: K.gemm(a, w, out)
+for _ in range(3):
+    fn()
+torch.cuda.synchronize()

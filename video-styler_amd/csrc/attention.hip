@@ -115,16 +115,31 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     const int g4 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
     const int vrd = (4 * (g4 >> 1) + q4) * VROW + 32 * (g4 & 1) + 8 * p4;   // + ks*16*VROW + 64*dt (+8 rows)
 
+    // S^T for keys 0-31 (t=0) and 32-63 (t=1) as two interleaved accumulation chains; K fragments
+    // are read two d-steps ahead of their MFMAs so LDS latency hides under the chain.
     auto qk = [&](int slot, f32x16_t* s) {
-        const char* base = smem + slot * KT;
+        const char* base = smem + slot * KT + krd;
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int i = 0; i < 16; ++i) {
+            s[0][i] = 0.f;
+            s[1][i] = 0.f;
+        }
+        bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(base);
+        bf16x8_t kb = *reinterpret_cast<const bf16x8_t*>(base + 32 * KROW);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) s[t][i] = 0.f;
-#pragma unroll
-            for (int ss = 0; ss < 8; ++ss) {
-                const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(base + krd + t * 32 * KROW + 32 * ss);
-                s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ss], s[t], 0, 0, 0);
+        for (int ss = 0; ss < 8; ++ss) {
+            bf16x8_t na, nb;
+            if (ss + 1 < 8) {
+                na = *reinterpret_cast<const bf16x8_t*>(base + 32 * (ss + 1));
+                nb = *reinterpret_cast<const bf16x8_t*>(base + 32 * KROW + 32 * (ss + 1));
+            }
+            // keep the next fragments' LDS reads issued ahead of this step's MFMAs
+            __builtin_amdgcn_sched_barrier(0);
+            s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ss], s[0], 0, 0, 0);
+            s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[ss], s[1], 0, 0, 0);
+            if (ss + 1 < 8) {
+                ka = na;
+                kb = nb;
             }
         }
     };
@@ -133,6 +148,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     // Runs after the previous tile's PV has been issued and before this tile's PV (T13 order).
     auto softmax = [&](f32x16_t* s, int kv0, bool mask) {
         if (mask) {
+            asm volatile("");     // keep this a real (uniform) branch: never if-convert into every tile
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -191,7 +207,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     };
 
     const int nkv = (Skv + BKV - 1) / BKV;
-    // prologue: K(0), K(1), V(0) in LDS; S(0) computed
+    // prologue: K(0), K(1), V(0) in LDS; S(0) computed by every wave; K(2) in flight to registers
     load_k(0);
     load_v(0);
     store_k(0);
@@ -203,18 +219,38 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     __syncthreads();
     f32x16_t sa[2], sb[2];
     qk(0, sa);
-    __syncthreads();      // every wave has read K slot 0 before iteration 0 restages it with K(2)
-    // two named S states (no runtime-indexed register arrays): iterations alternate sa/sb
-    auto body = [&](int it, f32x16_t* cur, f32x16_t* nxt) {
-        const bool has1 = it + 1 < nkv, has2 = it + 2 < nkv;
-        if (has2) load_k((it + 2) * BKV);
-        if (has1) load_v((it + 1) * BKV);
-        if (has1) qk((it + 1) & 1, nxt);                // MFMAs independent of this softmax
-        softmax(cur, it * BKV, (it + 1) * BKV > Skv);
-        pv(it & 1, cur);
-        if (has2) store_k(it & 1);                      // K(it) slot is free
-        if (has1) store_v((it + 1) & 1);                // V(it-1) slot is free
+    if (nkv > 2) load_k(2 * BKV);
+    __syncthreads();      // every wave has read K slot 0 before it is restaged with K(2)
+
+    // Staggered two-phase loop.  Per tile i every wave runs
+    //   A_i: [load V(i+1)] QK(i+1) (MFMA) + softmax(i) (VALU) ; store K(i+2) -> K slot i&1
+    //   B_i: [load K(i+3)] PV(i) (MFMA)                      ; store V(i+1) -> V slot (i+1)&1
+    // with a barrier after each phase.  Waves 4-7 pass one extra barrier first, so on every SIMD
+    // one wave's softmax overlaps its partner's MFMAs.  Ring hazards (phase index of group 0 /
+    // group 1 = 2i / 2i+1 for A_i, 2i+1 / 2i+2 for B_i): K(i+2) is written in phases 2i..2i+1
+    // after its slot's last read (qk(i), phases 2i-2..2i-1) and before its first read (qk(i+2),
+    // phases 2i+2..2i+3); V(i+1) is written in 2i+1..2i+2, after pv(i-1) (2i-1..2i) and before
+    // pv(i+1) (2i+3..2i+4).
+    auto phase_bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
         __syncthreads();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    const int grp = wave >> 2;
+    if (grp == 1) phase_bar();
+    auto body = [&](int it, f32x16_t* cur, f32x16_t* nxt) {
+        const bool has1 = it + 1 < nkv, has2 = it + 2 < nkv, has3 = it + 3 < nkv;
+        // ---- phase A
+        if (has1) load_v((it + 1) * BKV);
+        if (has1) qk((it + 1) & 1, nxt);
+        softmax(cur, it * BKV, (it + 1) * BKV > Skv);
+        if (has2) store_k(it & 1);
+        phase_bar();
+        // ---- phase B
+        if (has3) load_k((it + 3) * BKV);
+        pv(it & 1, cur);
+        if (has1) store_v((it + 1) & 1);
+        phase_bar();
     };
     int it = 0;
     for (; it + 1 < nkv; it += 2) {
@@ -222,6 +258,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
         body(it + 1, sb, sa);
     }
     if (it < nkv) body(it, sa, sb);
+    if (grp == 0) phase_bar();
 
     const float lt = l + __shfl_xor(l, 32);
     const float inv = 1.f / lt;
