@@ -128,6 +128,84 @@ int vs_axpy(void* x, const void* y, float scale, long long n, void* stream);
 int vs_ulysses_permute(const void* src, void* dst, int batch, int s_local, int world,
                        int cols_per_rank, long long ld_local, long long jstride, int mode, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Causal 3-D VAE (diffsynth/models/wan_video_vae.py, Wan2.1 part).  Activations are channels-last
+ * "NTHWC" tiles: element (n, t, y, x, c) of a tensor lives at base + n*ns + ((t*H + y)*W + x)*ld + c.
+ * ------------------------------------------------------------------------------------------- */
+
+/* Implicit-GEMM convolution (MFMA), one call per CausalConv3d / Conv2d / 1x1 conv of the VAE:
+ *   y(z, n, t, yo, xo, co) = bf16(bias[co] + sum_{kt,ky,kx,ci} X(z, n, t*st+kt-pt, ...)*W[co][kt][ky][kx][ci])
+ * X is read as zero outside [t_lo, t_in) x [0, H) x [0, W) (causal time pad, spatial zero pad,
+ * ZeroPad2d), through a fused nearest-x2 spatial upsample when up2 (wan_video_vae.py:73-79,94,98).
+ * Output frame = t*t_mul + t_add (+1 for co >= split when split > 0: the channel->time interleave
+ * of Resample upsample3d, :153-156); res (same geometry as y) adds the ResidualBlock shortcut
+ * bf16(bf16(conv) + res) (:301).  out_f32 = 1 writes fp32 alpha*acc instead (attention scores).
+ * Also a batched plain GEMM (kt=kh=kw=1, t_in=h_in=1, w_in=rows) over nz slices with *_zs strides.
+ * Requires cin % 32 == 0, ldx/ldw % 8 == 0; weights are [cout][kt*kh*kw*cin] (ci fastest).
+ * Replaces CausalConv3d.forward (:33-52) and the nn.Conv2d of Resample / AttentionBlock. */
+typedef struct vs_conv3d {
+    const void* x; long long x_zs, x_ns, ldx;
+    int n, t_in, h_in, w_in, cin;
+    int kt, kh, kw, st, sh, sw, pt, ph, pw, up2, t_lo;
+    int t_out, h_out, w_out;
+    const void* w; long long w_zs, ldw;
+    const void* bias;           /* bf16 [cout] or NULL */
+    int cout;
+    void* y; long long y_zs, y_ns, ldy;
+    int t_mul, t_add, split, out_f32;
+    float alpha;
+    const void* res;            /* bf16, geometry of y, or NULL */
+    int nz;
+} vs_conv3d;
+int vs_vae_conv(const vs_conv3d* p, void* stream);
+
+/* RMS_norm over channels (F.normalize(x, dim=C) * sqrt(C) * gamma, wan_video_vae.py:55-70) with
+ * the bf16 rounding points of the reference, optionally followed by nn.SiLU (:276-278).
+ * x, y: npix rows of c channels (row strides ldx, ldy); c % 32 == 0. */
+int vs_vae_rmsnorm(const void* x, long long ldx, void* y, long long ldy, const void* gamma,
+                   long long npix, int c, int silu, void* stream);
+
+/* Row softmax of fp32 scores s[rows][ld_s] over the first ncols columns -> bf16 p[rows][ld_p],
+ * columns ncols..ld_p-1 written as 0 (AttentionBlock F.scaled_dot_product_attention, :331). */
+int vs_vae_softmax(const float* s, long long ld_s, void* p, long long ld_p, long long rows, int ncols,
+                   void* stream);
+
+/* vt[z][c][r] = v[z][r][c] for r < rows, 0 for rows <= r < ld_vt (V^T operand of P.V). */
+int vs_vae_transpose(const void* v, long long v_zs, long long ld_v, void* vt, long long vt_zs,
+                     long long ld_vt, int nz, int rows, int cols, void* stream);
+
+/* Tile cut of the first t frames of an NCTHW bf16 tensor src[C][t_src][H][W] into an NTHWC tile
+ * dst[t][th][tw][cpad]
+ * (channels >= C zero) with an optional per-channel affine (mode 0 none; 1: bf16(bf16(x-a)*b),
+ * the encode latent normalisation :1004-1005; 2: bf16(bf16(x/b)+a), the decode de-normalisation
+ * :1016-1017).  Replaces the video[:, :, :, h:h_, w:w_] slicing of tiled_encode/tiled_decode. */
+int vs_vae_tile_gather(const void* src, int c, int t_src, int h, int w, int t, int h0, int w0, int th,
+                       int tw, void* dst, int cpad, int mode, const void* a, const void* b, void* stream);
+
+/* One step of the tiled blend (wan_video_vae.py:1081-1101,1128-1149,1180-1201), in the reference's
+ * bf16 arithmetic and task order: values[c][t][h0+i][w0+j] += bf16(tile * mask), weight += mask,
+ * mask = bf16(min(ramp_h(i), ramp_w(j))) with linear ramps of widths bw_h/bw_w on the non-bound
+ * edges (bound = bit0 top, bit1 bottom, bit2 left, bit3 right).  tile is NTHWC [t][th][tw][ldc]
+ * (with the per-channel affine `mode` of vs_vae_tile_gather applied first); values is NCTHW
+ * [c][t][H][W], weight [t][H][W], both bf16. */
+int vs_vae_tile_blend(const void* tile, long long ldc, int c, int t, int th, int tw, void* values,
+                      void* weight, int h, int w, int h0, int w0, int bound, int bw_h, int bw_w,
+                      int mode, const void* a, const void* b, void* stream);
+
+/* out = bf16(values / weight) (weight broadcast over channels), clamped to [-1, 1] if clamp. */
+int vs_vae_blend_finish(const void* values, const void* weight, void* out, int c, long long plane,
+                        int clamp, void* stream);
+
+/* BasePipeline.vae_output_to_video (diffsynth/pipelines/wan_video_new.py:557 -> utils/__init__.py:76-91) for B = 1:
+ * video bf16 [3][t][h][w] in [-1, 1] -> out uint8 [t][h][w][3] = trunc(clip(bf16(bf16(x+1)*127.5))). */
+int vs_vae_to_u8(const void* video, void* out, int t, int h, int w, void* stream);
+
+/* Copy n frames of frame_elems elements (src/dst strides per n in elements): the pass-through
+ * first frame of Resample downsample3d/upsample3d (:125-127,165-167). */
+int vs_vae_copy_frames(const void* src, long long src_ns, void* dst, long long dst_ns, int n,
+                       long long frame_elems, void* stream);
+
+
 #ifdef __cplusplus
 }
 #endif

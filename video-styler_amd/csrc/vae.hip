@@ -1,0 +1,479 @@
+// Causal 3-D VAE kernels (Wan2.1 VAE, diffsynth/models/wan_video_vae.py) for gfx950.
+//
+// vae_conv_kernel: one implicit-GEMM MFMA kernel covers every convolution of the VAE
+//   (CausalConv3d 3x3x3 / 1x1x1 / (3,1,1) time convs, the 3x3 stride-1/2 Conv2d of Resample with
+//   the nearest-x2 upsample fused into its gather, the 1x1 convs of AttentionBlock) and the two
+//   batched GEMMs of the VAE attention (fp32 scores, P.V).
+//   Tile: 128 output pixels x 32*NB output channels, K-step 32 (one 64-B row chunk group), 4 waves
+//   of 32 pixels each.  Operands are register-staged global->LDS (double buffered, loads of step
+//   s+1 in flight during the MFMAs of step s, one barrier per step); LDS rows are 64 B with the
+//   16-B chunk swizzle c ^ ((row>>1)&3), conflict-free for the 32-row ds_read_b128 fragments.
+//   The product is computed transposed, D[co][pix] = W . X^T with v_mfma_f32_32x32x16_bf16, so
+//   each lane owns one pixel and 4 consecutive channels per register group (8-byte stores into
+//   the channels-last output).  Padding (causal time pad, spatial pad, ZeroPad2d) is a predicate
+//   on the gather, never a padded copy.
+// The elementwise kernels (channel RMS norm + SiLU, softmax, transpose, tile gather/blend) are
+// HBM-bound one-pass kernels.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BK = 32, CNTHR = 256;
+
+__device__ __forceinline__ int swz(int row, int ch) { return row * 64 + 16 * (ch ^ ((row >> 1) & 3)); }
+
+template <int NB, bool F32>
+__global__ __launch_bounds__(CNTHR, 2) void vae_conv_kernel(vs_conv3d p, long long M, int ntn) {
+    constexpr int BN = 32 * NB;
+    constexpr int NBL = (BN * 4 + CNTHR - 1) / CNTHR;
+    constexpr int STAGE = (BM + BN) * 64;
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long mt = blockIdx.x / ntn;
+    const int n0 = (blockIdx.x % ntn) * BN;
+    const int z = blockIdx.y;
+    const long long m0 = mt * BM;
+
+    // ---- A (pixel) loader state: row tid>>1, chunks 2*(tid&1)+{0,1}
+    const int arow = tid >> 1, ach = (tid & 1) * 2;
+    const long long am = m0 + arow;
+    const bool avalid = am < M;
+    int ti0, yi0, xi0;
+    const bf16_t* xb;
+    {
+        long long q = avalid ? am : 0;
+        int xo = (int)(q % p.w_out); q /= p.w_out;
+        int yo = (int)(q % p.h_out); q /= p.h_out;
+        int to = (int)(q % p.t_out);
+        long long nn = q / p.t_out;
+        xb = (const bf16_t*)p.x + z * p.x_zs + nn * p.x_ns + ach * 8;
+        ti0 = to * p.st - p.pt;
+        yi0 = yo * p.sh - p.ph;
+        xi0 = xo * p.sw - p.pw;
+    }
+    const int hv = p.up2 ? 2 * p.h_in : p.h_in, wv = p.up2 ? 2 * p.w_in : p.w_in;
+    const bf16_t* wb = (const bf16_t*)p.w + z * p.w_zs;
+
+    const int csteps = p.cin / BK;
+    const int nsteps = p.kt * p.kh * p.kw * csteps;
+    int lc = 0, lkx = 0, lky = 0, lkt = 0;  // loader position (uniform)
+
+    u32x4_t ra0, ra1, rb[NBL];
+    auto load = [&]() {
+        const int ti = ti0 + lkt, yi = yi0 + lky, xi = xi0 + lkx;
+        const bool v = avalid && ti >= p.t_lo && ti < p.t_in && yi >= 0 && yi < hv && xi >= 0 && xi < wv;
+        if (v) {
+            const int ys = p.up2 ? (yi >> 1) : yi, xs = p.up2 ? (xi >> 1) : xi;
+            const bf16_t* src = xb + ((long long)(ti * p.h_in + ys) * p.w_in + xs) * p.ldx + lc;
+            ra0 = *(const u32x4_t*)src;
+            ra1 = *(const u32x4_t*)(src + 8);
+        } else {
+            ra0 = u32x4_t{0, 0, 0, 0};
+            ra1 = ra0;
+        }
+        const int kofs = ((lkt * p.kh + lky) * p.kw + lkx) * p.cin + lc;
+#pragma unroll
+        for (int i = 0; i < NBL; ++i) {
+            const int c = tid + CNTHR * i;
+            rb[i] = u32x4_t{0, 0, 0, 0};
+            if (c < BN * 4) {
+                const int nr = n0 + (c >> 2);
+                if (nr < p.cout) rb[i] = *(const u32x4_t*)(wb + (long long)nr * p.ldw + kofs + (c & 3) * 8);
+            }
+        }
+        // advance (c0, kx, ky, kt)
+        lc += BK;
+        if (lc == p.cin) {
+            lc = 0;
+            if (++lkx == p.kw) {
+                lkx = 0;
+                if (++lky == p.kh) { lky = 0; ++lkt; }
+            }
+        }
+    };
+    auto store = [&](int buf) {
+        char* A = lds + buf * STAGE;
+        char* B = A + BM * 64;
+        *(u32x4_t*)(A + swz(arow, ach)) = ra0;
+        *(u32x4_t*)(A + swz(arow, ach + 1)) = ra1;
+#pragma unroll
+        for (int i = 0; i < NBL; ++i) {
+            const int c = tid + CNTHR * i;
+            if (c < BN * 4) *(u32x4_t*)(B + swz(c >> 2, c & 3)) = rb[i];
+        }
+    };
+
+    f32x16_t acc[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+    auto compute = [&](int buf) {
+        const char* A = lds + buf * STAGE;
+        const char* B = A + BM * 64;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int ch = 2 * s + (lane >> 5);
+            const bf16x8_t xa = *(const bf16x8_t*)(A + swz(wave * 32 + (lane & 31), ch));
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+                const bf16x8_t wf = *(const bf16x8_t*)(B + swz(j * 32 + (lane & 31), ch));
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xa, acc[j], 0, 0, 0);
+            }
+        }
+    };
+
+    load();
+    store(0);
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+        const bool more = s + 1 < nsteps;
+        if (more) load();
+        compute(s & 1);
+        if (more) store((s + 1) & 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: lane owns pixel m, channels n0 + 32j + 8g + 4h + {0..3}
+    const long long me = m0 + wave * 32 + (lane & 31);
+    if (me >= M) return;
+    long long q = me;
+    const int xo = (int)(q % p.w_out); q /= p.w_out;
+    const int yo = (int)(q % p.h_out); q /= p.h_out;
+    const int to = (int)(q % p.t_out);
+    const long long nn = q / p.t_out;
+    const int h = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = n0 + 32 * j + 8 * g + 4 * h;
+            if (n >= p.cout) continue;
+            int co = n, sub = 0;
+            if (p.split > 0 && n >= p.split) { co = n - p.split; sub = 1; }
+            const int tt = to * p.t_mul + p.t_add + sub;
+            const long long off = z * p.y_zs + nn * p.y_ns + ((long long)(tt * p.h_out + yo) * p.w_out + xo) * p.ldy + co;
+            const int nv = min(4, p.cout - n);
+            if constexpr (F32) {
+                float* y = (float*)p.y + off;
+                if (nv == 4) {
+                    *(f32x4_t*)y = f32x4_t{p.alpha * acc[j][4 * g], p.alpha * acc[j][4 * g + 1],
+                                           p.alpha * acc[j][4 * g + 2], p.alpha * acc[j][4 * g + 3]};
+                } else {
+                    for (int e = 0; e < nv; ++e) y[e] = p.alpha * acc[j][4 * g + e];
+                }
+            } else {
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float a = acc[j][4 * g + e];
+                    if (p.bias && e < nv) a += bf2f(((const bf16_t*)p.bias)[n + e]);
+                    v[e] = rbf(a);
+                }
+                bf16_t* y = (bf16_t*)p.y + off;
+                if (p.res) {
+                    const bf16_t* r = (const bf16_t*)p.res + off;
+                    for (int e = 0; e < nv; ++e) v[e] = rbf(v[e] + bf2f(r[e]));
+                }
+                if (nv == 4) {
+                    *(u32x2_t*)y = u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
+                } else {
+                    for (int e = 0; e < nv; ++e) y[e] = (bf16_t)f2bf(v[e]);
+                }
+            }
+        }
+    }
+}
+
+template <int NB>
+int launch_conv(const vs_conv3d& p, long long M, hipStream_t st) {
+    const int ntn = (p.cout + 32 * NB - 1) / (32 * NB);
+    const long long mt = (M + BM - 1) / BM;
+    if (mt * ntn > 0x7fffffffLL) return VS_E_UNSUPPORTED;
+    dim3 grid((unsigned)(mt * ntn), p.nz);
+    if (p.out_f32)
+        hipLaunchKernelGGL((vae_conv_kernel<NB, true>), grid, dim3(CNTHR), 0, st, p, M, ntn);
+    else
+        hipLaunchKernelGGL((vae_conv_kernel<NB, false>), grid, dim3(CNTHR), 0, st, p, M, ntn);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Channel RMS norm (+SiLU): 4 lanes per pixel, lane q owns 16-B chunks q, q+4, q+8, ...
+__global__ __launch_bounds__(256) void vae_rmsnorm_kernel(const bf16_t* __restrict__ x, long long ldx,
+                                                          bf16_t* __restrict__ y, long long ldy,
+                                                          const bf16_t* __restrict__ gamma, long long npix,
+                                                          int c, int silu, float scale) {
+    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long pix = gid >> 2;
+    const int q = (int)(gid & 3);
+    const bool valid = pix < npix;
+    const int nch = c >> 5;  // chunks per lane
+    const bf16_t* xr = x + (valid ? pix : 0) * ldx;
+    float ss = 0.f;
+    for (int i = 0; i < nch; ++i) {
+        const u32x4_t w = *(const u32x4_t*)(xr + (q + 4 * i) * 8);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float a = bflo(w[e]), b = bfhi(w[e]);
+            ss += a * a + b * b;
+        }
+    }
+    ss += __shfl_xor(ss, 1);
+    ss += __shfl_xor(ss, 2);
+    if (!valid) return;
+    const float nrm = fmaxf(rbf(sqrtf(ss)), 1e-12f);  // F.normalize: x / max(||x||, eps), norm in bf16
+    bf16_t* yr = y + pix * ldy;
+    for (int i = 0; i < nch; ++i) {
+        const int c0 = (q + 4 * i) * 8;
+        const u32x4_t w = *(const u32x4_t*)(xr + c0);
+        const u32x4_t gw = *(const u32x4_t*)(gamma + c0);
+        u32x4_t o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float v0 = rbf(rbf(rbf(bflo(w[e]) / nrm) * scale) * bflo(gw[e]));
+            float v1 = rbf(rbf(rbf(bfhi(w[e]) / nrm) * scale) * bfhi(gw[e]));
+            if (silu) {
+                v0 = v0 / (1.0f + expf(-v0));
+                v1 = v1 / (1.0f + expf(-v1));
+            }
+            o[e] = pack2(v0, v1);
+        }
+        *(u32x4_t*)(yr + c0) = o;
+    }
+}
+
+// One wave per row.
+__global__ __launch_bounds__(256) void vae_softmax_kernel(const float* __restrict__ s, long long ld_s,
+                                                          bf16_t* __restrict__ p, long long ld_p,
+                                                          long long rows, int ncols) {
+    const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    const float* sr = s + row * ld_s;
+    bf16_t* pr = p + row * ld_p;
+    float mx = -INFINITY;
+    for (int j = lane; j < ncols; j += 64) mx = fmaxf(mx, sr[j]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float sum = 0.f;
+    for (int j = lane; j < ncols; j += 64) sum += expf(sr[j] - mx);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
+    const float inv = 1.0f / sum;
+    for (int j = lane; j < ld_p; j += 64) pr[j] = j < ncols ? (bf16_t)f2bf(expf(sr[j] - mx) * inv) : (bf16_t)0;
+}
+
+__global__ __launch_bounds__(256) void vae_transpose_kernel(const bf16_t* __restrict__ v, long long v_zs,
+                                                            long long ld_v, bf16_t* __restrict__ vt,
+                                                            long long vt_zs, long long ld_vt, int rows,
+                                                            int cols) {
+    __shared__ bf16_t tile[32][33];
+    const int z = blockIdx.z;
+    const int r0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    for (int i = ty; i < 32; i += 8) {
+        const int r = r0 + i, c = c0 + tx;
+        tile[i][tx] = (r < rows && c < cols) ? v[z * v_zs + (long long)r * ld_v + c] : (bf16_t)0;
+    }
+    __syncthreads();
+    for (int i = ty; i < 32; i += 8) {
+        const int c = c0 + i, r = r0 + tx;
+        if (c < cols && r < ld_vt) vt[z * vt_zs + (long long)c * ld_vt + r] = tile[tx][i];
+    }
+}
+
+__device__ __forceinline__ float affine(float x, int mode, const bf16_t* a, const bf16_t* b, int c) {
+    if (mode == 1) return rbf(rbf(x - bf2f(a[c])) * bf2f(b[c]));
+    if (mode == 2) return rbf(rbf(x / bf2f(b[c])) + bf2f(a[c]));
+    return x;
+}
+
+__global__ __launch_bounds__(256) void vae_tile_gather_kernel(const bf16_t* __restrict__ src, int c, int t_src,
+                                                              int h, int w, int t, int h0, int w0, int th, int tw,
+                                                              bf16_t* __restrict__ dst, int cpad, int mode,
+                                                              const bf16_t* a, const bf16_t* b) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;  // (t, i, j)
+    const long long npix = (long long)t * th * tw;
+    if (idx >= npix) return;
+    const int j = (int)(idx % tw);
+    const int i = (int)((idx / tw) % th);
+    const int tt = (int)(idx / ((long long)tw * th));
+    const long long plane = (long long)t_src * h * w;
+    const long long so = ((long long)tt * h + h0 + i) * w + w0 + j;
+    bf16_t* d = dst + idx * cpad;
+    for (int cc = 0; cc < cpad; cc += 2) {
+        float v0 = 0.f, v1 = 0.f;
+        if (cc < c) v0 = affine(bf2f(src[cc * plane + so]), mode, a, b, cc);
+        if (cc + 1 < c) v1 = affine(bf2f(src[(cc + 1) * plane + so]), mode, a, b, cc + 1);
+        *(uint32_t*)(d + cc) = pack2(v0, v1);
+    }
+}
+
+__device__ __forceinline__ float ramp(int i, int len, bool lo_bound, bool hi_bound, int bw) {
+    float m = 1.0f;
+    if (!lo_bound && i < bw) m = (float)(i + 1) / (float)bw;
+    if (!hi_bound && i >= len - bw) m = (float)(len - i) / (float)bw;
+    return m;
+}
+
+__global__ __launch_bounds__(256) void vae_tile_blend_kernel(const bf16_t* __restrict__ tile, long long ldc,
+                                                             int c, int t, int th, int tw,
+                                                             bf16_t* __restrict__ values, bf16_t* __restrict__ weight,
+                                                             int h, int w, int h0, int w0, int bound, int bw_h,
+                                                             int bw_w, int mode, const bf16_t* a, const bf16_t* b) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long npix = (long long)t * th * tw;
+    if (idx >= npix) return;
+    const int j = (int)(idx % tw);
+    const int i = (int)((idx / tw) % th);
+    const int tt = (int)(idx / ((long long)tw * th));
+    const float mh = ramp(i, th, bound & 1, bound & 2, bw_h);
+    const float mw = ramp(j, tw, bound & 4, bound & 8, bw_w);
+    const float mask = rbf(fminf(mh, mw));
+    const long long plane = (long long)t * h * w;
+    const long long o = ((long long)tt * h + h0 + i) * w + w0 + j;
+    const bf16_t* tr = tile + idx * ldc;
+    for (int cc = 0; cc < c; ++cc) {
+        const float v = affine(bf2f(tr[cc]), mode, a, b, cc);
+        values[cc * plane + o] = (bf16_t)f2bf(bf2f(values[cc * plane + o]) + rbf(v * mask));
+    }
+    weight[o] = (bf16_t)f2bf(bf2f(weight[o]) + mask);
+}
+
+__global__ __launch_bounds__(256) void vae_blend_finish_kernel(const bf16_t* __restrict__ values,
+                                                               const bf16_t* __restrict__ weight,
+                                                               bf16_t* __restrict__ out, int c, long long plane,
+                                                               int clamp) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= plane * c) return;
+    float v = rbf(bf2f(values[idx]) / bf2f(weight[idx % plane]));
+    if (clamp) v = fminf(fmaxf(v, -1.0f), 1.0f);
+    out[idx] = (bf16_t)f2bf(v);
+}
+
+// vae_output_to_video: bf16 (x - (-1)) * 127.5, clip [0, 255], truncating uint8 cast, CTHW -> THWC.
+__global__ __launch_bounds__(256) void vae_to_u8_kernel(const bf16_t* __restrict__ v, uint8_t* __restrict__ out,
+                                                        long long plane) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= plane) return;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float x = rbf(rbf(bf2f(v[c * plane + idx]) + 1.0f) * 127.5f);
+        x = fminf(fmaxf(x, 0.0f), 255.0f);
+        out[idx * 3 + c] = (uint8_t)(int)x;
+    }
+}
+
+}  // namespace
+
+extern "C" int vs_vae_to_u8(const void* video, void* out, int t, int h, int w, void* stream) {
+    if (!video || !out || t <= 0 || h <= 0 || w <= 0) return VS_E_INVALID;
+    const long long plane = (long long)t * h * w;
+    hipLaunchKernelGGL(vae_to_u8_kernel, dim3((unsigned)((plane + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)video, (uint8_t*)out, plane);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_vae_conv(const vs_conv3d* pp, void* stream) {
+    if (!pp) return VS_E_INVALID;
+    const vs_conv3d& p = *pp;
+    if (!p.x || !p.w || !p.y || p.cin <= 0 || p.cin % BK || p.ldx % 8 || p.ldw % 8 || p.cout <= 0 ||
+        p.n <= 0 || p.nz <= 0 || p.t_out < 0 || p.h_out <= 0 || p.w_out <= 0 || p.kt <= 0 || p.kh <= 0 ||
+        p.kw <= 0 || p.st <= 0 || p.sh <= 0 || p.sw <= 0 || p.ldy % 4 || (p.split > 0 && p.split % 4) ||
+        (p.out_f32 && (p.bias || p.res)))
+        return VS_E_INVALID;
+    if (((uintptr_t)p.x | (uintptr_t)p.w) & 15) return VS_E_INVALID;
+    if (p.t_out == 0) return VS_OK;
+    const long long M = (long long)p.n * p.t_out * p.h_out * p.w_out;
+    hipStream_t st = (hipStream_t)stream;
+    if (p.cout <= 32) return launch_conv<1>(p, M, st);
+    if (p.cout <= 64) return launch_conv<2>(p, M, st);
+    if (p.cout <= 96) return launch_conv<3>(p, M, st);
+    const int w4 = (p.cout + 127) / 128 * 128 - p.cout, w3 = (p.cout + 95) / 96 * 96 - p.cout;
+    return w3 < w4 ? launch_conv<3>(p, M, st) : launch_conv<4>(p, M, st);
+}
+
+extern "C" int vs_vae_rmsnorm(const void* x, long long ldx, void* y, long long ldy, const void* gamma,
+                              long long npix, int c, int silu, void* stream) {
+    if (!x || !y || !gamma || c <= 0 || c % 32 || ldx % 8 || ldy % 8 || npix < 0) return VS_E_INVALID;
+    if (npix == 0) return VS_OK;
+    const long long threads = npix * 4;
+    hipLaunchKernelGGL(vae_rmsnorm_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)x, ldx, (bf16_t*)y, ldy, (const bf16_t*)gamma, npix,
+                       c, silu, (float)sqrt((double)c));
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_vae_softmax(const float* s, long long ld_s, void* p, long long ld_p, long long rows, int ncols,
+                              void* stream) {
+    if (!s || !p || ncols <= 0 || ld_s < ncols || ld_p < ncols || rows < 0) return VS_E_INVALID;
+    if (rows == 0) return VS_OK;
+    hipLaunchKernelGGL(vae_softmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                       s, ld_s, (bf16_t*)p, ld_p, rows, ncols);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_vae_transpose(const void* v, long long v_zs, long long ld_v, void* vt, long long vt_zs,
+                                long long ld_vt, int nz, int rows, int cols, void* stream) {
+    if (!v || !vt || nz <= 0 || rows <= 0 || cols <= 0 || ld_vt < rows || ld_v < cols) return VS_E_INVALID;
+    dim3 grid((unsigned)((ld_vt + 31) / 32), (unsigned)((cols + 31) / 32), nz);
+    hipLaunchKernelGGL(vae_transpose_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)v, v_zs, ld_v,
+                       (bf16_t*)vt, vt_zs, ld_vt, rows, cols);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_vae_tile_gather(const void* src, int c, int t_src, int h, int w, int t, int h0, int w0, int th,
+                                  int tw, void* dst, int cpad, int mode, const void* a, const void* b, void* stream) {
+    if (!src || !dst || c <= 0 || cpad < c || cpad % 2 || t <= 0 || t > t_src || th <= 0 || tw <= 0 || h0 < 0 || w0 < 0 ||
+        h0 + th > h || w0 + tw > w || mode < 0 || mode > 2 || (mode && (!a || !b)))
+        return VS_E_INVALID;
+    const long long n = (long long)t * th * tw;
+    hipLaunchKernelGGL(vae_tile_gather_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)src, c, t_src, h, w, t, h0, w0, th, tw, (bf16_t*)dst, cpad, mode, (const bf16_t*)a,
+                       (const bf16_t*)b);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_vae_tile_blend(const void* tile, long long ldc, int c, int t, int th, int tw, void* values,
+                                 void* weight, int h, int w, int h0, int w0, int bound, int bw_h, int bw_w,
+                                 int mode, const void* a, const void* b, void* stream) {
+    if (!tile || !values || !weight || c <= 0 || ldc < c || t <= 0 || th <= 0 || tw <= 0 || h0 < 0 || w0 < 0 ||
+        h0 + th > h || w0 + tw > w || mode < 0 || mode > 2 || (mode && (!a || !b)) ||
+        ((bound & 3) != 3 && bw_h <= 0) || ((bound & 12) != 12 && bw_w <= 0))
+        return VS_E_INVALID;
+    const long long n = (long long)t * th * tw;
+    hipLaunchKernelGGL(vae_tile_blend_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)tile, ldc, c, t, th, tw, (bf16_t*)values, (bf16_t*)weight, h, w, h0, w0, bound,
+                       bw_h, bw_w, mode, (const bf16_t*)a, (const bf16_t*)b);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_vae_blend_finish(const void* values, const void* weight, void* out, int c, long long plane,
+                                   int clamp, void* stream) {
+    if (!values || !weight || !out || c <= 0 || plane <= 0) return VS_E_INVALID;
+    const long long n = plane * c;
+    hipLaunchKernelGGL(vae_blend_finish_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)values, (const bf16_t*)weight, (bf16_t*)out, c, plane, clamp);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_vae_copy_frames(const void* src, long long src_ns, void* dst, long long dst_ns, int n,
+                                  long long frame_elems, void* stream) {
+    if (!src || !dst || n <= 0 || frame_elems <= 0 || src_ns < frame_elems || dst_ns < frame_elems)
+        return VS_E_INVALID;
+    if (hipMemcpy2DAsync(dst, dst_ns * 2, src, src_ns * 2, frame_elems * 2, n, hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream) != hipSuccess)
+        return VS_E_LAUNCH;
+    return VS_OK;
+}

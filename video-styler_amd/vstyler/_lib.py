@@ -29,6 +29,25 @@ class VsEpilogue(ctypes.Structure):
 
 _P, _LL, _I, _F = ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_float
 
+
+class VsConv3d(ctypes.Structure):
+    """struct vs_conv3d of include/vstyler.h (implicit-GEMM VAE convolution)."""
+    _fields_ = [
+        ("x", _P), ("x_zs", _LL), ("x_ns", _LL), ("ldx", _LL),
+        ("n", _I), ("t_in", _I), ("h_in", _I), ("w_in", _I), ("cin", _I),
+        ("kt", _I), ("kh", _I), ("kw", _I), ("st", _I), ("sh", _I), ("sw", _I),
+        ("pt", _I), ("ph", _I), ("pw", _I), ("up2", _I), ("t_lo", _I),
+        ("t_out", _I), ("h_out", _I), ("w_out", _I),
+        ("w", _P), ("w_zs", _LL), ("ldw", _LL),
+        ("bias", _P),
+        ("cout", _I),
+        ("y", _P), ("y_zs", _LL), ("y_ns", _LL), ("ldy", _LL),
+        ("t_mul", _I), ("t_add", _I), ("split", _I), ("out_f32", _I),
+        ("alpha", _F),
+        ("res", _P),
+        ("nz", _I),
+    ]
+
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 SIGNATURES = {
     "vs_abi_version": [],
@@ -46,6 +65,15 @@ SIGNATURES = {
     "vs_mod_add": [_P, _P, _P, _I, _I, _I, _LL, _LL, _P],
     "vs_axpy": [_P, _P, _F, _LL, _P],
     "vs_ulysses_permute": [_P, _P, _I, _I, _I, _I, _LL, _LL, _I, _P],
+    "vs_vae_conv": [ctypes.POINTER(VsConv3d), _P],
+    "vs_vae_rmsnorm": [_P, _LL, _P, _LL, _P, _LL, _I, _I, _P],
+    "vs_vae_softmax": [_P, _LL, _P, _LL, _LL, _I, _P],
+    "vs_vae_transpose": [_P, _LL, _LL, _P, _LL, _LL, _I, _I, _I, _P],
+    "vs_vae_tile_gather": [_P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P],
+    "vs_vae_to_u8": [_P, _P, _I, _I, _I, _P],
+    "vs_vae_tile_blend": [_P, _LL, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
+    "vs_vae_blend_finish": [_P, _P, _P, _I, _LL, _I, _P],
+    "vs_vae_copy_frames": [_P, _LL, _P, _LL, _I, _LL, _P],
 }
 _RESTYPES = {"vs_strerror": ctypes.c_char_p}
 
