@@ -104,6 +104,10 @@ int vs_unpatchify(const void* tokens, void* lat, int batch, int channels, int fr
  * Replaces the CFG combine (wan_video_new.py:535) + FlowMatchScheduler.step (flow_match.py:72-82). */
 int vs_cfg_euler(const void* v_pos, const void* v_neg, void* x, long long n, float cfg_scale,
                  float dsigma, int use_cfg, void* stream);
+/* Same, with dsigma read from device memory (one fp32): lets a hipGraph-captured denoising step
+ * be replayed for every step index with the step's dsigma written to that slot before launch. */
+int vs_cfg_euler_dev(const void* v_pos, const void* v_neg, void* x, long long n, float cfg_scale,
+                     const float* dsigma, int use_cfg, void* stream);
 
 /* out[b] = bf16([cos(t*10000^(-i/(dim/2))) || sin(...)]) in fp64, t = bf16 timestep[b]
  * (sinusoidal_embedding_1d, wan_video_dit.py:68-72). */
@@ -199,6 +203,17 @@ int vs_vae_blend_finish(const void* values, const void* weight, void* out, int c
 /* BasePipeline.vae_output_to_video (diffsynth/pipelines/wan_video_new.py:557 -> utils/__init__.py:76-91) for B = 1:
  * video bf16 [3][t][h][w] in [-1, 1] -> out uint8 [t][h][w][3] = trunc(clip(bf16(bf16(x+1)*127.5))). */
 int vs_vae_to_u8(const void* video, void* out, int t, int h, int w, void* stream);
+
+/* WanVideoUnit_VACE.process (diffsynth/pipelines/wan_video_new.py:878-888): uint8 frames
+ * [t][h][w][3] (video_u8 NULL = zeros, mask_u8 NULL = ones) -> preprocess_video to bf16 in [-1, 1]
+ * (mask in [0, 1]), inactive = v*(1-m) + 0*m and reactive = v*m + 0*(1-m) as NCTHW [3][t][h][w]
+ * bf16, and mask channel 0 as mask0 [t][h][w] bf16 -- the reference's bf16 rounding points. */
+int vs_vace_prepare(const void* video_u8, const void* mask_u8, void* inactive, void* reactive, void* mask0,
+                    int t, int h, int w, void* stream);
+
+/* VACE mask latents (wan_video_new.py:893-894): out [64][t_out][h/8][w/8] bf16 (a channel slice of
+ * vace_context) = nearest-exact temporal resize of rearrange(mask0, "T (H 8) (W 8) -> (8 8) T H W"). */
+int vs_vace_mask_latents(const void* mask0, void* out, int t, int h, int w, int t_out, void* stream);
 
 /* Copy n frames of frame_elems elements (src/dst strides per n in elements): the pass-through
  * first frame of Resample downsample3d/upsample3d (:125-127,165-167). */

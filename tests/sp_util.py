@@ -3,7 +3,7 @@ gloo collectives (several ranks sharing one GPU).  Never used by the product pat
 import torch
 import torch.distributed as dist
 
-from vstyler.usp import UlyssesGroup
+from vstyler.usp import UlyssesGroup, _Done
 
 
 def permute_ref(src, dst, batch, s_local, world, cpr, ld_local, jstride, mode):
@@ -49,6 +49,7 @@ class HostStagedUlysses(UlyssesGroup):
         r = torch.empty(recv.shape, dtype=recv.dtype)
         dist.all_to_all_single(r, send.cpu(), group=self.group)
         recv.copy_(r)
+        return _Done()
 
     def _all_gather(self, recv, send):
         torch.cuda.synchronize()

@@ -144,3 +144,18 @@ def test_lora_merge_and_hotload():
     linear(m.q, x.cuda(), out, Workspace("cuda"))
     ref = O.lora_linear(x, w, b, O.bf(down.float() * 0.7), up)
     assert err(out, ref)[1] < 1e-2
+
+
+def test_denoise_graph_replay_bit_identical_to_eager(tiny):
+    """The hipGraph-captured step (captured once, replayed with per-step timestep/dsigma slots)
+    gives exactly the eager loop's latents (same kernels, same order)."""
+    from vstyler import WanVideoPipeline
+    cfg, W, dit, vace = tiny
+    pipe = WanVideoPipeline(device="cuda")
+    pipe.dit, pipe.vace = dit, vace
+    lat, cp, cn, vc = O.synthetic_inputs(cfg, 5, 128, 128)
+    eager = pipe.denoise(lat, cp.cuda(), cn.cuda(), vc.cuda(), num_inference_steps=4, use_graph=False)
+    assert pipe.last_graph is None
+    graph = pipe.denoise(lat, cp.cuda(), cn.cuda(), vc.cuda(), num_inference_steps=4, use_graph=True)
+    assert pipe.last_graph is not None
+    assert torch.equal(eager, graph)

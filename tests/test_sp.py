@@ -98,11 +98,16 @@ def _gpu_worker(rank, world, port, q):
         t = torch.tensor([833.3333]).to(torch.bfloat16).cuda()
         ctx = torch.cat([cp, cn]).cuda()
         single = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx, vace_context=vc.cuda())
-        sp = HostStagedUlysses()
-        par = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx, vace_context=vc.cuda(),
-                                 use_unified_sequence_parallel=True, sp_group=sp)
-        torch.cuda.synchronize()
-        q.put((rank, torch.equal(single.cpu(), par.cpu()), (single.float() - par.float()).abs().max().item()))
+        same, mx = True, 0.0
+        for overlap in (True, False):   # per-sample micro-batch overlap schedule, then sequential
+            sp = HostStagedUlysses()
+            sp.overlap = overlap
+            par = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx,
+                                     vace_context=vc.cuda(), use_unified_sequence_parallel=True, sp_group=sp)
+            torch.cuda.synchronize()
+            same = same and torch.equal(single.cpu(), par.cpu())
+            mx = max(mx, (single.float() - par.float()).abs().max().item())
+        q.put((rank, same, mx))
     except Exception as e:  # pragma: no cover
         import traceback
         q.put((rank, traceback.format_exc(), None))

@@ -194,9 +194,11 @@ __global__ void unpatchify_kernel(const bf16_t* __restrict__ tok, bf16_t* __rest
 }
 
 __global__ void cfg_euler_kernel(const bf16_t* __restrict__ vp, const bf16_t* __restrict__ vn,
-                                 bf16_t* __restrict__ x, long long n8, float g, float ds, int use_cfg) {
+                                 bf16_t* __restrict__ x, long long n8, float g, float ds, int use_cfg,
+                                 const float* __restrict__ ds_dev) {
     const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= n8) return;
+    if (ds_dev) ds = *ds_dev;
     float a[8], b[8], xv[8];
     unpack8(reinterpret_cast<const u32x4_t*>(vp)[i], a);
     unpack8(reinterpret_cast<const u32x4_t*>(x)[i], xv);
@@ -354,7 +356,19 @@ extern "C" int vs_cfg_euler(const void* v_pos, const void* v_neg, void* x, long 
     const long long n8 = n / 8;
     hipLaunchKernelGGL(cfg_euler_kernel, dim3(nblk(n8, 256)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)v_pos, (const bf16_t*)v_neg, (bf16_t*)x, n8, cfg_scale,
-                       dsigma, use_cfg);
+                       dsigma, use_cfg, (const float*)nullptr);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_cfg_euler_dev(const void* v_pos, const void* v_neg, void* x, long long n, float cfg_scale,
+                                const float* dsigma, int use_cfg, void* stream) {
+    if (!v_pos || !x || !dsigma || n <= 0 || n % 8 || (use_cfg && !v_neg)) return VS_E_INVALID;
+    if (!al16(v_pos) || !al16(x) || (use_cfg && !al16(v_neg))) return VS_E_INVALID;
+    const long long n8 = n / 8;
+    hipLaunchKernelGGL(cfg_euler_kernel, dim3(nblk(n8, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)v_pos, (const bf16_t*)v_neg, (bf16_t*)x, n8, cfg_scale,
+                       0.0f, use_cfg, dsigma);
     VS_CHECK_LAUNCH();
     return VS_OK;
 }

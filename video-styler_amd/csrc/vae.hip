@@ -368,7 +368,66 @@ __global__ __launch_bounds__(256) void vae_to_u8_kernel(const bf16_t* __restrict
     }
 }
 
+// WanVideoUnit_VACE.process (wan_video_new.py:878-888) on uint8 frames [T][H][W][3]:
+// preprocess_video (utils/__init__.py:60-73) then inactive = v*(1-m) + 0*m, reactive = v*m + 0*(1-m),
+// every op a bf16 tensor op.  video == NULL -> zeros, mask == NULL -> ones (:880-886).
+__global__ __launch_bounds__(256) void vace_prepare_kernel(const uint8_t* __restrict__ video,
+                                                           const uint8_t* __restrict__ mask,
+                                                           bf16_t* __restrict__ inactive, bf16_t* __restrict__ reactive,
+                                                           bf16_t* __restrict__ mask0, long long plane) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= plane) return;
+    const float sv = 2.0f / 255.0f, sm = 1.0f / 255.0f;  // (max - min) / 255 as fp32 opmath scalars
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float v = video ? rbf(rbf((float)video[idx * 3 + c] * sv) - 1.0f) : 0.0f;
+        const float m = mask ? rbf(rbf((float)mask[idx * 3 + c] * sm) + 0.0f) : 1.0f;
+        const float om = rbf(1.0f - m);
+        inactive[c * plane + idx] = (bf16_t)f2bf(rbf(v * om) + rbf(0.0f * m));
+        reactive[c * plane + idx] = (bf16_t)f2bf(rbf(v * m) + rbf(0.0f * om));
+        if (c == 0) mask0[idx] = (bf16_t)f2bf(m);
+    }
+}
+
+// vace_mask_latents (wan_video_new.py:893-894): rearrange "T (H 8) (W 8) -> (8 8) T H W" and
+// nearest-exact resize of T to t_out = (T + 3) // 4 (src = min(floor((j + 0.5) * T / t_out), T - 1)).
+__global__ __launch_bounds__(256) void vace_mask_latents_kernel(const bf16_t* __restrict__ mask0,
+                                                                bf16_t* __restrict__ out, int t, int h, int w,
+                                                                int t_out) {
+    const int hl = h / 8, wl = w / 8;
+    const long long n = 64LL * t_out * hl * wl;
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= n) return;
+    const int ww = (int)(idx % wl);
+    const int hh = (int)((idx / wl) % hl);
+    const int j = (int)((idx / ((long long)wl * hl)) % t_out);
+    const int c = (int)(idx / ((long long)wl * hl * t_out));
+    const float scale = (float)t / (float)t_out;
+    const int src = min((int)floorf(((float)j + 0.5f) * scale), t - 1);
+    out[idx] = mask0[((long long)src * h + hh * 8 + c / 8) * w + ww * 8 + c % 8];
+}
+
 }  // namespace
+
+extern "C" int vs_vace_prepare(const void* video_u8, const void* mask_u8, void* inactive, void* reactive,
+                               void* mask0, int t, int h, int w, void* stream) {
+    if (!inactive || !reactive || !mask0 || t <= 0 || h <= 0 || w <= 0) return VS_E_INVALID;
+    const long long plane = (long long)t * h * w;
+    hipLaunchKernelGGL(vace_prepare_kernel, dim3((unsigned)((plane + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t*)video_u8, (const uint8_t*)mask_u8, (bf16_t*)inactive, (bf16_t*)reactive,
+                       (bf16_t*)mask0, plane);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_vace_mask_latents(const void* mask0, void* out, int t, int h, int w, int t_out, void* stream) {
+    if (!mask0 || !out || t <= 0 || h <= 0 || w <= 0 || h % 8 || w % 8 || t_out <= 0) return VS_E_INVALID;
+    const long long n = 64LL * t_out * (h / 8) * (w / 8);
+    hipLaunchKernelGGL(vace_mask_latents_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)mask0, (bf16_t*)out, t, h, w, t_out);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
 
 extern "C" int vs_vae_to_u8(const void* video, void* out, int t, int h, int w, void* stream) {
     if (!video || !out || t <= 0 || h <= 0 || w <= 0) return VS_E_INVALID;

@@ -61,6 +61,7 @@ SIGNATURES = {
     "vs_patchify": [_P, _P, _I, _I, _I, _I, _I, _P],
     "vs_unpatchify": [_P, _P, _I, _I, _I, _I, _I, _P],
     "vs_cfg_euler": [_P, _P, _P, _LL, _F, _F, _I, _P],
+    "vs_cfg_euler_dev": [_P, _P, _P, _LL, _F, _P, _I, _P],
     "vs_time_sinusoid": [_P, _P, _I, _I, _P],
     "vs_mod_add": [_P, _P, _P, _I, _I, _I, _LL, _LL, _P],
     "vs_axpy": [_P, _P, _F, _LL, _P],
@@ -71,6 +72,8 @@ SIGNATURES = {
     "vs_vae_transpose": [_P, _LL, _LL, _P, _LL, _LL, _I, _I, _I, _P],
     "vs_vae_tile_gather": [_P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P],
     "vs_vae_to_u8": [_P, _P, _I, _I, _I, _P],
+    "vs_vace_prepare": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "vs_vace_mask_latents": [_P, _P, _I, _I, _I, _I, _P],
     "vs_vae_tile_blend": [_P, _LL, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
     "vs_vae_blend_finish": [_P, _P, _P, _I, _LL, _I, _P],
     "vs_vae_copy_frames": [_P, _LL, _P, _LL, _I, _LL, _P],

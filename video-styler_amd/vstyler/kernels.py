@@ -147,6 +147,19 @@ def cfg_euler(v_pos, v_neg, x, cfg_scale, dsigma):
     return x
 
 
+def cfg_euler_dev(v_pos, v_neg, x, cfg_scale, dsigma_dev):
+    """cfg_euler with dsigma read from a one-element fp32 device tensor (graph-replayable)."""
+    for t, n in ((v_pos, "v_pos"), (x, "x")):
+        _req(t, n)
+        if not t.is_contiguous():
+            raise ValueError(f"{n} must be contiguous")
+    if dsigma_dev.dtype != torch.float32 or not dsigma_dev.is_cuda:
+        raise ValueError("dsigma_dev must be a float32 device tensor")
+    _lib.check(_lib.load().vs_cfg_euler_dev(v_pos.data_ptr(), _ptr(v_neg), x.data_ptr(), x.numel(), float(cfg_scale),
+                                            dsigma_dev.data_ptr(), int(v_neg is not None), _stream(x)))
+    return x
+
+
 def time_sinusoid(t, out):
     _lib.check(_lib.load().vs_time_sinusoid(t.data_ptr(), out.data_ptr(), t.numel(), out.shape[-1], _stream(t)))
     return out

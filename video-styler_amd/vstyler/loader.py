@@ -80,13 +80,32 @@ def build_vace(state_dict, device):
     return model
 
 
+# configs/model_config.py:163-164 -- the two Wan2.1 VAE file layouts (WanVideoVAE, z_dim 16)
+WAN_VAE_HASHES = ("1378ea763357eea97acdef78e65d6d96", "ccc42284ea13e1ad04693284c7a09be6")
+
+
+def build_vae(state_dict, device):
+    """WanVideoVAE (wan_video_vae.py:1058) from the civitai layout (optionally under 'model_state')."""
+    sd = state_dict.get("model_state", state_dict)
+    if hash_state_dict_keys(sd) not in WAN_VAE_HASHES and \
+            not ("encoder.conv1.weight" in sd and "decoder.head.2.weight" in sd and "conv2.weight" in sd):
+        return None
+    from .vae import WanVideoVAE
+    z_dim = sd["conv2.weight"].shape[0]
+    if z_dim != 16:
+        return None  # the 48-channel Wan2.2 VAE (WanVideoVAE38) is out of scope
+    return WanVideoVAE(z_dim=z_dim, dim=sd["encoder.conv1.weight"].shape[0], device=device).load_state_dict(sd)
+
+
 def load_models(paths, device="cuda"):
     """Returns {'wan_video_dit': WanModel, 'wan_video_vace': VaceWanModel, ...} for the files given."""
     out = {}
     for path in paths:
         sd = load_state_dict(path, device="cpu")
-        if "model_state" in sd:       # Wan VAE .pth layout (wan_video_vae.py:1262-1263)
-            raise NotImplementedError("Wan2.1 VAE checkpoint: VAE kernels are not built in this round")
+        vae = build_vae(sd, device)
+        if vae is not None:
+            out["wan_video_vae"] = vae
+            continue
         dit = build_dit(sd, device)
         if dit is not None:
             out["wan_video_dit"] = dit

@@ -118,14 +118,15 @@ class Workspace:
 
 class KernelTimer:
     """Optional HIP-event bracketing of chosen launches (bench.py roofline): events are recorded on
-    the stream the kernel is launched on (torch's current stream), elapsed times read afterwards."""
+    the stream the kernel is launched on (torch's current stream), elapsed times read afterwards.
+    Inactive while a hipGraph is being captured (ROCm refuses external event nodes in graphs)."""
 
     def __init__(self):
         self.enabled = False
         self.events = {}
 
     def start(self, name):
-        if not self.enabled:
+        if not self.enabled or torch.cuda.is_current_stream_capturing():
             return None
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -139,7 +140,7 @@ class KernelTimer:
     def mean_ms(self, name):
         ev = self.events.get(name, [])
         if not ev:
-            return None
+            return None, 0
         torch.cuda.synchronize()
         return sum(a.elapsed_time(b) for a, b in ev) / len(ev), len(ev)
 
@@ -173,17 +174,45 @@ class DiTBlock(nn.Module):
         self.modulation = _param(1, 6, dim, device=device)
 
     def forward(self, x, t_mod, rc, hint=None, hint_scale=1.0):
-        """x: [B*S, D] updated in place.  t_mod: [B, 6, D].  hint: [B*S, D] added after the block."""
-        B, S, D, eps, ws = rc.batch, rc.seq, self.dim, self.eps, rc.ws
-        M = B * S
+        """x: [B*S, D] updated in place.  t_mod: [B, 6, D].  hint: [B*S, D] added after the block.
+
+        Three phases per micro-batch: (1) LN1 + q/k/v + QK-RMSNorm/RoPE, (2) self-attention,
+        (3) o-proj (gated residual), cross-attention, FFN (gated residual + VACE hint).  Without SP
+        the whole CFG batch is one micro-batch.  Under Ulysses SP with overlap on, each CFG sample
+        is its own micro-batch and phases are issued 1(0) 1(1) 2(0) 2(1) 3(0) 3(1): sample 0's q|k|v
+        all-to-all runs under sample 1's projections, sample 1's under sample 0's attention, and
+        the return exchanges under the other sample's attention / o-proj / cross-attn / FFN."""
+        B, S, D, ws = rc.batch, rc.seq, self.dim, rc.ws
         mod = ws.get("mod", (B, 6, D))
         K.mod_add(self.modulation.view(6, D), t_mod, mod, 6 * D, D)   # :218-219
-        sh_msa, sc_msa, g_msa, sh_mlp, sc_mlp, g_mlp = (mod[:, i] for i in range(6))
-        h = ws.get("h", (M, D))
-        # --- self-attention (wan_video_dit.py:225-226, :140-147)
-        K.layernorm_modulate(x, h, eps, shift=sh_msa, scale=sc_msa, mod_bstride=6 * D, rows_per_batch=S)
+        sp = rc.sp
+        if sp is not None and B > 1 and getattr(sp, "overlap", False):
+            parts = [self._part(x, mod, rc, b, 1, hint, f".{b}") for b in range(B)]
+        else:
+            parts = [self._part(x, mod, rc, 0, B, hint, "")]
+        for p in parts:
+            self._phase_qkv(p, rc)
+        for p in parts:
+            self._phase_attn(p, rc)
+        for p in parts:
+            self._phase_out(p, rc, hint_scale)
+        return x
+
+    def _part(self, x, mod, rc, b0, nb, hint, tag):
+        S, D, L, ws = rc.seq, self.dim, rc.ctx_len, rc.ws
+        r0, M = b0 * S, nb * S
+        p = dict(nb=nb, M=M, x=x[r0:r0 + M], mod=mod[b0:b0 + nb], ctx=rc.ctx[b0 * L:(b0 + nb) * L],
+                 hint=None if hint is None else hint[r0:r0 + M], tag=tag)
+        for n in ("h", "q", "k", "v", "o"):
+            p[n] = ws.get(n + tag, (M, D))
+        return p
+
+    def _phase_qkv(self, p, rc):
+        # --- self-attention inputs (wan_video_dit.py:225-226, :140-145)
+        S, D, eps, ws = rc.seq, self.dim, self.eps, rc.ws
+        mod, h, q, k, v = p["mod"], p["h"], p["q"], p["k"], p["v"]
+        K.layernorm_modulate(p["x"], h, eps, shift=mod[:, 0], scale=mod[:, 1], mod_bstride=6 * D, rows_per_batch=S)
         sa = self.self_attn
-        q, k, v, o = (ws.get(n, (M, D)) for n in ("q", "k", "v", "o"))
         linear(sa.q, h, q, ws)
         linear(sa.k, h, k, ws)
         linear(sa.v, h, v, ws)
@@ -192,32 +221,42 @@ class DiTBlock(nn.Module):
         K.rmsnorm_rope(k, sa.norm_k.weight, eps, rope=rc.rope, grid=rc.grid, rows_per_batch=S,
                        token_offset=rc.token_offset)
         if rc.sp is not None:
-            rc.sp.attention(q, k, v, o, self.num_heads, B)
+            p["xchg"] = rc.sp.exchange_start(q, k, v, self.num_heads, p["nb"], p["tag"])
+
+    def _phase_attn(self, p, rc):
+        if rc.sp is not None:
+            rc.sp.attend(p["xchg"])
         else:
             ev = TIMER.start("self_attn")
-            K.attention(q, k, v, o, self.num_heads, B)
+            K.attention(p["q"], p["k"], p["v"], p["o"], self.num_heads, p["nb"])
             TIMER.stop(ev)
-        linear(sa.o, o, x, ws, epilogue=K.VS_EPI_GATE_RES, residual=x, gate=g_msa,
+
+    def _phase_out(self, p, rc, hint_scale):
+        S, D, eps, ws = rc.seq, self.dim, self.eps, rc.ws
+        x, mod, h, q, o, nb, M = p["x"], p["mod"], p["h"], p["q"], p["o"], p["nb"], p["M"]
+        if rc.sp is not None:
+            rc.sp.finish(p["xchg"], o)
+        sa = self.self_attn
+        linear(sa.o, o, x, ws, epilogue=K.VS_EPI_GATE_RES, residual=x, gate=mod[:, 2],
                gate_bstride=6 * D, rows_per_batch=S)
         # --- cross-attention (wan_video_dit.py:227, :171-186)
         K.layernorm_modulate(x, h, eps, weight=self.norm3.weight, bias=self.norm3.bias)
         ca = self.cross_attn
         L = rc.ctx_len
-        kc, vc = ws.get("kc", (B * L, D)), ws.get("vc", (B * L, D))
+        kc, vc = ws.get("kc" + p["tag"], (nb * L, D)), ws.get("vc" + p["tag"], (nb * L, D))
         linear(ca.q, h, q, ws)
         K.rmsnorm_rope(q, ca.norm_q.weight, eps)
-        linear(ca.k, rc.ctx, kc, ws)
+        linear(ca.k, p["ctx"], kc, ws)
         K.rmsnorm_rope(kc, ca.norm_k.weight, eps)
-        linear(ca.v, rc.ctx, vc, ws)
-        K.attention(q, kc, vc, o, self.num_heads, B)
+        linear(ca.v, p["ctx"], vc, ws)
+        K.attention(q, kc, vc, o, self.num_heads, nb)
         linear(ca.o, o, x, ws, epilogue=K.VS_EPI_RES, residual=x)
         # --- FFN (wan_video_dit.py:228-229) + VACE hint (wan_video_new.py:1450)
-        K.layernorm_modulate(x, h, eps, shift=sh_mlp, scale=sc_mlp, mod_bstride=6 * D, rows_per_batch=S)
-        f = ws.get("f", (M, self.ffn_dim))
+        K.layernorm_modulate(x, h, eps, shift=mod[:, 3], scale=mod[:, 4], mod_bstride=6 * D, rows_per_batch=S)
+        f = ws.get("f" + p["tag"], (M, self.ffn_dim))
         linear(self.ffn[0], h, f, ws, epilogue=K.VS_EPI_GELU)
         linear(self.ffn[2], f, x, ws, epilogue=K.VS_EPI_GATE_RES, residual=x,
-               gate=g_mlp, gate_bstride=6 * D, rows_per_batch=S, hint=hint, hint_scale=hint_scale)
-        return x
+               gate=mod[:, 5], gate_bstride=6 * D, rows_per_batch=S, hint=p["hint"], hint_scale=hint_scale)
 
 
 class Head(nn.Module):

@@ -133,6 +133,36 @@ class ModelConfig:
         self.path = files[0] if len(files) == 1 else files
 
 
+class DenoiseStepper:
+    """Runs CFG denoising steps over device-resident state.  `step_fn(t_buf, d_buf)` enqueues one
+    whole step (model_fn + fused CFG/Euler) reading the bf16 timestep and the fp32 dsigma from the
+    two device slots.  The first call runs eagerly (sizing every Workspace buffer); the step is then
+    captured once into a hipGraph and every later call refreshes the two slots and replays it."""
+
+    def __init__(self, step_fn, timesteps_bf16, dsigmas_f32, use_graph=True, on_replay=None):
+        self.step_fn, self.ts, self.ds = step_fn, timesteps_bf16, dsigmas_f32
+        self.t_buf, self.d_buf = timesteps_bf16[0:1].clone(), dsigmas_f32[0:1].clone()
+        self.use_graph, self.graph, self.on_replay = use_graph, None, on_replay
+
+    def __call__(self, i):
+        self.t_buf.copy_(self.ts[i:i + 1])
+        self.d_buf.copy_(self.ds[i:i + 1])
+        if self.graph is not None:
+            self.graph.replay()
+            if self.on_replay is not None:
+                self.on_replay()
+            return
+        self.step_fn(self.t_buf, self.d_buf)
+        if self.use_graph:
+            self.capture()
+
+    def capture(self):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.step_fn(self.t_buf, self.d_buf)
+        self.graph = g
+
+
 class WanVideoPipeline:
     """The Ditto drop-in (wan_video_new.py:32).  DiT/VACE/Euler/CFG on libvstyler kernels."""
 
@@ -227,23 +257,42 @@ class WanVideoPipeline:
 
     # ---------------------------------------------------------------- denoise
     def denoise(self, latents, context_posi, context_nega, vace_context=None, vace_scale=1.0, cfg_scale=5.0,
-                num_inference_steps=50, sigma_shift=5.0, denoising_strength=1.0, progress_bar_cmd=None):
-        """The loop of wan_video_new.py:515-542 (cfg_merge batched), returns the final latents."""
+                num_inference_steps=50, sigma_shift=5.0, denoising_strength=1.0, progress_bar_cmd=None,
+                use_graph=None):
+        """The loop of wan_video_new.py:515-542 (cfg_merge batched), returns the final latents.
+
+        Step 0 runs eagerly (it also sizes the Workspace); the whole step -- model_fn (DiT + VACE,
+        CFG as one batch-2 forward) + fused CFG/Euler update -- is then captured once into a hipGraph
+        (torch.cuda.CUDAGraph over hipStreamBeginCapture) and replayed for every later step.  The
+        graph reads the step's bf16 timestep and fp32 dsigma from two device slots refreshed before
+        each replay, so one capture serves all steps.  Eager under Ulysses SP (RCCL collectives are
+        issued eagerly) and when use_graph=False / VSTYLER_GRAPH=0."""
         self.scheduler.set_timesteps(num_inference_steps, denoising_strength=denoising_strength, shift=sigma_shift)
+        n_steps = len(self.scheduler.timesteps)
         use_cfg = cfg_scale != 1.0
+        if use_graph is None:
+            use_graph = os.environ.get("VSTYLER_GRAPH", "1") != "0"
+        use_graph = use_graph and not self.use_unified_sequence_parallel and n_steps > 1
         ctx = torch.cat([context_posi, context_nega], 0) if use_cfg else context_posi
         latents = latents.to(device=self.device, dtype=BF16).contiguous().clone()
-        steps = range(len(self.scheduler.timesteps))
-        if progress_bar_cmd is not None:
-            steps = progress_bar_cmd(steps)
-        for i in steps:
-            timestep = self.scheduler.timesteps[i].reshape(1).to(dtype=BF16, device=self.device)
-            v = self.model_fn(dit=self.dit, vace=self.vace, latents=latents, timestep=timestep, context=ctx,
+        ts = self.scheduler.timesteps.to(dtype=BF16).to(self.device)                     # :526
+        ds = torch.tensor([self.scheduler.delta(i) for i in range(n_steps)], dtype=torch.float32,
+                          device=self.device)
+
+        def step(t_buf, d_buf):
+            v = self.model_fn(dit=self.dit, vace=self.vace, latents=latents, timestep=t_buf, context=ctx,
                               vace_context=vace_context, vace_scale=vace_scale,
                               use_unified_sequence_parallel=self.use_unified_sequence_parallel,
                               sp_group=self.sp_group)
-            K.cfg_euler(v[0:1].contiguous(), v[1:2].contiguous() if use_cfg else None, latents, cfg_scale,
-                        self.scheduler.delta(i))
+            K.cfg_euler_dev(v[0:1], v[1:2] if use_cfg else None, latents, cfg_scale, d_buf)
+
+        stepper = DenoiseStepper(step, ts, ds, use_graph)
+        steps = range(n_steps)
+        if progress_bar_cmd is not None:
+            steps = progress_bar_cmd(steps)
+        for i in steps:
+            stepper(i)
+        self.last_graph = stepper.graph
         return latents
 
     @torch.no_grad()
@@ -279,9 +328,9 @@ class WanVideoPipeline:
         if output_type == "latents":
             return latents
         if self.vae is None:
-            raise NotImplementedError("VAE decode requires a loaded Wan2.1 VAE (not available in this build)")
+            raise RuntimeError("VAE decode requires a loaded Wan2.1 VAE (or use output_type='latents')")
         video = self.vae.decode(latents, device=self.device, tiled=tiled, tile_size=tile_size, tile_stride=tile_stride)
-        return self.vae_output_to_video(video)
+        return self.vae_output_to_video(video, output_type)
 
     def encode_prompt(self, prompt):
         if self.text_encoder is None or self.prompter is None:
@@ -289,9 +338,23 @@ class WanVideoPipeline:
         return self.prompter.encode_prompt(prompt, device=self.device)
 
     def encode_vace(self, vace_video, vace_video_mask, height, width, num_frames, tiled, tile_size, tile_stride):
+        """WanVideoUnit_VACE (wan_video_new.py:861-920): 2 tiled VAE encodes + mask latents."""
         if self.vae is None:
-            raise NotImplementedError("VACE video encoding requires the Wan2.1 VAE: pass vace_context=")
-        raise NotImplementedError("VAE encode path not built yet")
+            raise RuntimeError("VACE video encoding requires a loaded Wan2.1 VAE (or pass vace_context=)")
+        from .vae import vace_context
+        if vace_video is not None and not isinstance(vace_video, torch.Tensor):
+            vace_video = list(vace_video)[:num_frames]
+        if vace_video_mask is not None and not isinstance(vace_video_mask, torch.Tensor):
+            vace_video_mask = list(vace_video_mask)[:num_frames]
+        return vace_context(self.vae, vace_video, vace_video_mask, num_frames, height, width, tiled, tile_size,
+                            tile_stride)
 
-    def vae_output_to_video(self, vae_output):
-        raise NotImplementedError("VAE output conversion not built yet")
+    def vae_output_to_video(self, vae_output, output_type="video"):
+        """BasePipeline.vae_output_to_video (utils/__init__.py:76-91): uint8 conversion on the GPU;
+        output_type "u8" returns the (T, H, W, 3) uint8 device tensor, "video" PIL images."""
+        from .vae import vae_output_to_u8
+        u8 = vae_output_to_u8(vae_output[0])
+        if output_type == "u8":
+            return u8
+        from PIL import Image
+        return [Image.fromarray(f) for f in u8.cpu().numpy()]

@@ -39,11 +39,26 @@ def get_default_group():
     return _DEFAULT
 
 
+class _Done:
+    def wait(self):
+        pass
+
+
+class _Exchange:
+    """In-flight state of one Ulysses attention (one micro-batch of one block)."""
+    __slots__ = ("q", "B", "Sl", "Hp", "cpr", "D", "chunk", "tag", "ws", "work", "work2", "recv2")
+
+
 class UlyssesGroup:
+    """overlap: split the CFG batch into per-sample micro-batches inside each block so one half's
+    all-to-alls (async on RCCL's stream) run under the other half's GEMMs / attention / FFN
+    (VSTYLER_SP_OVERLAP=0 disables)."""
+
     def __init__(self, group=None):
         self.group = group
         self.world_size = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self.overlap = os.environ.get("VSTYLER_SP_OVERLAP", "1") != "0"
 
     # -------------------------------------------------------------- layout helpers (kernels)
     def _permute(self, src, dst, batch, s_local, cpr, ld_local, jstride, mode):
@@ -56,7 +71,9 @@ class UlyssesGroup:
         TIMER.stop(ev)
 
     def _all_to_all(self, recv, send):
-        dist.all_to_all_single(recv, send, group=self.group)
+        """Asynchronous: RCCL's stream waits for the work enqueued so far on the current stream;
+        the returned handle's wait() makes the current stream wait for the exchange."""
+        return dist.all_to_all_single(recv, send, group=self.group, async_op=True)
 
     def _all_gather(self, recv, send):
         dist.all_gather_into_tensor(recv, send, group=self.group)
@@ -93,36 +110,53 @@ class UlyssesGroup:
         self._permute(packed, full, B, Sl, C, C, B * Sl * C, 2)
         return full
 
-    # -------------------------------------------------------------- attention
-    def attention(self, q, k, v, o, num_heads, batch):
-        """Local q/k/v/o [B*Sl, H*128] -> all-to-all -> attention over all S tokens for H/p heads ->
-        all-to-all back into o."""
+    # -------------------------------------------------------------- attention (3 stages)
+    def exchange_start(self, q, k, v, num_heads, batch, tag=""):
+        """Pack local q|k|v [B*Sl, H*128] per destination rank and start the all-to-all."""
         P = self.world_size
         if num_heads % P:
             raise ValueError(f"Ulysses SP needs heads % world == 0 (heads={num_heads}, world={P})")
+        e = _Exchange()
         M, D = q.shape
-        B = batch
-        Sl = M // B
-        Hp = num_heads // P
-        cpr = Hp * 128
-        ws_ = _ws_of(q)
-        chunk = B * Sl * cpr                     # elements of one tensor per rank chunk
-        send = ws_.get("sp_send", (P * 3 * chunk,))
-        recv = ws_.get("sp_recv", (P * 3 * chunk,))
+        e.q, e.B, e.D, e.tag = q, batch, D, tag
+        e.Sl = M // batch
+        e.Hp = num_heads // P
+        e.cpr = e.Hp * 128
+        e.ws = _ws_of(q)
+        e.chunk = batch * e.Sl * e.cpr                # elements of one tensor per rank chunk
+        send = e.ws.get("sp_send" + tag, (P * 3 * e.chunk,))
+        recv = e.ws.get("sp_recv" + tag, (P * 3 * e.chunk,))
         for i, t in enumerate((q, k, v)):
-            self._permute(t, send[i * chunk:], B, Sl, cpr, D, 3 * chunk, 0)
-        self._all_to_all(recv, send)
-        full = ws_.get("sp_full", (3, B * P * Sl, cpr))
+            self._permute(t, send[i * e.chunk:], batch, e.Sl, e.cpr, D, 3 * e.chunk, 0)
+        e.work = self._all_to_all(recv, send)
+        return e
+
+    def attend(self, e):
+        """Wait for q|k|v, attention over all S tokens for H/p heads, start the return exchange."""
+        P, B, Sl, cpr, D, chunk, ws = self.world_size, e.B, e.Sl, e.cpr, e.D, e.chunk, e.ws
+        e.work.wait()
+        recv = ws.get("sp_recv" + e.tag, (P * 3 * chunk,))
+        full = ws.get("sp_full" + e.tag, (3, B * P * Sl, cpr))
         for i in range(3):
             self._permute(recv[i * chunk:], full[i], B, Sl, cpr, D, 3 * chunk, 2)
-        of = ws_.get("sp_out_full", (B * P * Sl, cpr))
-        self._attention(full[0], full[1], full[2], of, Hp, B)
-        send2 = ws_.get("sp_send2", (P * chunk,))
-        recv2 = ws_.get("sp_recv2", (P * chunk,))
+        of = ws.get("sp_out_full" + e.tag, (B * P * Sl, cpr))
+        self._attention(full[0], full[1], full[2], of, e.Hp, B)
+        send2 = ws.get("sp_send2" + e.tag, (P * chunk,))
+        e.recv2 = ws.get("sp_recv2" + e.tag, (P * chunk,))
         self._permute(of, send2, B, Sl, cpr, D, chunk, 3)
-        self._all_to_all(recv2, send2)
-        self._permute(recv2, o, B, Sl, cpr, D, chunk, 1)
+        e.work2 = self._all_to_all(e.recv2, send2)
+        return e
+
+    def finish(self, e, o):
+        """Wait for the head-sharded output and scatter it back into local rows o [B*Sl, H*128]."""
+        e.work2.wait()
+        self._permute(e.recv2, o, e.B, e.Sl, e.cpr, e.D, e.chunk, 1)
         return o
+
+    def attention(self, q, k, v, o, num_heads, batch):
+        """Local q/k/v/o [B*Sl, H*128] -> all-to-all -> attention over all S tokens for H/p heads ->
+        all-to-all back into o (the three stages back to back)."""
+        return self.finish(self.attend(self.exchange_start(q, k, v, num_heads, batch)), o)
 
 
 _WS_BY_DEV = {}

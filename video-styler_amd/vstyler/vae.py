@@ -53,11 +53,16 @@ class ConvW:
         if w.dim() == 4:  # nn.Conv2d
             w = w.unsqueeze(2)
         co, ci, kt, kh, kw = w.shape
-        self.cout, self.cin, self.k = co, _r32(ci), (kt, kh, kw)
+        self.cout, self.cin, self.k, self.cin_real = co, _r32(ci), (kt, kh, kw), ci
         wp = torch.zeros((co, kt, kh, kw, self.cin), dtype=BF16, device=device)
         wp[..., :ci] = w.to(device=device, dtype=BF16).permute(0, 2, 3, 4, 1)
         self.w = wp.reshape(co, -1).contiguous()
         self.bias = None if bias is None else bias.detach().to(device=device, dtype=BF16).contiguous()
+
+
+# algorithmic FLOPs issued through conv()/batched_gemm() (real channel counts, no padding);
+# bench/probe code reads and resets it.
+FLOPS = [0]
 
 
 def conv(x, cw, out_thw, *, stride=(1, 1, 1), pad=(0, 0, 0), up2=False, t_lo=0, y=None, t_mul=1,
@@ -91,6 +96,7 @@ def conv(x, cw, out_thw, *, stride=(1, 1, 1), pad=(0, 0, 0), up2=False, t_lo=0, 
         p.res = res.data_ptr()
     p.nz = 1
     _lib.check(_lib.load().vs_vae_conv(p, _stream(x)))
+    FLOPS[0] += 2 * n * t_out * h_out * w_out * cw.cout * cw.cin_real * cw.k[0] * cw.k[1] * cw.k[2]
     return y
 
 
@@ -108,6 +114,7 @@ def batched_gemm(a, a_zs, lda, rows, k, b, b_zs, ldb, n_out, y, y_zs, ldy, nz, o
     p.t_mul, p.t_add, p.split, p.out_f32, p.alpha = 1, 0, 0, int(out_f32), alpha
     p.res, p.nz = None, nz
     _lib.check(_lib.load().vs_vae_conv(p, _stream(a)))
+    FLOPS[0] += 2 * nz * rows * n_out * k
 
 
 def rmsnorm(x, gamma, silu, out=None):
@@ -408,4 +415,46 @@ def vae_output_to_u8(video):
     _, T, H, W = video.shape
     out = torch.empty((T, H, W, 3), dtype=torch.uint8, device=video.device)
     _lib.check(_lib.load().vs_vae_to_u8(video.data_ptr(), out.data_ptr(), T, H, W, _stream(video)))
+    return out
+
+
+def frames_to_u8(frames, device):
+    """A video as the reference's pipelines receive it (list of PIL images / HxWx3 uint8 arrays, or a
+    (T, H, W, 3) uint8 tensor) -> contiguous (T, H, W, 3) uint8 on the device."""
+    if isinstance(frames, torch.Tensor):
+        t = frames
+    else:
+        import numpy as np
+        t = torch.from_numpy(np.stack([np.asarray(f.convert("RGB") if hasattr(f, "convert") else f, dtype=np.uint8)
+                                       for f in frames]))
+    if t.dtype != torch.uint8 or t.dim() != 4 or t.shape[-1] != 3:
+        raise ValueError(f"expected uint8 frames (T, H, W, 3), got {tuple(t.shape)} {t.dtype}")
+    return t.to(device).contiguous()
+
+
+def vace_context(vae, vace_video=None, vace_video_mask=None, num_frames=None, height=None, width=None,
+                 tiled=True, tile_size=(30, 52), tile_stride=(15, 26)):
+    """WanVideoUnit_VACE.process (wan_video_new.py:861-920) without reference images:
+    -> vace_context (1, 96, (T+3)//4, H/8, W/8) bf16 = [encode(inactive) | encode(reactive) | mask latents]."""
+    dev = vae.device
+    v = None if vace_video is None else frames_to_u8(vace_video, dev)
+    m = None if vace_video_mask is None else frames_to_u8(vace_video_mask, dev)
+    ref = v if v is not None else m
+    if ref is not None:
+        num_frames, height, width = ref.shape[0], ref.shape[1], ref.shape[2]
+    if v is not None and m is not None and v.shape != m.shape:
+        raise ValueError("vace_video and vace_video_mask must have the same shape")
+    T, H, W = num_frames, height, width
+    inactive = torch.empty((1, 3, T, H, W), dtype=BF16, device=dev)
+    reactive = torch.empty_like(inactive)
+    mask0 = torch.empty((T, H, W), dtype=BF16, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    lib = _lib.load()
+    _lib.check(lib.vs_vace_prepare(None if v is None else v.data_ptr(), None if m is None else m.data_ptr(),
+                                   inactive.data_ptr(), reactive.data_ptr(), mask0.data_ptr(), T, H, W, st))
+    t_lat = (T + 3) // 4
+    out = torch.empty((1, 96, t_lat, H // 8, W // 8), dtype=BF16, device=dev)
+    out[:, 0:16] = vae.encode(inactive, dev, tiled=tiled, tile_size=tile_size, tile_stride=tile_stride)
+    out[:, 16:32] = vae.encode(reactive, dev, tiled=tiled, tile_size=tile_size, tile_stride=tile_stride)
+    _lib.check(lib.vs_vace_mask_latents(mask0.data_ptr(), out[0, 32:].data_ptr(), T, H, W, t_lat, st))
     return out
