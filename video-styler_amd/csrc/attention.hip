@@ -237,6 +237,11 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
         __builtin_amdgcn_sched_barrier(0);
     };
     const int grp = wave >> 2;
+    // static priority for the younger half (waves 4-7): it loses VALU arbitration to the older
+    // half on every segment otherwise (CDNA guide T5 static form; readfirstlane keeps it scalar)
+#ifdef VS_ATTN_YOUNG_PRIO  // measured -1.2 % on MI355X (1067 vs 1080 TF/s): off
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
     if (grp == 1) phase_bar();
     auto body = [&](int it, f32x16_t* cur, f32x16_t* nxt) {
         const bool has1 = it + 1 < nkv, has2 = it + 2 < nkv, has3 = it + 3 < nkv;

@@ -203,22 +203,63 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_bf16_tn(
 // s_barrier.  64-B LDS rows, 16-B chunk swizzle c ^ ((3*(row>>2)) & 3) (conflict-free 16x16x32
 // fragment reads).
 // ---------------------------------------------------------------------------------------------
+#ifndef VS_GEMM_RING
+#define VS_GEMM_RING 4
+#endif
+#ifndef VS_GEMM_GM
+#define VS_GEMM_GM 4            // M-tiles per raster group (L2 reuse of the weight tile)
+#endif
 constexpr int BT = 256, HK = 32, NTHR8 = 512, SLOT = 2 * BT * HK * 2;   // 32 KB per slot
+constexpr int RING = VS_GEMM_RING;          // LDS slots (<= 5: 160 KB); prefetch distance RING-1
 
 __device__ __forceinline__ int h_off(int row, int ch) {
     return row * 64 + 16 * (ch ^ ((3 * (row >> 2)) & 3));
 }
 
 __device__ __forceinline__ void wait_barrier(int n_after) {
+    // The LDS-DMA of the needed half-step (vmcnt) must land before the barrier makes it visible;
+    // the wave's own fragment reads (lgkmcnt) only have to land before its MFMAs, so with
+    // this order they are waited for after the barrier (the slot they read is restaged two
+    // phases later at the earliest).  Measured +0.5..1 % (VS_GEMM_EARLY_LGKM restores the old order).
     __builtin_amdgcn_sched_barrier(0);
-    if (n_after >= 2)
+#ifndef VS_GEMM_EARLY_LGKM
+    if (n_after >= 3)
+        asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    else if (n_after == 2)
+        asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    else if (n_after == 1)
+        asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+    if (n_after >= 3)
+        asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (n_after == 2)
         asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else if (n_after == 1)
         asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
     __builtin_amdgcn_sched_barrier(0);
 }
+
+#ifdef VS_GEMM_STAMPS
+// debug: s_memtime stamps of wave 0 and wave 4 of workgroup 0 (5 per half-step, 32 half-steps)
+__device__ unsigned long long g_gemm_stamps[2][5 * 32];
+#define STAMP(slot)                                                                             \
+    do {                                                                                        \
+        if (blockIdx.x == 0 && lane == 0 && (wave & 3) == 0 && h < 32) {                        \
+            unsigned long long t_;                                                              \
+            __builtin_amdgcn_sched_barrier(0);                                                  \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+            __builtin_amdgcn_sched_barrier(0);                                                  \
+            g_gemm_stamps[wave >> 2][5 * h + (slot)] = t_;                                      \
+        }                                                                                       \
+    } while (0)
+#else
+#define STAMP(slot) do {} while (0)
+#endif
 
 __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
     const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
@@ -227,7 +268,7 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int pid = xcd_remap(blockIdx.x, gridDim.x);
-    constexpr int GM = 4;
+    constexpr int GM = VS_GEMM_GM;
     const int per_group = GM * ntn;
     const int group = pid / per_group;
     const int first_m = group * GM;
@@ -265,7 +306,7 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
     const int rbase = r0 + wn * 64 + prow;
     int issued = -1;                                // highest half-step this wave has issued
     auto issue = [&](int h) {
-        char* dst = smem + (h & 3) * SLOT + dst_off;
+        char* dst = smem + (h % RING) * SLOT + dst_off;
         const bool lora = h >= nh1;
         const bf16_t* P = (lora ? Pl : Pm) + (lora ? h - nh1 : h) * HK + pch * 8;
         const long long ld = lora ? ldl : ldm;
@@ -279,7 +320,7 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
     const int frow = lane & 15, fch = lane >> 4;
     bf16x8_t wf[4], af[8];
     auto load_frags = [&](int h) {
-        const char* As = smem + (h & 3) * SLOT;
+        const char* As = smem + (h % RING) * SLOT;
         const char* Bs = As + BT * 64;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -298,10 +339,10 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
         __builtin_amdgcn_s_setprio(0);
     };
 
-    // prologue: half-steps 0..2 in flight, then wait for half-step 0
-    issue(0);
-    if (nh > 1) issue(1);
-    if (nh > 2) issue(2);
+    // prologue: half-steps 0..RING-2 in flight, then wait for half-step 0
+#pragma unroll
+    for (int j = 0; j < RING - 1; ++j)
+        if (j < nh) issue(j);
     wait_barrier(issued);                           // needed = 0
     // Every wave runs the same body [L(h); barrier; C(h); barrier]; group 1 executes one extra
     // barrier first, so its L phases coincide with group 0's C phases (s_barrier counts arrivals,
@@ -315,11 +356,16 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
     if (wm == 1) bar();
 #pragma nounroll
     for (int h = 0; h < nh; ++h) {
+        STAMP(0);
         load_frags(h);
-        if (h + 3 < nh) issue(h + 3);
+        if (h + RING - 1 < nh) issue(h + RING - 1);
+        STAMP(1);
         bar();
+        STAMP(2);
         mfmas();
+        STAMP(3);
         bar();
+        STAMP(4);
     }
     if (wm == 0) bar();
 
@@ -340,6 +386,12 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
 
 }  // namespace
+
+#ifdef VS_GEMM_STAMPS
+extern "C" int vs_debug_gemm_stamps(unsigned long long* host_out) {
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_gemm_stamps), sizeof(g_gemm_stamps)) == hipSuccess ? 0 : 2;
+}
+#endif
 
 extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ldw, void* c,
                        long long ldc, int m, int n, int k, int epilogue, const vs_epilogue* epi,
@@ -389,10 +441,10 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
         static bool attr256 = false;
         if (!attr256) {
             (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_256,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 4 * SLOT);
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, RING * SLOT);
             attr256 = true;
         }
-        hipLaunchKernelGGL(gemm_bf16_tn_256, dim3((unsigned)(tm * tn)), dim3(NTHR8), 4 * SLOT,
+        hipLaunchKernelGGL(gemm_bf16_tn_256, dim3((unsigned)(tm * tn)), dim3(NTHR8), RING * SLOT,
                            (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw,
                            (bf16_t*)c, ldc, m, n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2,
                            k2, ep, tm, tn);
