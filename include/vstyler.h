@@ -57,6 +57,19 @@ int vs_gemm(const void* a, long long lda, const void* w, long long ldw, void* c,
             const void* a2, long long lda2, const void* w2, long long ldw2, int k2, void* stream);
 
 /*
+ * fp8 path (config 5; AutoWrappedLinear.fp8_linear, diffsynth/vram_management/layers.py:115-151):
+ * vs_quant_fp8_rows quantises activations per row, s[m] = max(max_k |x[m][k]| / 448, 1),
+ * x8 = e4m3fn(x / (s + 1e-8)) (OCP e4m3, round-to-nearest-even); vs_gemm_fp8 computes
+ * C = epilogue(s[m] * (A8 . W8^T)) with unscaled e4m3 weights W8 [N][K] (scale_b = 1, as the
+ * reference) and the same epilogues as vs_gemm (bias added in fp32 before the single bf16 rounding,
+ * as torch._scaled_mm).  K % 64 == 0, N % 4 == 0, lda/ldw multiples of 16 bytes.
+ */
+int vs_quant_fp8_rows(const void* x, long long ldx, void* x8, long long ld8, float* scale, int rows, int cols,
+                      void* stream);
+int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, const void* w8, long long ldw, void* c,
+                long long ldc, int m, int n, int k, int epilogue, const vs_epilogue* epi, void* stream);
+
+/*
  * O = softmax(Q K^T * scale) V per (batch, head), non-causal, no mask.  head_dim must be 128.
  * Q: [batch][sq] rows of stride ldq (head h at columns h*128..), K/V: [batch][skv], O like Q.
  * Replaces flash_attention() / AttentionModule.forward (diffsynth/models/wan_video_dit.py:28-61,

@@ -156,6 +156,15 @@ def linear(x, w, b=None):
     return bf(y)
 
 
+# fp8 path switch (config 5): when True, every Linear inside a DiT/VACE block runs as
+# AutoWrappedLinear.fp8_linear (vram_management/layers.py:115-151); embeddings/head stay bf16.
+FP8_BLOCK_LINEARS = False
+
+
+def blk_linear(x, w, b=None):
+    return fp8_linear(x, w, b) if FP8_BLOCK_LINEARS else linear(x, w, b)
+
+
 def gelu_tanh(x):
     return bf(F.gelu(x.float(), approximate="tanh"))
 
@@ -186,22 +195,22 @@ def attention_rows(q, k, v, num_heads, rows):
 # --------------------------------------------------------------------------------------
 def self_attention(x, freqs, W, p, num_heads, eps=1e-6):
     """SelfAttention.forward, wan_video_dit.py:140-147."""
-    q = rms_norm(linear(x, W[p + "q.weight"], W[p + "q.bias"]), W[p + "norm_q.weight"], eps)
-    k = rms_norm(linear(x, W[p + "k.weight"], W[p + "k.bias"]), W[p + "norm_k.weight"], eps)
-    v = linear(x, W[p + "v.weight"], W[p + "v.bias"])
+    q = rms_norm(blk_linear(x, W[p + "q.weight"], W[p + "q.bias"]), W[p + "norm_q.weight"], eps)
+    k = rms_norm(blk_linear(x, W[p + "k.weight"], W[p + "k.bias"]), W[p + "norm_k.weight"], eps)
+    v = blk_linear(x, W[p + "v.weight"], W[p + "v.bias"])
     q = rope_apply(q, freqs, num_heads)
     k = rope_apply(k, freqs, num_heads)
     o = attention(q, k, v, num_heads)
-    return linear(o, W[p + "o.weight"], W[p + "o.bias"])
+    return blk_linear(o, W[p + "o.weight"], W[p + "o.bias"])
 
 
 def cross_attention(x, ctx, W, p, num_heads, eps=1e-6):
     """CrossAttention.forward (has_image_input=False), wan_video_dit.py:171-186."""
-    q = rms_norm(linear(x, W[p + "q.weight"], W[p + "q.bias"]), W[p + "norm_q.weight"], eps)
-    k = rms_norm(linear(ctx, W[p + "k.weight"], W[p + "k.bias"]), W[p + "norm_k.weight"], eps)
-    v = linear(ctx, W[p + "v.weight"], W[p + "v.bias"])
+    q = rms_norm(blk_linear(x, W[p + "q.weight"], W[p + "q.bias"]), W[p + "norm_q.weight"], eps)
+    k = rms_norm(blk_linear(ctx, W[p + "k.weight"], W[p + "k.bias"]), W[p + "norm_k.weight"], eps)
+    v = blk_linear(ctx, W[p + "v.weight"], W[p + "v.bias"])
     o = attention(q, k, v, num_heads)
-    return linear(o, W[p + "o.weight"], W[p + "o.bias"])
+    return blk_linear(o, W[p + "o.weight"], W[p + "o.bias"])
 
 
 def dit_block(x, ctx, t_mod, freqs, W, p, num_heads, eps=1e-6):
@@ -213,7 +222,7 @@ def dit_block(x, ctx, t_mod, freqs, W, p, num_heads, eps=1e-6):
     h = layer_norm(x, eps, W[p + "norm3.weight"], W[p + "norm3.bias"])
     x = add(x, cross_attention(h, ctx, W, p + "cross_attn.", num_heads, eps))   # :227
     h = modulate(layer_norm(x, eps), shift_mlp, scale_mlp)        # :228
-    f = linear(gelu_tanh(linear(h, W[p + "ffn.0.weight"], W[p + "ffn.0.bias"])),
+    f = blk_linear(gelu_tanh(blk_linear(h, W[p + "ffn.0.weight"], W[p + "ffn.0.bias"])),
                W[p + "ffn.2.weight"], W[p + "ffn.2.bias"])
     return gate_residual(x, gate_mlp, f)                           # :229
 
@@ -306,6 +315,31 @@ def denoise(W, cfg, latents, context_pos, context_neg, vace_context=None, num_in
         else:
             latents = bf(latents.float() + bf(vp.float() * euler_delta(sigmas, i)).float())
     return latents
+
+
+# --------------------------------------------------------------------------------------
+# fp8 linear (AutoWrappedLinear.fp8_linear, vram_management/layers.py:115-151; e4m3fn, OCP)
+# --------------------------------------------------------------------------------------
+def fp8_quant_rows(x):
+    """layers.py:124-135: scale_a = clamp(rowmax|x| / 448, min=1) (fp32), x8 = (x / (scale_a + 1e-8))
+    cast to float8_e4m3fn.  Returns (x8 as float8_e4m3fn, scale_a [M, 1] fp32)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    x_max = torch.max(torch.abs(x2), dim=-1, keepdim=True).values
+    scale_a = torch.clamp(x_max.float() / 448.0, min=1.0)
+    x8 = (x2.float() / (scale_a + 1e-8)).to(torch.float8_e4m3fn)
+    return x8, scale_a
+
+
+def fp8_linear(x, w, b):
+    """layers.py:115-151 with torch._scaled_mm restated: (x8 . w8^T) * scale_a * 1 + bias in fp32,
+    one bf16 rounding.  w is the bf16 weight (cast to e4m3fn, :133) or already e4m3fn."""
+    x8, sa = fp8_quant_rows(x)
+    w8 = w if w.dtype == torch.float8_e4m3fn else w.to(torch.float8_e4m3fn)
+    acc = x8.to(ACC_DTYPE) @ w8.to(ACC_DTYPE).T
+    out = acc * sa.to(ACC_DTYPE)
+    if b is not None:
+        out = out + b.to(ACC_DTYPE)
+    return out.to(BF16).reshape(*x.shape[:-1], w.shape[0])
 
 
 # --------------------------------------------------------------------------------------

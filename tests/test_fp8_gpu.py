@@ -1,0 +1,111 @@
+"""GPU parity of the fp8 path (config 5) against the oracle's restatement of
+AutoWrappedLinear.fp8_linear (diffsynth/vram_management/layers.py:115-151).
+
+Quantisation: bit-exact (scale and every e4m3 byte).  GEMM: bit-exact on integer-valued operands
+(exact fp32 sums: pins the MFMA operand layout), and on random data within the bf16 rounding of a
+differently ordered fp32 sum.  Model: tiny DiT+VACE with fp8 block linears vs the oracle with
+FP8_BLOCK_LINEARS, within 1.5x the oracle's own fp32-vs-fp64 noise floor."""
+import pytest
+import torch
+
+from gpu_util import err
+from oracle import wan_oracle as O
+
+pytestmark = pytest.mark.gpu
+BF16 = torch.bfloat16
+
+
+def _k():
+    from vstyler import kernels as K
+    return K
+
+
+def test_quant_fp8_rows_bit_exact():
+    K = _k()
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(300, 640, generator=g)
+    x[::3] *= 1000.0           # rows with max > 448: scale > 1
+    x[1::7] *= 1e-3            # e4m3 subnormal range
+    x = x.to(BF16)
+    ref8, ref_s = O.fp8_quant_rows(x)
+    x8 = torch.empty(300, 640, dtype=torch.uint8, device="cuda")
+    sc = torch.empty(300, dtype=torch.float32, device="cuda")
+    K.quant_fp8_rows(x.cuda(), x8, sc)
+    assert torch.equal(sc.cpu(), ref_s[:, 0])
+    assert torch.equal(x8.cpu(), ref8.view(torch.uint8))
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 64), (300, 520, 192), (1000, 768, 640)])
+def test_gemm_fp8_integer_exact(M, N, Kd):
+    """Integer operands (exact in e4m3, exact fp32 sums) -> the result must match bit for bit."""
+    K = _k()
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randint(-4, 5, (M, Kd), generator=g).to(BF16)
+    w = torch.randint(-3, 4, (N, Kd), generator=g).to(BF16)
+    ref = O.fp8_linear(x, w, None)
+    x8 = torch.empty(M, Kd, dtype=torch.uint8, device="cuda")
+    sc = torch.empty(M, dtype=torch.float32, device="cuda")
+    K.quant_fp8_rows(x.cuda(), x8, sc)
+    out = torch.empty(M, N, dtype=BF16, device="cuda")
+    K.gemm_fp8(x8, sc, w.to(torch.float8_e4m3fn).view(torch.uint8).cuda(), out)
+    assert torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("epi", ["bias", "gelu", "gate_res"])
+def test_gemm_fp8_random_epilogues(epi):
+    K = _k()
+    M, N, Kd = 700, 1024, 1536
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(M, Kd, generator=g).to(BF16)
+    w = (0.03 * torch.randn(N, Kd, generator=g)).to(BF16)
+    b = (0.1 * torch.randn(N, generator=g)).to(BF16)
+    y = O.fp8_linear(x, w, b)
+    kw = dict(bias=b.cuda())
+    if epi == "gelu":
+        ref = O.gelu_tanh(y)
+        kw["epilogue"] = K.VS_EPI_GELU
+    elif epi == "gate_res":
+        res = torch.randn(M, N, generator=g).to(BF16)
+        gate = torch.randn(1, N, generator=g).to(BF16)
+        ref = O.gate_residual(res, gate, y)
+        kw.update(epilogue=K.VS_EPI_GATE_RES, residual=res.cuda(), gate=gate.cuda(), gate_bstride=N)
+    else:
+        ref = y
+    x8 = torch.empty(M, Kd, dtype=torch.uint8, device="cuda")
+    sc = torch.empty(M, dtype=torch.float32, device="cuda")
+    K.quant_fp8_rows(x.cuda(), x8, sc)
+    out = torch.empty(M, N, dtype=BF16, device="cuda")
+    if epi == "gate_res":
+        out.copy_(kw["residual"])
+        kw["residual"] = out
+    K.gemm_fp8(x8, sc, w.to(torch.float8_e4m3fn).view(torch.uint8).cuda(), out, **kw)
+    d = (out.cpu().float() - ref.float()).abs()
+    ulp = ref.float().abs().clamp_min(1e-3) * 2.0 ** -7
+    assert (d <= 2 * ulp).float().mean().item() > 0.999, d.max().item()
+    assert (out.cpu() == ref).float().mean().item() > 0.95
+
+
+def test_model_fn_fp8_tiny_vs_oracle():
+    from test_model_gpu import build
+    from vstyler import model_fn_wan_video
+    from vstyler.models import quantize_fp8_
+    cfg = O.WAN_CONFIGS["tiny"]
+    W = O.random_weights(cfg, seed=5)
+    dit, vace = build(cfg, W)
+    assert quantize_fp8_(dit) + quantize_fp8_(vace) == 10 * (cfg["num_layers"] + len(cfg["vace_layers"]))
+    lat, cp, cn, vc = O.synthetic_inputs(cfg, 5, 128, 128)
+    t = torch.tensor([900.0]).to(BF16)
+    old, oldacc = O.FP8_BLOCK_LINEARS, O.ACC_DTYPE
+    try:
+        O.FP8_BLOCK_LINEARS = True
+        ref = O.model_fn(W, cfg, lat, t, cp, vc)
+        O.ACC_DTYPE = torch.float64
+        ref64 = O.model_fn(W, cfg, lat, t, cp, vc)
+    finally:
+        O.FP8_BLOCK_LINEARS, O.ACC_DTYPE = old, oldacc
+    out = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t.cuda(), context=cp.cuda(),
+                             vace_context=vc.cuda())
+    fmx, frl = err(ref64, ref)
+    mx, rl = err(out, ref)
+    print(f"fp8 tiny forward: max-abs {mx:.4g} rel-L2 {rl:.4g} (floor {fmx:.4g} / {frl:.4g})")
+    assert rl <= 1.5 * frl + 2e-3 and mx <= 1.5 * fmx + 2e-2

@@ -382,6 +382,174 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// fp8 e4m3 (OCP) GEMM for the fp8 path (config 5; AutoWrappedLinear.fp8_linear,
+// diffsynth/vram_management/layers.py:115-151): C = epilogue(scale_a[m] * (A8 . W8^T)) with the
+// activations quantised per row by vs_quant_fp8_rows and unscaled fp8 weights (scale_b = 1).
+// Same 256x256 ping-pong skeleton as gemm_bf16_tn_256: a slot row holds 64 fp8 (64 B), so the
+// LDS ring, LDS-DMA pieces and swizzle are unchanged; each half-step is 8 MX-rate
+// v_mfma_scale_f32_32x32x64_f8f6f4 per wave (unit E8M0 scales) = twice the bf16 FLOPs in the same
+// MFMA cycles.  The product is formed transposed (D[n][m] = W8 . A8^T) so each lane owns 4
+// consecutive output columns per register group and the bf16 epilogue is reused unchanged.
+// ---------------------------------------------------------------------------------------------
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+
+__global__ __launch_bounds__(NTHR8, 2) void gemm_fp8_tn_256(
+    const uint8_t* __restrict__ A, long long lda, const float* __restrict__ scale_a,
+    const uint8_t* __restrict__ W, long long ldw, bf16_t* C, long long ldc, int M, int N, int K, Epi ep,
+    int ntm, int ntn) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int pid = xcd_remap(blockIdx.x, gridDim.x);
+    constexpr int GM = VS_GEMM_GM;
+    const int per_group = GM * ntn;
+    const int group = pid / per_group;
+    const int first_m = group * GM;
+    const int gsz = min(ntm - first_m, GM);
+    const int in_g = pid % per_group;
+    const int tm = first_m + in_g % gsz;
+    const int tn = in_g / gsz;
+    const int m0 = tm * BT, n0 = tn * BT;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+
+    f32x16_t acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int prow = lane >> 2;
+    const int pch = (lane & 3) ^ ((3 * (prow >> 2)) & 3);
+    constexpr int HB = 64;                            // fp8 per half-step = bytes per slot row
+    const int nh = K / HB;
+    const uint8_t* P = wm == 0 ? A : W;
+    const long long ld = wm == 0 ? lda : ldw;
+    const int lim = (wm == 0 ? M : N) - 1;
+    const int r0 = wm == 0 ? m0 : n0;
+    const int dst_off = wm * (BT * 64) + wn * 4 * 1024;
+    const int rbase = r0 + wn * 64 + prow;
+    int issued = -1;
+    auto issue = [&](int h) {
+        char* dst = smem + (h % RING) * SLOT + dst_off;
+        const uint8_t* src = P + (long long)h * HB + pch * 16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_global_load_lds((const GLB_AS void*)(src + (long long)min(rbase + j * 16, lim) * ld),
+                                             (LDS_AS void*)(dst + j * 1024), 16, 0, 0);
+        issued = h;
+    };
+
+    // fragments: lane (r = l&31, hf = l>>5) holds row r, k = 32 hf .. 32 hf + 31 (chunks 2hf, 2hf+1)
+    const int fr = lane & 31, fh = lane >> 5;
+    i32x8_t wfr[2], afr[4];
+    auto load_frags = [&](int h) {
+        const char* As = smem + (h % RING) * SLOT;
+        const char* Bs = As + BT * 64;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int row = wn * 64 + j * 32 + fr;
+            const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(Bs + h_off(row, 2 * fh));
+            const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(Bs + h_off(row, 2 * fh + 1));
+            wfr[j] = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = wm * 128 + i * 32 + fr;
+            const u32x4_t lo = *reinterpret_cast<const u32x4_t*>(As + h_off(row, 2 * fh));
+            const u32x4_t hi = *reinterpret_cast<const u32x4_t*>(As + h_off(row, 2 * fh + 1));
+            afr[i] = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+        }
+    };
+    auto mfmas = [&]() {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wfr[j], afr[i], acc[i][j], 0, 0, 0, 0x7f,
+                                                                           0, 0x7f);
+        __builtin_amdgcn_s_setprio(0);
+    };
+
+#pragma unroll
+    for (int j = 0; j < RING - 1; ++j)
+        if (j < nh) issue(j);
+    wait_barrier(issued);
+    int q = 0;
+    auto bar = [&]() {
+        wait_barrier(issued - min((q + 1) >> 1, nh - 1));
+        ++q;
+    };
+    if (wm == 1) bar();
+#pragma nounroll
+    for (int h = 0; h < nh; ++h) {
+        load_frags(h);
+        if (h + RING - 1 < nh) issue(h + RING - 1);
+        bar();
+        mfmas();
+        bar();
+    }
+    if (wm == 0) bar();
+
+    // D[n][m]: lane column m = m0 + wm*128 + 32i + (l&31); rows n = n0 + wn*64 + 32j + 8g + 4hf + {0..3}
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * 128 + i * 32 + fr;
+        if (m >= M) continue;
+        const float sa = scale_a[m];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n = n0 + wn * 64 + j * 32 + 8 * g + 4 * fh;
+                if (n >= N) continue;
+                const f32x4_t a = f32x4_t{acc[i][j][4 * g] * sa, acc[i][j][4 * g + 1] * sa, acc[i][j][4 * g + 2] * sa,
+                                          acc[i][j][4 * g + 3] * sa};
+                epilogue_store(a, m, n, C, ldc, ep);
+            }
+    }
+}
+
+// Per-row activation quantisation of fp8_linear (layers.py:124-137): s = max(max|x| / 448, 1),
+// x8 = e4m3(x / (s + 1e-8)) (fp32 division, round-to-nearest-even), one wave per row.
+__global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __restrict__ x, long long ldx,
+                                                             uint8_t* __restrict__ x8, long long ld8,
+                                                             float* __restrict__ scale, int rows, int cols) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    const bf16_t* xr = x + (long long)row * ldx;
+    float mx = 0.f;
+    for (int c = lane * 8; c < cols; c += 512) {
+        const u32x4_t w = *reinterpret_cast<const u32x4_t*>(xr + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(bflo(w[e])), fabsf(bfhi(w[e]))));
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    const float s = fmaxf(mx / 448.0f, 1.0f);
+    const float d = s + 1e-8f;
+    if (lane == 0) scale[row] = s;
+    uint8_t* yr = x8 + (long long)row * ld8;
+    for (int c = lane * 8; c < cols; c += 512) {
+        const u32x4_t w = *reinterpret_cast<const u32x4_t*>(xr + c);
+        u32x2_t o;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            int v = __builtin_amdgcn_cvt_pk_fp8_f32(bflo(w[2 * e]) / d, bfhi(w[2 * e]) / d, 0, false);
+            v = __builtin_amdgcn_cvt_pk_fp8_f32(bflo(w[2 * e + 1]) / d, bfhi(w[2 * e + 1]) / d, v, true);
+            o[e] = (uint32_t)v;
+        }
+        *reinterpret_cast<u32x2_t*>(yr + c) = o;
+    }
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7) == 0; }
 
@@ -393,20 +561,9 @@ extern "C" int vs_debug_gemm_stamps(unsigned long long* host_out) {
 }
 #endif
 
-extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ldw, void* c,
-                       long long ldc, int m, int n, int k, int epilogue, const vs_epilogue* epi,
-                       const void* a2, long long lda2, const void* w2, long long ldw2, int k2,
-                       void* stream) {
-    if (!a || !w || !c || m <= 0 || n <= 0 || k <= 0) return VS_E_INVALID;
-    if (k % BK || k2 % BK || k2 < 0 || n % 4) return VS_E_INVALID;
-    if (lda < k || ldw < k || ldc < n || (lda & 7) || (ldw & 7) || (ldc & 3)) return VS_E_INVALID;
-    if (!aligned16(a) || !aligned16(w) || !aligned8(c)) return VS_E_INVALID;
-    if (k2 > 0) {
-        if (!a2 || !w2 || lda2 < k2 || ldw2 < k2 || (lda2 & 7) || (ldw2 & 7)) return VS_E_INVALID;
-        if (!aligned16(a2) || !aligned16(w2)) return VS_E_INVALID;
-    }
+static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n) {
     if (epilogue < VS_EPI_BIAS || epilogue > VS_EPI_RES) return VS_E_INVALID;
-    Epi ep{};
+    ep = Epi{};
     ep.mode = epilogue;
     ep.rows_per_batch = m;
     ep.alpha = 1.f;
@@ -423,10 +580,28 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
         ep.alpha = epi->alpha;
         if (epi->rows_per_batch > 0) ep.rows_per_batch = epi->rows_per_batch;
     }
-    if ((epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES) && (!ep.res || ep.ld_res < n))
-        return VS_E_INVALID;
+    if ((epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES) && (!ep.res || ep.ld_res < n)) return VS_E_INVALID;
     if (epilogue == VS_EPI_GATE_RES && !ep.gate) return VS_E_INVALID;
     if (ep.hint && ep.ld_hint < n) return VS_E_INVALID;
+    return VS_OK;
+}
+
+
+extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ldw, void* c,
+                       long long ldc, int m, int n, int k, int epilogue, const vs_epilogue* epi,
+                       const void* a2, long long lda2, const void* w2, long long ldw2, int k2,
+                       void* stream) {
+    if (!a || !w || !c || m <= 0 || n <= 0 || k <= 0) return VS_E_INVALID;
+    if (k % BK || k2 % BK || k2 < 0 || n % 4) return VS_E_INVALID;
+    if (lda < k || ldw < k || ldc < n || (lda & 7) || (ldw & 7) || (ldc & 3)) return VS_E_INVALID;
+    if (!aligned16(a) || !aligned16(w) || !aligned8(c)) return VS_E_INVALID;
+    if (k2 > 0) {
+        if (!a2 || !w2 || lda2 < k2 || ldw2 < k2 || (lda2 & 7) || (ldw2 & 7)) return VS_E_INVALID;
+        if (!aligned16(a2) || !aligned16(w2)) return VS_E_INVALID;
+    }
+    Epi ep;
+    const int rc = fill_epi(ep, epilogue, epi, m, n);
+    if (rc) return rc;
     // 256x256 schedule once there are enough tiles to fill the chip, 128x128 otherwise
     // (VSTYLER_GEMM_TILE=128|256 forces one for A/B measurements)
     static int force = -1;
@@ -464,6 +639,41 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
                        (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw,
                        (bf16_t*)c, ldc, m, n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2,
                        k2, ep, ntm, ntn);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, const void* w8, long long ldw,
+                           void* c, long long ldc, int m, int n, int k, int epilogue, const vs_epilogue* epi,
+                           void* stream) {
+    if (!a8 || !scale_a || !w8 || !c || m <= 0 || n <= 0 || k <= 0) return VS_E_INVALID;
+    if (k % 64 || n % 4 || lda < k || ldw < k || ldc < n || (lda & 15) || (ldw & 15) || (ldc & 3))
+        return VS_E_INVALID;
+    if (!aligned16(a8) || !aligned16(w8) || !aligned8(c)) return VS_E_INVALID;
+    Epi ep;
+    const int rc = fill_epi(ep, epilogue, epi, m, n);
+    if (rc) return rc;
+    const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gemm_fp8_tn_256, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  RING * SLOT);
+        attr = true;
+    }
+    hipLaunchKernelGGL(gemm_fp8_tn_256, dim3((unsigned)(tm * tn)), dim3(NTHR8), RING * SLOT, (hipStream_t)stream,
+                       (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c, ldc, m, n, k, ep, tm,
+                       tn);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_quant_fp8_rows(const void* x, long long ldx, void* x8, long long ld8, float* scale, int rows,
+                                 int cols, void* stream) {
+    if (!x || !x8 || !scale || rows <= 0 || cols <= 0 || cols % 8 || ldx < cols || ld8 < cols || (ldx & 7) ||
+        (ld8 & 7) || !aligned16(x) || !aligned8(x8))
+        return VS_E_INVALID;
+    hipLaunchKernelGGL(quant_fp8_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, ldx, (uint8_t*)x8, ld8, scale, rows, cols);
     VS_CHECK_LAUNCH();
     return VS_OK;
 }

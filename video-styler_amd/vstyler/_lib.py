@@ -54,6 +54,8 @@ SIGNATURES = {
     "vs_strerror": [_I],
     "vs_gemm": [_P, _LL, _P, _LL, _P, _LL, _I, _I, _I, _I, ctypes.POINTER(VsEpilogue),
                 _P, _LL, _P, _LL, _I, _P],
+    "vs_quant_fp8_rows": [_P, _LL, _P, _LL, _P, _I, _I, _P],
+    "vs_gemm_fp8": [_P, _LL, _P, _P, _LL, _P, _LL, _I, _I, _I, _I, ctypes.POINTER(VsEpilogue), _P],
     "vs_attn_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _LL, _LL, _LL, _LL, _LL, _LL, _LL, _LL,
                     _F, _P],
     "vs_layernorm_modulate": [_P, _LL, _P, _LL, _I, _I, _I, _P, _P, _LL, _P, _P, _F, _P],

@@ -46,6 +46,23 @@ def _ptr(t):
     return None if t is None else t.data_ptr()
 
 
+def _epilogue(bias, residual, gate, gate_bstride, hint, hint_scale, alpha, rows_per_batch):
+    ep = VsEpilogue()
+    ep.bias = _ptr(bias)
+    ep.hint_scale = float(hint_scale)
+    ep.alpha = float(alpha)
+    ep.rows_per_batch = int(rows_per_batch)
+    if residual is not None:
+        _, _, ldr = _rows(residual, "residual")
+        ep.residual, ep.ld_res = residual.data_ptr(), ldr
+    if gate is not None:
+        ep.gate, ep.gate_bstride = gate.data_ptr(), int(gate_bstride)
+    if hint is not None:
+        _, _, ldh = _rows(hint, "hint")
+        ep.hint, ep.ld_hint = hint.data_ptr(), ldh
+    return ep
+
+
 def gemm(a, w, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, gate_bstride=0,
          hint=None, hint_scale=1.0, alpha=1.0, rows_per_batch=0, a2=None, w2=None):
     """out[M,N] = epilogue(a[M,K] @ w[N,K]^T (+ a2 @ w2^T)) (see include/vstyler.h vs_gemm)."""
@@ -54,25 +71,44 @@ def gemm(a, w, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, g
     Mo, No, ldc = _rows(out, "out")
     if Kw != K or Mo != M or No != N:
         raise ValueError(f"gemm shape mismatch a={tuple(a.shape)} w={tuple(w.shape)} out={tuple(out.shape)}")
-    ep = VsEpilogue()
-    ep.bias = _ptr(bias)
-    ep.hint_scale = float(hint_scale)
-    ep.alpha = float(alpha)
-    ep.rows_per_batch = int(rows_per_batch)
-    if residual is not None:
-        _, Nr, ldr = _rows(residual, "residual")
-        ep.residual, ep.ld_res = residual.data_ptr(), ldr
-    if gate is not None:
-        ep.gate, ep.gate_bstride = gate.data_ptr(), int(gate_bstride)
-    if hint is not None:
-        _, _, ldh = _rows(hint, "hint")
-        ep.hint, ep.ld_hint = hint.data_ptr(), ldh
+    ep = _epilogue(bias, residual, gate, gate_bstride, hint, hint_scale, alpha, rows_per_batch)
     k2, lda2, ldw2 = 0, 0, 0
     if a2 is not None:
         _, k2, lda2 = _rows(a2, "a2")
         _, _, ldw2 = _rows(w2, "w2")
     _lib.check(_lib.load().vs_gemm(a.data_ptr(), lda, w.data_ptr(), ldw, out.data_ptr(), ldc, M, N, K,
                                    int(epilogue), ep, _ptr(a2), lda2, _ptr(w2), ldw2, k2, _stream(a)))
+    return out
+
+
+def _rows_u8(t, name):
+    if t.dtype != torch.uint8 or not t.is_cuda or t.dim() != 2 or t.stride(-1) != 1:
+        raise ValueError(f"{name}: expected a 2-D row-major uint8 (e4m3 bits) device tensor")
+    return t.shape[0], t.shape[1], t.stride(0)
+
+
+def quant_fp8_rows(x, x8, scale):
+    """x8 (uint8 e4m3 bits) and per-row fp32 scale of x, as fp8_linear (layers.py:124-137)."""
+    M, K, ldx = _rows(x, "x")
+    M8, K8, ld8 = _rows_u8(x8, "x8")
+    if (M8, K8) != (M, K) or scale.dtype != torch.float32 or scale.numel() < M:
+        raise ValueError("quant_fp8_rows: shape mismatch")
+    _lib.check(_lib.load().vs_quant_fp8_rows(x.data_ptr(), ldx, x8.data_ptr(), ld8, scale.data_ptr(), M, K,
+                                             _stream(x)))
+    return x8, scale
+
+
+def gemm_fp8(a8, scale_a, w8, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, gate_bstride=0,
+             hint=None, hint_scale=1.0, alpha=1.0, rows_per_batch=0):
+    """out = epilogue(scale_a[m] * (a8 @ w8^T)) with e4m3 operands (see vs_gemm_fp8)."""
+    M, K, lda = _rows_u8(a8, "a8")
+    N, Kw, ldw = _rows_u8(w8, "w8")
+    Mo, No, ldc = _rows(out, "out")
+    if Kw != K or Mo != M or No != N or scale_a.dtype != torch.float32:
+        raise ValueError(f"gemm_fp8 shape mismatch a8={tuple(a8.shape)} w8={tuple(w8.shape)} out={tuple(out.shape)}")
+    ep = _epilogue(bias, residual, gate, gate_bstride, hint, hint_scale, alpha, rows_per_batch)
+    _lib.check(_lib.load().vs_gemm_fp8(a8.data_ptr(), lda, scale_a.data_ptr(), w8.data_ptr(), ldw, out.data_ptr(),
+                                       ldc, M, N, K, int(epilogue), ep, _stream(a8)))
     return out
 
 

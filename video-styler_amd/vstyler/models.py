@@ -34,7 +34,18 @@ class Linear(nn.Module):
 
 def linear(lin, x, out, ws, **epi):
     """Linear through vs_gemm; a hot-loaded LoRA (lin.lora_A = alpha*A, lin.lora_B = B) is fused as
-    the GEMM's second K phase (AutoWrappedLinear, vram_management/layers.py:173-188)."""
+    the GEMM's second K phase (AutoWrappedLinear, vram_management/layers.py:173-188).  A layer
+    converted by quantize_fp8_ runs the fp8 path of AutoWrappedLinear.fp8_linear (:115-151):
+    per-row activation quantisation + e4m3 MFMA GEMM with the same fused epilogue."""
+    w8 = getattr(lin, "weight_fp8", None)
+    if w8 is not None:
+        if getattr(lin, "lora_A", None) is not None:
+            raise NotImplementedError("hot-loaded LoRA on an fp8 layer: merge the LoRA before quantize_fp8_")
+        M, Kd = x.shape
+        x8 = ws.get("fp8_x", (M, Kd), torch.uint8)
+        sc = ws.get("fp8_scale", (M,), torch.float32)
+        K.quant_fp8_rows(x, x8, sc)
+        return K.gemm_fp8(x8, sc, w8, out, bias=lin.bias, **epi)
     la = getattr(lin, "lora_A", None)
     a2 = w2 = None
     if la is not None:
@@ -42,6 +53,19 @@ def linear(lin, x, out, ws, **epi):
         K.gemm(x, la, t)
         a2, w2 = t, lin.lora_B
     return K.gemm(x, lin.weight, out, bias=lin.bias, a2=a2, w2=w2, **epi)
+
+
+def quantize_fp8_(module):
+    """Give every block Linear (self/cross-attention q/k/v/o, FFN; DiT and VACE blocks) an e4m3fn
+    copy of its weight (weight.to(float8_e4m3fn), as fp8_linear casts it, layers.py:133) used by
+    linear(); embeddings, VACE before/after projections and the head stay bf16."""
+    n = 0
+    for blk in [m for m in module.modules() if isinstance(m, DiTBlock)]:
+        for lin in (blk.self_attn.q, blk.self_attn.k, blk.self_attn.v, blk.self_attn.o, blk.cross_attn.q,
+                    blk.cross_attn.k, blk.cross_attn.v, blk.cross_attn.o, blk.ffn[0], blk.ffn[2]):
+            lin.weight_fp8 = lin.weight.detach().to(torch.float8_e4m3fn).view(torch.uint8).contiguous()
+            n += 1
+    return n
 
 
 class PatchEmbed(nn.Module):
