@@ -111,6 +111,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=1024)
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
+    ap.add_argument("--config", default="bf16", choices=("bf16", "fp8"),
+                    help="bf16: BASELINE config (50-step Euler, CFG 5); fp8: config 5 (fp8 block linears, "
+                         "UniPC, CFG 1.2, shift 2, SLG block 2, VACE strength 0.975)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -152,42 +155,69 @@ def main():
     vc = torch.ones(1, 96, T, Hl, Wl)
     vc[:, :32] = torch.randn(1, 32, T, Hl, Wl, generator=g)
     vc = vc.to(torch.bfloat16).to(dev)
-    sched = FlowMatchScheduler(shift=5, sigma_min=0.0, extra_one_step=True)
-    n_total = args.warmup + args.steps
-    sched.set_timesteps(max(n_total, 2), shift=5.0)
-    ts = sched.timesteps.to(torch.bfloat16).to(dev)
-    ds = torch.tensor([sched.delta(i) for i in range(len(sched.timesteps))], dtype=torch.float32, device=dev)
-
-    def step_fn(t_buf, d_buf):
-        v = model_fn_wan_video(dit, vace=vace, latents=latents, timestep=t_buf, context=ctx, vace_context=vc,
-                               use_unified_sequence_parallel=sp is not None, sp_group=sp)
-        K.cfg_euler_dev(v[0:1], v[1:2], latents, 5.0, d_buf)
-
-    # the product's step runner: step 0 eager, then one hipGraph capture replayed per step (single
-    # GPU; Ulysses SP steps run eagerly).  Capture happens inside the warmup.
-    use_graph = world == 1 and not args.no_graph and args.warmup >= 1
-    stepper = DenoiseStepper(step_fn, ts, ds, use_graph=use_graph)
-    for i in range(args.warmup):
-        stepper(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    TIMER.reset()
-    TIMER.enabled = not use_graph     # eager: attention events inside the timed steps
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.warmup, n_total):
-        stepper(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if use_graph:
-        # ROCm refuses event nodes inside a graph: time the attention launches on one instrumented
-        # eager step of the same workload right after the timed replays
-        TIMER.enabled = True
-        step_fn(stepper.t_buf, stepper.d_buf)
+    use_graph = False
+    if args.config == "fp8":
+        # config 5: the sampler is stateful (UniPC multistep), so the W warmup steps run as their own
+        # short sampler and the K timed steps as one K-step sampler (CFG 1.2, shift 2, SLG block 2
+        # for step fractions in [0.2, 0.7], VACE strength 0.975), eager launches
+        from vstyler.models import quantize_fp8_
+        from vstyler.pipeline import WanVideoPipeline
+        quantize_fp8_(dit)
+        quantize_fp8_(vace)
+        pipe = WanVideoPipeline(device=dev)
+        pipe.dit, pipe.vace = dit, vace
+        pipe.use_unified_sequence_parallel, pipe.sp_group = sp is not None, sp
+        kw = dict(vace_scale=0.975, cfg_scale=1.2, sigma_shift=2.0, slg_blocks=(2,))
+        if args.warmup > 0:
+            pipe.denoise_unipc(latents, ctx[0:1], ctx[1:2], vc, num_inference_steps=args.warmup, **kw)
         torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        TIMER.reset()
+        TIMER.enabled = True
+        t0 = time.perf_counter()
+        pipe.denoise_unipc(latents, ctx[0:1], ctx[1:2], vc, num_inference_steps=args.steps, **kw)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+    else:
+        sched = FlowMatchScheduler(shift=5, sigma_min=0.0, extra_one_step=True)
+        n_total = args.warmup + args.steps
+        sched.set_timesteps(max(n_total, 2), shift=5.0)
+        ts = sched.timesteps.to(torch.bfloat16).to(dev)
+        ds = torch.tensor([sched.delta(i) for i in range(len(sched.timesteps))], dtype=torch.float32, device=dev)
+
+        def step_fn(t_buf, d_buf):
+            v = model_fn_wan_video(dit, vace=vace, latents=latents, timestep=t_buf, context=ctx, vace_context=vc,
+                                   use_unified_sequence_parallel=sp is not None, sp_group=sp)
+            K.cfg_euler_dev(v[0:1], v[1:2], latents, 5.0, d_buf)
+
+        # the product's step runner: step 0 eager, then one hipGraph capture replayed per step (single
+        # GPU; Ulysses SP steps run eagerly).  Capture happens inside the warmup.
+        use_graph = world == 1 and not args.no_graph and args.warmup >= 1
+        stepper = DenoiseStepper(step_fn, ts, ds, use_graph=use_graph)
+        for i in range(args.warmup):
+            stepper(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        TIMER.reset()
+        TIMER.enabled = not use_graph     # eager: attention events inside the timed steps
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.warmup, n_total):
+            stepper(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if use_graph:
+            # ROCm refuses event nodes inside a graph: time the attention launches on one instrumented
+            # eager step of the same workload right after the timed replays
+            TIMER.enabled = True
+            step_fn(stepper.t_buf, stepper.d_buf)
+            torch.cuda.synchronize()
     TIMER.enabled = False
     attn_ms, attn_n = TIMER.mean_ms("self_attn")
     if world > 1:
@@ -202,11 +232,13 @@ def main():
     attn_flops = 4.0 * S * S * m["dim"] * 2 / world
     achieved = attn_flops / (attn_ms / 1000) / 1e12
     out = {
-        "metric": "denoising steps/sec, Wan2.1-VACE-14B 832x480x73" if args.model == "14B" else
-                  f"denoising steps/sec, Wan2.1-VACE-{args.model} {args.width}x{args.height}x{args.frames}",
+        "metric": ("denoising steps/sec, Wan2.1-VACE-14B 832x480x73" if args.model == "14B" else
+                   f"denoising steps/sec, Wan2.1-VACE-{args.model} {args.width}x{args.height}x{args.frames}")
+                  + (" [config 5: fp8 e4m3 block linears, UniPC, CFG 1.2, SLG]" if args.config == "fp8" else ""),
         "value": round(value, 5), "unit": "steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+        "scaling": "strong", "vs_baseline": None,
+        "dtype": "fp8_e4m3 (block linears) + bf16 (attention, norms)" if args.config == "fp8" else "bf16",
         "data": "synthetic (random-init weights, seeded latents/contexts/VACE context)",
         "config": {"workload": f"Wan2.1-VACE-{args.model} {args.width}x{args.height}x{args.frames}: "
                                f"{m['num_layers']} DiT + {len(m['vace_layers'])} VACE blocks, CFG 5.0 as one "
@@ -214,7 +246,9 @@ def main():
                    "model": f"Wan2.1-VACE-{args.model}", "global_batch": 1, "seq_len": S,
                    "latent_shape": [1, 16, T, Hl, Wl], "parallelism": f"sp{world}" if world > 1 else "single",
                    "lora": "merged (zero runtime cost, as the reference's GeneralLoRALoader)",
-                   "step_exec": "hipGraph replay" if use_graph else "eager launches"},
+                   "step_exec": "hipGraph replay" if use_graph else "eager launches",
+                   "sampler": ("UniPC bh2 order 2, cfg 1.2, shift 2.0, SLG block 2 @ 0.2-0.7, VACE 0.975"
+                               if args.config == "fp8" else "flow-match Euler, cfg 5.0, shift 5.0")},
         "model_tflops_per_step": round(fl_step / 1e12, 1),
         "mfu_bf16": round(fl_step * value / world / 1e12 / PEAK_BF16_TFLOPS, 4),
         "roofline": {"kernel": "attn_fwd_d128 (self-attention)", "bound": "mfma",

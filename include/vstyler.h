@@ -228,6 +228,17 @@ int vs_vace_prepare(const void* video_u8, const void* mask_u8, void* inactive, v
  * vace_context) = nearest-exact temporal resize of rearrange(mask0, "T (H 8) (W 8) -> (8 8) T H W"). */
 int vs_vace_mask_latents(const void* mask0, void* out, int t, int h, int w, int t_out, void* stream);
 
+/* UniPC multistep tensor update (FlowUniPCMultistepScheduler,
+ * denoising_enhancing/wan/utils/fm_solvers_unipc.py:281-628; config 5's 4-step sampler), fp32 with the reference's op order:
+ * mode 0 convert out = x - c1*mt; 1 UniP order 1; 2 UniP order 2; 3 UniC order 1; 4 UniC order 2
+ * (formulas at the kernel).  coef = host array {c1, c2, c3, r0, r1, rk} computed by the scheduler.
+ * Pointers not used by a mode may be NULL. */
+int vs_unipc_update(float* out, const float* x, const float* m0, const float* m1, const float* mt, long long n,
+                    int mode, const float* coef, void* stream);
+
+/* Elementwise dtype cast: to_bf16 = 1: fp32 -> bf16 (RNE), 0: bf16 -> fp32. */
+int vs_cast(const void* src, void* dst, long long n, int to_bf16, void* stream);
+
 /* Copy n frames of frame_elems elements (src/dst strides per n in elements): the pass-through
  * first frame of Resample downsample3d/upsample3d (:125-127,165-167). */
 int vs_vae_copy_frames(const void* src, long long src_ns, void* dst, long long dst_ns, int n,

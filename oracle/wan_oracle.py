@@ -280,9 +280,12 @@ def vace_forward(x, vace_context, ctx, t_mod, freqs, W, vace_layers, num_heads, 
     return hints
 
 
-def model_fn(W, cfg, latents, timestep, context, vace_context=None, vace_scale=1.0, num_layers=None):
+def model_fn(W, cfg, latents, timestep, context, vace_context=None, vace_scale=1.0, num_layers=None,
+             skip_blocks=()):
     """model_fn_wan_video, wan_video_new.py:1338-1468 (non-S2V, non-animate, no TeaCache,
-    no sliding window, no SP).  `timestep` is the (B,) bf16 tensor of wan_video_new.py:526."""
+    no sliding window, no SP).  `timestep` is the (B,) bf16 tensor of wan_video_new.py:526.
+    skip_blocks: skip-layer guidance of config 5 (ComfyUI WanVideoSLG, external): the listed main
+    blocks -- and the VACE hint added after them -- are skipped."""
     D, H, eps = cfg["dim"], cfg["num_heads"], cfg["eps"]
     L = cfg["num_layers"] if num_layers is None else num_layers
     t, t_mod = time_embed(timestep, W, D)
@@ -295,6 +298,8 @@ def model_fn(W, cfg, latents, timestep, context, vace_context=None, vace_scale=1
         hints = vace_forward(x, vace_context, ctx, t_mod, freqs, W, cfg["vace_layers"], H, eps)
         vmap = {layer: n for n, layer in enumerate(cfg["vace_layers"])}
     for i in range(L):
+        if i in skip_blocks:
+            continue
         x = dit_block(x, ctx, t_mod, freqs, W, f"blocks.{i}.", H, eps)
         if hints is not None and i in vmap:                       # :1445-1450
             x = add(x, bf(hints[vmap[i]].float() * vace_scale))
@@ -340,6 +345,31 @@ def fp8_linear(x, w, b):
     if b is not None:
         out = out + b.to(ACC_DTYPE)
     return out.to(BF16).reshape(*x.shape[:-1], w.shape[0])
+
+
+def denoise_unipc(W, cfg, latents, context_pos, context_neg, vace_context=None, vace_scale=1.0, cfg_scale=1.2,
+                  num_inference_steps=4, sigma_shift=2.0, slg_blocks=(), slg_range=(0.2, 0.7)):
+    """Config 5's sampler chain (ditto_comfyui_workflow.json: WanVideoSampler 4 steps / cfg 1.2 /
+    shift 2.0 / unipc, WanVideoSLG): UniPC on fp32 latents (oracle/unipc_oracle.py), model input
+    bf16, CFG combined in bf16 as wan_video_new.py:535, SLG on the uncond pass.  The ComfyUI wrapper
+    itself is external (not in the reference): parity unpinned."""
+    from .unipc_oracle import UniPCOracle
+    sched = UniPCOracle(shift=1.0)
+    sched.set_timesteps(num_inference_steps, shift=sigma_shift)
+    x = latents.float()
+    n = len(sched.timesteps)
+    for i, t in enumerate(sched.timesteps):
+        tb = t.reshape(1).to(BF16)
+        lat = x.to(BF16)
+        vp = model_fn(W, cfg, lat, tb, context_pos, vace_context, vace_scale)
+        if cfg_scale != 1.0:
+            skip = tuple(slg_blocks) if slg_range[0] <= i / n <= slg_range[1] else ()
+            vn = model_fn(W, cfg, lat, tb, context_neg, vace_context, vace_scale, skip_blocks=skip)
+            v = bf(vn.float() + bf(cfg_scale * bf(vp.float() - vn.float()).float()).float())
+        else:
+            v = vp
+        x = sched.step(v.float(), t, x)
+    return x.to(BF16)
 
 
 # --------------------------------------------------------------------------------------

@@ -30,5 +30,5 @@ for (M, N, Kd) in [(59280, 5120, 5120), (59280, 13824, 5120), (59280, 5120, 1382
     tq = timeit(lambda: K.quant_fp8_rows(a, a8, sc))
     tg = timeit(lambda: K.gemm_fp8(a8, sc, w8, out))
     tb = timeit(lambda: K.gemm(a, w, out))
-    print(f"M={M} N={N} K={Kd}: quant {tq:.3f} ms ({M*Kd*3/tq/1e9:.0f} GB/s)  fp8 gemm {tg:.3f} ms "
+    print(f"M={M} N={N} K={Kd}: quant {tq:.3f} ms ({M*Kd*3/tq/1e6:.0f} GB/s)  fp8 gemm {tg:.3f} ms "
           f"{fl/tg/1e9:.0f} TF/s  (+quant {fl/(tg+tq)/1e9:.0f})  bf16 gemm {tb:.3f} ms {fl/tb/1e9:.0f} TF/s", flush=True)

@@ -212,6 +212,53 @@ __global__ void cfg_euler_kernel(const bf16_t* __restrict__ vp, const bf16_t* __
     reinterpret_cast<u32x4_t*>(x)[i] = pack8(xv);
 }
 
+
+// FlowUniPCMultistepScheduler tensor updates (denoising_enhancing/wan/utils/fm_solvers_unipc.py),
+// fp32, each op rounded as the reference's separate fp32 tensor ops (no contraction):
+//   mode 0 convert   : out = x - c[0]*mt                                       (:317-323)
+//   mode 1 UniP o1   : out = c1*x - c2*m0                                       (:469,475)
+//   mode 2 UniP o2   : out = (c1*x - c2*m0) - c3*(r0*((m1 - m0)/rk))            (:427,469-475)
+//   mode 3 UniC o1   : out = (c1*x - c2*m0) - c3*(r1*(mt - m0))                 (:612-618)
+//   mode 4 UniC o2   : out = (c1*x - c2*m0) - c3*(r0*((m1 - m0)/rk) + r1*(mt - m0))
+// with c = {c1, c2, c3, r0, r1, rk}; m0 = newest stored x0 prediction, m1 = the one before, mt = the
+// current model output (mode 0: raw velocity; modes 3/4: current x0 prediction).
+__global__ void unipc_kernel(float* __restrict__ out, const float* __restrict__ x, const float* __restrict__ m0,
+                             const float* __restrict__ m1, const float* __restrict__ mt, long long n, int mode,
+                             float c1, float c2, float c3, float r0, float r1, float rk) {
+    // the reference rounds after every op: hipcc's default -ffp-contract=fast would fuse
+    // c*x - y into one v_fma_f32 (the __f*_rn helpers do not stop it: their inlined bodies carry
+    // the contract flag), so the expressions are written here, under contract(off)
+#pragma clang fp contract(off)
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (mode == 0) {
+        out[i] = x[i] - c1 * mt[i];
+        return;
+    }
+    const float base = c1 * x[i] - c2 * m0[i];
+    float res;
+    if (mode == 1) {
+        out[i] = base;
+        return;
+    } else if (mode == 2) {
+        res = r0 * ((m1[i] - m0[i]) / rk);
+    } else if (mode == 3) {
+        res = r1 * (mt[i] - m0[i]);
+    } else {
+        res = r0 * ((m1[i] - m0[i]) / rk) + r1 * (mt[i] - m0[i]);
+    }
+    out[i] = base - c3 * res;
+}
+
+__global__ void cast_kernel(const void* __restrict__ src, void* __restrict__ dst, long long n, int to_bf16) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (to_bf16)
+        ((bf16_t*)dst)[i] = (bf16_t)f2bf(((const float*)src)[i]);
+    else
+        ((float*)dst)[i] = bf2f(((const bf16_t*)src)[i]);
+}
+
 __global__ void time_sinusoid_kernel(const bf16_t* __restrict__ t, bf16_t* __restrict__ out, int dim) {
     const int b = blockIdx.x;
     const int half = dim >> 1;
@@ -429,3 +476,21 @@ extern "C" const char* vs_strerror(int code) {
 }
 
 extern "C" int vs_abi_version(void) { return 1; }
+
+extern "C" int vs_unipc_update(float* out, const float* x, const float* m0, const float* m1, const float* mt,
+                               long long n, int mode, const float* coef, void* stream) {
+    if (!out || !coef || n <= 0 || mode < 0 || mode > 4 || !x) return VS_E_INVALID;
+    if ((mode >= 1 && !m0) || ((mode == 2 || mode == 4) && !m1) || ((mode == 0 || mode >= 3) && !mt))
+        return VS_E_INVALID;
+    hipLaunchKernelGGL(unipc_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, out, x, m0, m1, mt, n,
+                       mode, coef[0], coef[1], coef[2], coef[3], coef[4], coef[5]);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_cast(const void* src, void* dst, long long n, int to_bf16, void* stream) {
+    if (!src || !dst || n <= 0) return VS_E_INVALID;
+    hipLaunchKernelGGL(cast_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, src, dst, n, to_bf16);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}

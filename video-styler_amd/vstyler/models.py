@@ -197,8 +197,10 @@ class DiTBlock(nn.Module):
         self.ffn = Sequential3(Linear(dim, ffn_dim, device=device), Linear(ffn_dim, dim, device=device))
         self.modulation = _param(1, 6, dim, device=device)
 
-    def forward(self, x, t_mod, rc, hint=None, hint_scale=1.0):
+    def forward(self, x, t_mod, rc, hint=None, hint_scale=1.0, only_batch=None):
         """x: [B*S, D] updated in place.  t_mod: [B, 6, D].  hint: [B*S, D] added after the block.
+        only_batch: run the block for that CFG sample only (skip-layer guidance leaves the others'
+        rows untouched).
 
         Three phases per micro-batch: (1) LN1 + q/k/v + QK-RMSNorm/RoPE, (2) self-attention,
         (3) o-proj (gated residual), cross-attention, FFN (gated residual + VACE hint).  Without SP
@@ -210,7 +212,9 @@ class DiTBlock(nn.Module):
         mod = ws.get("mod", (B, 6, D))
         K.mod_add(self.modulation.view(6, D), t_mod, mod, 6 * D, D)   # :218-219
         sp = rc.sp
-        if sp is not None and B > 1 and getattr(sp, "overlap", False):
+        if only_batch is not None:
+            parts = [self._part(x, mod, rc, only_batch, 1, hint, f".{only_batch}")]
+        elif sp is not None and B > 1 and getattr(sp, "overlap", False):
             parts = [self._part(x, mod, rc, b, 1, hint, f".{b}") for b in range(B)]
         else:
             parts = [self._part(x, mod, rc, 0, B, hint, "")]

@@ -37,8 +37,11 @@ _UNSUPPORTED = ("clip_feature", "y", "reference_latents", "audio_embeds", "motio
 def model_fn_wan_video(dit: WanModel, motion_controller=None, vace: VaceWanModel = None, animate_adapter=None,
                        latents: torch.Tensor = None, timestep: torch.Tensor = None, context: torch.Tensor = None,
                        vace_context=None, vace_scale=1.0, use_unified_sequence_parallel: bool = False,
-                       sp_group=None, **kwargs):
+                       sp_group=None, slg_blocks=(), **kwargs):
     """One DiT(+VACE) forward (wan_video_new.py:1338-1468) -> [B,16,T,H,W] bf16 velocity.
+
+    slg_blocks: skip-layer guidance (config 5, ComfyUI WanVideoSLG): the listed main blocks are
+    skipped for CFG sample 1 (the unconditional pass), run for sample 0 only.
 
     `context` is [B, L, text_dim]; latents/timestep/vace_context with batch 1 are broadcast to B
     (the cfg_merge convention of wan_video_new.py:1361-1364)."""
@@ -84,7 +87,8 @@ def model_fn_wan_video(dit: WanModel, motion_controller=None, vace: VaceWanModel
     vmap = vace.vace_layers_mapping if hints is not None else {}
     for i, blk in enumerate(dit.blocks):
         hint = hints[vmap[i]] if i in vmap else None
-        blk(x, t_mod, rc, hint=hint, hint_scale=float(vace_scale))
+        skip = B > 1 and i in slg_blocks
+        blk(x, t_mod, rc, hint=hint, hint_scale=float(vace_scale), only_batch=0 if skip else None)
     out = dit.head(x, t, rc)
     if sp is not None:
         out = sp.gather_tokens(out, rc)
@@ -294,6 +298,41 @@ class WanVideoPipeline:
             stepper(i)
         self.last_graph = stepper.graph
         return latents
+
+    def denoise_unipc(self, latents, context_posi, context_nega, vace_context=None, vace_scale=1.0,
+                      cfg_scale=1.2, num_inference_steps=4, sigma_shift=2.0, slg_blocks=(), slg_range=(0.2, 0.7),
+                      progress_bar_cmd=None):
+        """Config 5's sampler (ditto_comfyui_workflow.json WanVideoSampler 4 / 1.2 / 2.0 / unipc with
+        WanVideoSLG): FlowUniPCMultistepScheduler (vstyler.unipc) on fp32 latents, CFG as one
+        batch-2 forward, skip-layer guidance on the uncond sample for step fractions in slg_range.
+        CFG combine in bf16 (wan_video_new.py:535 semantics), model input bf16 each step."""
+        from .unipc import FlowUniPCMultistepScheduler, cast
+        sched = FlowUniPCMultistepScheduler(shift=1.0)
+        sched.set_timesteps(num_inference_steps, shift=sigma_shift)
+        use_cfg = cfg_scale != 1.0
+        ctx = torch.cat([context_posi, context_nega], 0) if use_cfg else context_posi
+        lat32 = latents.to(device=self.device, dtype=torch.float32).contiguous().clone()
+        lat16 = torch.empty(lat32.shape, dtype=BF16, device=self.device)
+        v16 = torch.empty(lat32.shape, dtype=BF16, device=self.device)
+        v32 = torch.empty_like(lat32)
+        n = len(sched.timesteps)
+        steps = range(n)
+        if progress_bar_cmd is not None:
+            steps = progress_bar_cmd(steps)
+        for i in steps:
+            t = sched.timesteps[i]
+            cast(lat32, lat16)
+            frac = i / n
+            slg = tuple(slg_blocks) if slg_range[0] <= frac <= slg_range[1] else ()
+            v = self.model_fn(dit=self.dit, vace=self.vace, latents=lat16, timestep=t.reshape(1).to(
+                dtype=BF16, device=self.device), context=ctx, vace_context=vace_context, vace_scale=vace_scale,
+                use_unified_sequence_parallel=self.use_unified_sequence_parallel, sp_group=self.sp_group,
+                slg_blocks=slg)
+            v16.zero_()
+            K.cfg_euler(v[0:1], v[1:2] if use_cfg else None, v16, cfg_scale, 1.0)   # v16 = cfg combine
+            cast(v16, v32)
+            lat32 = sched.step(v32, t, lat32)[0]
+        return cast(lat32, torch.empty(lat32.shape, dtype=BF16, device=self.device))
 
     @torch.no_grad()
     def __call__(self, prompt=None, negative_prompt="", input_image=None, end_image=None, input_video=None,
