@@ -14,6 +14,7 @@ import argparse
 import json
 import math
 import os
+import re
 import sys
 import time
 
@@ -97,6 +98,20 @@ def cpu_baseline(m, S, rows=1024, repeats=2):
             "sample": f"oracle DiT block, {rows} of {S} query tokens vs full {S}-token K/V, best of {repeats} "
                       f"({best:.2f}s), extrapolated x{S}/{rows} tokens x{blocks} blocks x2 CFG "
                       f"= {sec_per_step:.0f} s/step"}
+
+
+def pmc_traffic(path=os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1", "pmc_attn",
+                                   "summary.txt")):
+    """HBM bytes per self-attention launch from the committed rocprofv3 --pmc measurement of the same
+    kernel at the same shape (scripts/pmc.sh attn: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE,
+    KB -> bytes, median over the profiled dispatches), or None."""
+    try:
+        txt = open(path).read()
+        rd = float(re.search(r"HBM read\s+~\s+([0-9.]+) GB/dispatch", txt).group(1))
+        wr = float(re.search(r"HBM write\s+~\s+([0-9.]+) GB/dispatch", txt).group(1))
+        return (rd + wr) * 1e9
+    except (OSError, AttributeError):
+        return None
 
 
 def main():
@@ -253,7 +268,10 @@ def main():
         "mfu_bf16": round(fl_step * value / world / 1e12 / PEAK_BF16_TFLOPS, 4),
         "roofline": {"kernel": "attn_fwd_d128 (self-attention)", "bound": "mfma",
                      "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                     "traffic": pmc_traffic() if world == 1 else None,
+                     "traffic_source": "rocprofv3 --pmc FETCH_SIZE*2+WRITE_SIZE per launch, profiles/r1/pmc_attn "
+                                       "(same kernel, same shape; algorithmic Q+K+V+O = 2.43e9 B)",
                      "avg_launch_ms": round(attn_ms, 3), "launches": attn_n,
                      "timing": "HIP events on the launch stream, " + ("one instrumented eager step after the "
                                "timed hipGraph replays" if use_graph else "every launch of the timed steps"),
