@@ -146,6 +146,27 @@ int vs_ulysses_permute(const void* src, void* dst, int batch, int s_local, int w
                        int cols_per_rank, long long ld_local, long long jstride, int mode, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * UMT5-XXL text encoder (diffsynth/models/wan_video_text_encoder.py; GEMMs / norms / per-head
+ * products go through vs_gemm, vs_rmsnorm_rope and the batched mode of vs_vae_conv).
+ * ------------------------------------------------------------------------------------------- */
+
+/* out[r] = table[ids[r]] (nn.Embedding, :233); ids int64, rows of dim bf16. */
+int vs_embed_rows(const long long* ids, const void* table, long long ld_table, long long vocab, void* out,
+                  long long ld_out, long long rows, int dim, void* stream);
+
+/* T5Attention scores -> probabilities (:69-83): for head z (global head head0 + z), query i, key j:
+ * v = bf16(bf16(s) + bias), bias = emb[buckets[i*L + j]][head0 + z] (bf16, per-block relative
+ * position embedding) or the bf16 lowest value where keymask[j] == 0; p = bf16(softmax_j(v)) in
+ * fp32.  s fp32 [nz][L][ld_s], p bf16 [nz][L][ld_p] (columns >= L written 0), buckets int32 [L][L]. */
+int vs_t5_bias_softmax(const float* s, long long zs_s, long long ld_s, void* p, long long zs_p, long long ld_p,
+                       const int* buckets, const void* emb, int nheads, int head0, const int* keymask, int L, int nz,
+                       void* stream);
+
+/* out = bf16(a * gelu(g)) with the tanh-GELU evaluated op by op in bf16 (GELU :15-19,
+ * T5FeedForward :105-110). */
+int vs_t5_gelu_mul(const void* a, const void* g, void* out, long long n, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Causal 3-D VAE (diffsynth/models/wan_video_vae.py, Wan2.1 part).  Activations are channels-last
  * "NTHWC" tiles: element (n, t, y, x, c) of a tensor lives at base + n*ns + ((t*H + y)*W + x)*ld + c.
  * ------------------------------------------------------------------------------------------- */

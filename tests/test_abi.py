@@ -66,3 +66,24 @@ def test_wrappers_raise_on_bad_dtype():
     from vstyler import kernels as K
     with pytest.raises(ValueError):
         K.gemm(torch.zeros(4, 64), torch.zeros(4, 64), torch.zeros(4, 4))
+
+
+def test_lora_key_layouts():
+    """GeneralLoRALoader.get_name_dict (lora/__init__.py:11-25) naming, plus the kohya layout
+    (lora_down/lora_up/alpha) of CausVid-style LoRAs normalised onto it."""
+    import torch
+    from vstyler.lora import get_name_dict, normalize_lora_keys
+    sd = {"diffusion_model.blocks.0.self_attn.q.lora_B.default.weight": torch.ones(8, 4),
+          "diffusion_model.blocks.0.self_attn.q.lora_A.default.weight": torch.ones(4, 8),
+          "vace_blocks.1.ffn.0.lora_B.weight": torch.ones(8, 4),
+          "vace_blocks.1.ffn.0.lora_A.weight": torch.ones(4, 8)}
+    names = get_name_dict(sd)
+    assert set(names) == {"blocks.0.self_attn.q", "vace_blocks.1.ffn.0"}
+    kohya = {"diffusion_model.blocks.3.cross_attn.o.lora_down.weight": torch.ones(32, 16),
+             "diffusion_model.blocks.3.cross_attn.o.lora_up.weight": torch.full((16, 32), 2.0),
+             "diffusion_model.blocks.3.cross_attn.o.alpha": torch.tensor(16.0)}
+    norm = normalize_lora_keys(kohya)
+    names = get_name_dict(norm)
+    assert list(names) == ["blocks.3.cross_attn.o"]
+    b, a = norm[names["blocks.3.cross_attn.o"][0]], norm[names["blocks.3.cross_attn.o"][1]]
+    assert a.shape == (32, 16) and torch.allclose(b, torch.full((16, 32), 1.0))   # 2 * 16/32

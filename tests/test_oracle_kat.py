@@ -76,3 +76,17 @@ def test_unpatchify_inverts_patchify_layout():
     perm = torch.tensor([c * 4 + y * 2 + z for y in range(2) for z in range(2) for c in range(16)])
     back = O.unpatchify(tok[..., perm], grid, 16)
     assert torch.equal(back, lat)
+
+
+def test_t5_key_layout_matches_reference_registry():
+    """configs/model_config.py:161: the Wan UMT5-XXL text encoder file's md5 key hash."""
+    from oracle import t5_oracle as T
+    assert O.hash_state_dict_keys(T.t5_param_shapes()) == "9c8818c2cbea55eca56c7b447df170da"
+
+
+def test_t5_relative_position_buckets():
+    from oracle import t5_oracle as T
+    b = T.relative_position_bucket(512, 512)
+    assert b.min() == 0 and b.max() == 31
+    assert b[0, 0] == 0 and b[0, 1] == 17 and b[1, 0] == 1 and b[0, 7] == 23 and b[7, 0] == 7
+    assert b[0, 511] == 31 and b[511, 0] == 15

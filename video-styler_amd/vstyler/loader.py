@@ -97,6 +97,16 @@ def build_vae(state_dict, device):
     return WanVideoVAE(z_dim=z_dim, dim=sd["encoder.conv1.weight"].shape[0], device=device).load_state_dict(sd)
 
 
+T5_HASH = "9c8818c2cbea55eca56c7b447df170da"   # configs/model_config.py:161 (WanTextEncoder)
+
+
+def build_text_encoder(state_dict, device):
+    if hash_state_dict_keys(state_dict) != T5_HASH:
+        return None
+    from .t5 import WanTextEncoder
+    return WanTextEncoder(device=device).load_state_dict(state_dict)
+
+
 def load_models(paths, device="cuda"):
     """Returns {'wan_video_dit': WanModel, 'wan_video_vace': VaceWanModel, ...} for the files given."""
     out = {}
@@ -105,6 +115,10 @@ def load_models(paths, device="cuda"):
         vae = build_vae(sd, device)
         if vae is not None:
             out["wan_video_vae"] = vae
+            continue
+        te = build_text_encoder(sd, device)
+        if te is not None:
+            out["wan_video_text_encoder"] = te
             continue
         dit = build_dit(sd, device)
         if dit is not None:

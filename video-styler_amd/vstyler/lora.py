@@ -21,7 +21,28 @@ def load_lora_state_dict(lora_config, device):
     else:
         lora_config.download_if_necessary()
         path = lora_config.path
-    return load_state_dict(path, device=device, torch_dtype=BF16)
+    return normalize_lora_keys(load_state_dict(path, device=device, torch_dtype=BF16))
+
+
+def normalize_lora_keys(sd):
+    """Map the kohya/ComfyUI layout used by CausVid-style Wan LoRAs ('<name>.lora_down.weight' = A,
+    '<name>.lora_up.weight' = B, optional '<name>.alpha' scalar, scale alpha / rank) onto the
+    reference's lora_A/lora_B layout (the alpha/rank scale folded into B); other keys pass through."""
+    out = {}
+    for key, val in sd.items():
+        if key.endswith(".lora_down.weight"):
+            base = key[: -len(".lora_down.weight")]
+            up = sd[base + ".lora_up.weight"]
+            scale = 1.0
+            if base + ".alpha" in sd:
+                scale = float(sd[base + ".alpha"]) / val.shape[0]
+            out[base + ".lora_A.weight"] = val
+            out[base + ".lora_B.weight"] = up if scale == 1.0 else (up.float() * scale).to(up.dtype)
+        elif key.endswith(".lora_up.weight") or key.endswith(".alpha"):
+            continue
+        else:
+            out[key] = val
+    return out
 
 
 def get_name_dict(lora_state_dict):

@@ -212,6 +212,14 @@ class WanVideoPipeline:
         pipe.vace = models.get("wan_video_vace")
         pipe.vae = models.get("wan_video_vae")
         pipe.text_encoder = models.get("wan_video_text_encoder")
+        if pipe.text_encoder is not None:
+            from .t5 import WanPrompter
+            tok = None
+            if tokenizer_config is not None:
+                tokenizer_config.download_if_necessary()
+                tok = tokenizer_config.path
+            pipe.prompter = WanPrompter(tokenizer_path=tok)
+            pipe.prompter.fetch_models(pipe.text_encoder)
         if use_usp:
             pipe.enable_usp()
         return pipe
