@@ -114,6 +114,49 @@ def pmc_traffic(path=os.path.join(os.path.dirname(os.path.abspath(__file__)), "p
         return None
 
 
+def e2e_components(dev, frames, height, width, step_s, steps=50):
+    """End-to-end sec/video of the Ditto call (BASELINE metric 2): 2 prompts through UMT5-XXL,
+    WanVideoUnit_VACE (2 tiled VAE encodes + mask latents), `steps` denoising steps at the measured
+    step time, tiled VAE decode + uint8 conversion.  Random-init weights, synthetic frames; each
+    component timed once after one warm-up call."""
+    from vstyler.t5 import WanPrompter, WanTextEncoder
+    from vstyler.vae import WanVideoVAE, vace_context, vae_output_to_u8
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, out
+
+    te = WanTextEncoder(device=dev).init_random_(8)
+    pr = WanPrompter()
+    pr.fetch_models(te)
+    g = torch.Generator(device=dev).manual_seed(2)
+    ids = torch.randint(1, te.vocab, (1, 512), generator=g, device=dev)
+    mask = torch.zeros(1, 512, dtype=torch.long, device=dev)
+    mask[0, :48] = 1
+    ids[0, 48:] = 0
+    t5_s, _ = timed(lambda: (pr.encode_ids(ids, mask), pr.encode_ids(ids, mask)))
+    del te, pr
+    torch.cuda.empty_cache()
+    vae = WanVideoVAE(device=dev).init_random_(6)
+    video = torch.randint(0, 256, (frames, height, width, 3), generator=g, device=dev, dtype=torch.uint8)
+    enc_s, vc = timed(lambda: vace_context(vae, video, None, tiled=True, tile_size=(30, 52), tile_stride=(15, 26)))
+    lat = torch.randn(vc.shape[0], 16, *vc.shape[2:], generator=g, device=dev).to(torch.bfloat16)
+    dec_s, _ = timed(lambda: vae_output_to_u8(vae.decode(lat, dev, tiled=True, tile_size=(30, 52),
+                                                           tile_stride=(15, 26))[0]))
+    del vae, vc
+    torch.cuda.empty_cache()
+    total = t5_s + enc_s + steps * step_s + dec_s
+    return {"sec_per_video": round(total, 2), "unit": "s/video", "t5_2_prompts_s": round(t5_s, 4),
+            "vace_2_vae_encodes_s": round(enc_s, 3), "denoise_s": round(steps * step_s, 2), "steps": steps,
+            "vae_decode_u8_s": round(dec_s, 3),
+            "note": "2 prompts x UMT5-XXL (512 tokens) + VACE unit (2 tiled encodes) + 50 x measured step + "
+                    "tiled decode + uint8; random-init weights, synthetic frames"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -126,6 +169,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=1024)
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end sec/video components")
     ap.add_argument("--config", default="bf16", choices=("bf16", "fp8"),
                     help="bf16: BASELINE config (50-step Euler, CFG 5); fp8: config 5 (fp8 block linears, "
                          "UniPC, CFG 1.2, shift 2, SLG block 2, VACE strength 0.975)")
@@ -277,6 +321,8 @@ def main():
                                "timed hipGraph replays" if use_graph else "every launch of the timed steps"),
                      "flops_per_launch": attn_flops},
     }
+    if world == 1 and not args.no_e2e and args.config == "bf16":
+        out["e2e"] = e2e_components(dev, args.frames, args.height, args.width, elapsed / args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(m, S, rows=args.cpu_rows)
     if rank == 0:

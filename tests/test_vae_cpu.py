@@ -65,3 +65,14 @@ def test_output_to_u8_rounding():
     u = V.vae_output_to_u8(v)
     assert u.shape == (1, 1, 5, 3)
     assert u[0, 0, :, 0].tolist() == [0, 1, 127, 191, 255]
+
+
+def test_product_vae_layout_matches_oracle():
+    """The product's own state-dict layout (used for synthetic weights) is the reference file's."""
+    import vstyler.vae as PV
+    m = PV.WanVideoVAE.__new__(PV.WanVideoVAE)
+    m.z_dim, m.dim, m.dim_mult, m.nrb = 16, 96, (1, 2, 4, 4), 2
+    m.temperal_downsample = (False, True, True)
+    m.enc_layers, m.enc_dims = m._encoder_layers()
+    m.dec_layers, m.dec_dims = m._decoder_layers()
+    assert m.state_dict_shapes() == V.vae_param_shapes()

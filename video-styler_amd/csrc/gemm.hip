@@ -339,6 +339,52 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
         __builtin_amdgcn_s_setprio(0);
     };
 
+#ifdef VS_GEMM_PIPE
+    // Register-pipelined variant: every wave runs [barrier_h; DMA(h+RING-1); frags(h+1) -> other
+    // register set; MFMAs(h)], one barrier per half-step, no ping-pong.  barrier_h retires (vmcnt)
+    // the wave's DMA of half-step h+1 and, because each wave reaches it only after consuming
+    // frags(h-1), frees slot (h-1) % RING for the DMA issued right after it.
+    bf16x8_t wf2[4], af2[8];
+    auto load_frags2 = [&](int h, bf16x8_t* w, bf16x8_t* a) {
+        const char* As = smem + (h % RING) * SLOT;
+        const char* Bs = As + BT * 64;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            w[j] = *reinterpret_cast<const bf16x8_t*>(Bs + h_off(wn * 64 + j * 16 + frow, fch));
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            a[i] = *reinterpret_cast<const bf16x8_t*>(As + h_off(wm * 128 + i * 16 + frow, fch));
+    };
+    auto mfmas2 = [&](const bf16x8_t* w, const bf16x8_t* a) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[j], a[i], acc[i][j], 0, 0, 0);
+    };
+#pragma unroll
+    for (int j = 0; j < RING - 1; ++j)
+        if (j < nh) issue(j);
+    wait_barrier(issued);                           // half-step 0 landed and visible
+    load_frags2(0, wf, af);
+    for (int h = 0; h < nh; h += 2) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int hc = h + e;
+            if (hc >= nh) break;
+            // barrier: half-step hc+1 visible (all but the DMAs issued after it may be pending)
+            wait_barrier(issued - min(hc + 1, nh - 1));
+            if (hc + RING - 1 < nh) issue(hc + RING - 1);
+            if (e == 0) {
+                if (hc + 1 < nh) load_frags2(hc + 1, wf2, af2);
+                mfmas2(wf, af);
+            } else {
+                if (hc + 1 < nh) load_frags2(hc + 1, wf, af);
+                mfmas2(wf2, af2);
+            }
+        }
+    }
+#else
     // prologue: half-steps 0..RING-2 in flight, then wait for half-step 0
 #pragma unroll
     for (int j = 0; j < RING - 1; ++j)
@@ -368,6 +414,7 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
         STAMP(4);
     }
     if (wm == 0) bar();
+#endif
 
 #pragma unroll
     for (int i = 0; i < 8; ++i) {

@@ -54,6 +54,31 @@ class WanTextEncoder:
         self.w = {k: v.detach().to(device=self.device, dtype=BF16).contiguous() for k, v in sd.items()}
         return self
 
+    def state_dict_shapes(self):
+        d, da, df, n = self.dim, self.dim_attn, self.dim_ffn, self.num_heads
+        out = {"token_embedding.weight": (self.vocab, d), "norm.weight": (d,)}
+        for i in range(self.num_layers):
+            p = f"blocks.{i}."
+            out.update({p + "norm1.weight": (d,), p + "attn.q.weight": (da, d), p + "attn.k.weight": (da, d),
+                        p + "attn.v.weight": (da, d), p + "attn.o.weight": (d, da), p + "norm2.weight": (d,),
+                        p + "ffn.gate.0.weight": (df, d), p + "ffn.fc1.weight": (df, d),
+                        p + "ffn.fc2.weight": (d, df), p + "pos_embedding.embedding.weight": (self.num_buckets, n)})
+        return out
+
+    def init_random_(self, seed=8):
+        """Synthetic on-device weights (bench): N(0, 1/fan_in) matrices, N(0,1) embeddings, norms 1+0.1*N."""
+        g = torch.Generator(device=self.device).manual_seed(seed)
+        self.w = {}
+        for name, shape in self.state_dict_shapes().items():
+            if name.endswith("norm1.weight") or name.endswith("norm2.weight") or name == "norm.weight":
+                t = 1.0 + 0.1 * torch.randn(shape, generator=g, device=self.device)
+            elif "embedding" in name:
+                t = torch.randn(shape, generator=g, device=self.device) * (0.5 if "pos_" in name else 1.0)
+            else:
+                t = torch.randn(shape, generator=g, device=self.device) / math.sqrt(shape[1])
+            self.w[name] = t.to(BF16)
+        return self
+
     def _bucket_table(self, L):
         if L not in self._buckets:
             self._buckets[L] = relative_position_bucket(L, L, self.num_buckets).to(torch.int32).to(self.device)

@@ -200,8 +200,70 @@ class WanVideoVAE:
                 self.cw[base] = ConvW(sd[k], sd.get(base + "bias"), self.device)
         return self
 
-    def state_dict_keys(self):
-        return sorted(self.params) + sorted(k + s for k in self.cw for s in ("weight", "bias"))
+    def state_dict_shapes(self):
+        """The civitai file layout of this configuration (keys without 'model.')."""
+        d, z = {}, self.z_dim
+
+        def res(p, i, o):
+            d[p + "residual.0.gamma"] = (i, 1, 1, 1)
+            d[p + "residual.2.weight"], d[p + "residual.2.bias"] = (o, i, 3, 3, 3), (o,)
+            d[p + "residual.3.gamma"] = (o, 1, 1, 1)
+            d[p + "residual.6.weight"], d[p + "residual.6.bias"] = (o, o, 3, 3, 3), (o,)
+            if i != o:
+                d[p + "shortcut.weight"], d[p + "shortcut.bias"] = (o, i, 1, 1, 1), (o,)
+
+        def attn(p, c):
+            d[p + "norm.gamma"] = (c, 1, 1)
+            d[p + "to_qkv.weight"], d[p + "to_qkv.bias"] = (3 * c, c, 1, 1), (3 * c,)
+            d[p + "proj.weight"], d[p + "proj.bias"] = (c, c, 1, 1), (c,)
+
+        def resample(p, c, mode):
+            co = c // 2 if mode.startswith("up") else c
+            d[p + "resample.1.weight"], d[p + "resample.1.bias"] = (co, c, 3, 3), (co,)
+            if mode.endswith("3d"):
+                ct = 2 * c if mode == "upsample3d" else c
+                d[p + "time_conv.weight"], d[p + "time_conv.bias"] = (ct, c, 3, 1, 1), (ct,)
+
+        strip = lambda p: p[len("model."):]  # noqa: E731
+        e0, top = self.enc_dims[0], self.enc_dims[-1]
+        d["encoder.conv1.weight"], d["encoder.conv1.bias"] = (e0, 3, 3, 3, 3), (e0,)
+        for kind, p, args in self.enc_layers:
+            (res if kind == "res" else resample)(strip(p), *args)
+        res("encoder.middle.0.", top, top)
+        attn("encoder.middle.1.", top)
+        res("encoder.middle.2.", top, top)
+        d["encoder.head.0.gamma"] = (top, 1, 1, 1)
+        d["encoder.head.2.weight"], d["encoder.head.2.bias"] = (2 * z, top, 3, 3, 3), (2 * z,)
+        d["conv1.weight"], d["conv1.bias"] = (2 * z, 2 * z, 1, 1, 1), (2 * z,)
+        d["conv2.weight"], d["conv2.bias"] = (z, z, 1, 1, 1), (z,)
+        d0, dl = self.dec_dims[0], self.dec_dims[-1]
+        d["decoder.conv1.weight"], d["decoder.conv1.bias"] = (d0, z, 3, 3, 3), (d0,)
+        res("decoder.middle.0.", d0, d0)
+        attn("decoder.middle.1.", d0)
+        res("decoder.middle.2.", d0, d0)
+        for kind, p, args in self.dec_layers:
+            (res if kind == "res" else resample)(strip(p), *args)
+        d["decoder.head.0.gamma"] = (dl, 1, 1, 1)
+        d["decoder.head.2.weight"], d["decoder.head.2.bias"] = (3, dl, 3, 3, 3), (3,)
+        return d
+
+    def init_random_(self, seed=6):
+        """Synthetic on-device weights (bench / smoke): conv weights N(0, 1/fan_in), biases 0.01*N,
+        gammas 1 + 0.1*N."""
+        g = torch.Generator(device=self.device).manual_seed(seed)
+        sd = {}
+        for name, shape in self.state_dict_shapes().items():
+            if name.endswith("gamma"):
+                t = 1.0 + 0.1 * torch.randn(shape, generator=g, device=self.device)
+            elif name.endswith("bias"):
+                t = 0.01 * torch.randn(shape, generator=g, device=self.device)
+            else:
+                fan_in = 1
+                for v in shape[1:]:
+                    fan_in *= v
+                t = torch.randn(shape, generator=g, device=self.device) / math.sqrt(fan_in)
+            sd[name] = t.to(BF16)
+        return self.load_state_dict(sd)
 
     # ---------------------------------------------------------------- layers
     def _conv3(self, x, name, res=None):
