@@ -115,6 +115,22 @@ def test_attention_online_rescale_spike(K):
     assert mx < 3e-2, mx
 
 
+def test_attention_rescale_many(K):
+    """Exact-path (rescale) decisions in the middle of the key sweep for many rows: row 7's max is
+    raised three times in three different tiles, other rows once each, at keys spread over the
+    sweep (rule 26: bounded random data alone never takes the branch after the first tile)."""
+    B, S, H = 1, 2048, 2
+    q, k, v = rnd(B, S, H * 128, seed=50), rnd(B, S, H * 128, seed=51), rnd(B, S, H * 128, seed=52)
+    for key, row, a in ((300, 7, 0.3), (900, 7, 0.5), (1500, 7, 0.8), (130, 40, 0.4), (1999, 300, 0.6),
+                        (64, 1000, 0.35), (1000, 2047, 0.7), (2047, 12, 0.9)):
+        k[0, key] = (q[0, row].float() * a).to(BF16)
+    ref = O.attention(q, k, v, H)
+    out = torch.empty(S, H * 128, dtype=BF16, device="cuda")
+    K.attention(q.cuda().view(S, H * 128), k.cuda().view(S, H * 128), v.cuda().view(S, H * 128), out, H, B)
+    mx, rl = err(out.view(B, S, H * 128), ref)
+    assert mx < 3e-2 and rl < 1e-2, (mx, rl)
+
+
 def test_attention_strided_views(K):
     # q/k/v as column slices of a fused [M, 3D] buffer (row stride 3D)
     B, S, H = 1, 200, 2

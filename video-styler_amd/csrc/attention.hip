@@ -20,6 +20,7 @@
 //  * workgroup ids are remapped so each XCD works through contiguous (batch, head) ranges: the
 //    K/V of one head is streamed by the 32 CUs of one XCD together and served from its L2.
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -282,6 +283,301 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// v2: same tiles, rings and two-group stagger as v1, re-phased so one S tile is live:
+//   B_{i-1}: [load V(i)]   S = K(i) Q^T (16 MFMA)                     ; store K(i+1) -> slot (i+1)&1
+//   A_i:     [load K(i+2)] O^T += V(i-1)^T P(i-1) (16 MFMA) || softmax(S) -> P(i) ; store V(i) -> slot i&1
+// and the softmax is a max-free fast path: p = exp2(c*s - m) against the current reference max m,
+// packed to bf16 at once, and a lane's tile partial sum rs checked once per tile.  Every p <= rs,
+// so rs <= SUM_THR (= 2^8) guarantees P <= 2^8 -- the bound of v1's lazy rescale (CDNA guide T13).
+// When any lane of the wave exceeds it (always on the first tile; later only when a row's max has
+// grown), the exact path runs after the tile's PV(i-1) MFMAs: row max, m' = max(m, max), O (which
+// already holds P(i-1)V(i-1) at the old scale) and l scaled by exp2(m - m'), P(i) recomputed.
+// Ring hazards (group 0 runs B_{i-1} at phase 2i and A_i at 2i+1, group 1 one phase later):
+// K(i+1) is written at 2i / 2i+1 into the slot K(i-1) was read from at 2i-2 / 2i-1 and first read
+// at 2i+2; V(i) is written at 2i+1 / 2i+2 into the slot V(i-2) was read from at 2i-1 / 2i and first
+// read at 2i+3.  Per-tile VALU ~580 issue cycles (v1 ~850: max tree + shuffle + a 32-register copy
+// of its two-deep S ring).  Epilogue: permlane32_swap pairs -> 16-B stores (CDNA guide T21).
+constexpr float SUM_THR = 256.0f;
+
+__global__ __launch_bounds__(NTHR) void attn_fwd_d128_v2(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    bf16_t* __restrict__ O, int Sq, int Skv, int H, long long ldq, long long ldk, long long ldv,
+    long long ldo, long long bsq, long long bsk, long long bsv, long long bso, float c, int nqb) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int g = xcd_remap(blockIdx.x, gridDim.x);
+    const int qb = g % nqb;
+    const int bh = g / nqb;
+    const int h = bh % H, b = bh / H;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, hh = lane >> 5;
+    const int q0 = qb * BQ + wave * 32;
+
+    const bf16_t* Qb = Q + (long long)b * bsq + h * HD;
+    const bf16_t* Kb = K + (long long)b * bsk + h * HD;
+    const bf16_t* Vb = V + (long long)b * bsv + h * HD;
+
+    const unsigned kbytes = (unsigned)min((long long)(Skv - 1) * ldk * 2 + HD * 2, 0xffffffffLL);
+    const unsigned vbytes = (unsigned)min((long long)(Skv - 1) * ldv * 2 + HD * 2, 0xffffffffLL);
+    const __amdgpu_buffer_rsrc_t krs = make_rsrc(Kb, kbytes), vrs = make_rsrc(Vb, vbytes);
+    const int srow = tid >> 4, sch = tid & 15;
+    const unsigned kvo0 = (unsigned)(srow * ldk * 2 + sch * 16), kvo1 = kvo0 + (unsigned)(32 * ldk * 2);
+    const unsigned vvo0 = (unsigned)(srow * ldv * 2 + sch * 16), vvo1 = vvo0 + (unsigned)(32 * ldv * 2);
+    const int kw = srow * KROW + sch * 16, vw = srow * VROW + sch * 16;
+
+    i32x4_t kst[2], vst[2];
+    auto load_k = [&](int kv0) {
+        const int ks = kv0 * (int)ldk * 2;
+        kst[0] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo0, ks, 0);
+        kst[1] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo1, ks, 0);
+    };
+    auto load_v = [&](int kv0) {
+        const int vs = kv0 * (int)ldv * 2;
+        vst[0] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo0, vs, 0);
+        vst[1] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo1, vs, 0);
+    };
+    auto store_k = [&](int slot) {
+        char* base = smem + slot * KT;
+        *reinterpret_cast<i32x4_t*>(base + kw) = kst[0];
+        *reinterpret_cast<i32x4_t*>(base + kw + 32 * KROW) = kst[1];
+    };
+    auto store_v = [&](int slot) {
+        char* base = smem + 2 * KT + slot * VT;
+        *reinterpret_cast<i32x4_t*>(base + vw) = vst[0];
+        *reinterpret_cast<i32x4_t*>(base + vw + 32 * VROW) = vst[1];
+    };
+
+    const int nkv = (Skv + BKV - 1) / BKV;
+    // prologue: K(0) staged and in LDS, K(1) in flight, Q fragments (B operand of S^T = K Q^T)
+    load_k(0);
+    bf16x8_t qf[8];
+    {
+        const int qrow = min(q0 + r, Sq - 1);
+        const bf16_t* qp = Qb + (long long)qrow * ldq + 8 * hh;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            // Q pre-scaled by c = log2(e)/sqrt(d) (one bf16 rounding): S^T then lands in the exp2
+            // domain and the softmax needs no multiply
+            const bf16x8_t raw = *reinterpret_cast<const bf16x8_t*>(qp + 16 * s);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)((float)raw[j] * c);
+        }
+    }
+    store_k(0);
+    if (nkv > 1) load_k(BKV);
+
+    f32x16_t o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+    // m: the row's reference max (exp2 domain).  The QK accumulators start at -m (negm, 16 copies
+    // of one per-lane value, rewritten only by the exact path), so S^T = c*QK^T - m and p = exp2(S).
+    // The first tile always takes the exact path, which sets m to that tile's row max.
+    float m = 0.f, l = 0.f;
+    f32x16_t negm;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) negm[i] = 0.f;
+
+    const int krd = r * KROW + 16 * hh;
+    const int g4 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+    const int vrd = (4 * (g4 >> 1) + q4) * VROW + 32 * (g4 & 1) + 8 * p4;
+
+    f32x16_t s[2];        // S^T of the current tile: keys 32t + (i&3) + 8(i>>2) + 4hh, row q0 + r
+    u32x4_t pk[4];        // P as the PV B operands (bf16 pairs): keys 16ks .. 16ks+15 of this lane's row
+    float rs0, rs1;
+    auto p_chunk = [&](int ss) {   // elements 4ss..4ss+3 (flat 16t + i) of the tile's 32 scores
+        const int t = ss >> 2, i0 = 4 * (ss & 3);
+        const float p0 = __builtin_amdgcn_exp2f(s[t][i0]);
+        const float p1 = __builtin_amdgcn_exp2f(s[t][i0 + 1]);
+        const float p2 = __builtin_amdgcn_exp2f(s[t][i0 + 2]);
+        const float p3 = __builtin_amdgcn_exp2f(s[t][i0 + 3]);
+        rs0 += p0 + p1;
+        rs1 += p2 + p3;
+        const int ks = 2 * t + (i0 >> 3), j = (i0 & 7) >> 1;
+        const bf16x2_t w0 = {(__bf16)p0, (__bf16)p1}, w1 = {(__bf16)p2, (__bf16)p3};
+        pk[ks][j] = __builtin_bit_cast(unsigned, w0);
+        pk[ks][j + 1] = __builtin_bit_cast(unsigned, w1);
+        // pin the chunk here: without it LLVM sinks the whole softmax below the PV MFMAs
+    };
+    auto qk = [&](int slot) {
+        const char* base = smem + slot * KT + krd;
+        bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(base);
+        bf16x8_t kb = *reinterpret_cast<const bf16x8_t*>(base + 32 * KROW);
+#pragma unroll
+        for (int ss = 0; ss < 8; ++ss) {
+            bf16x8_t na, nb;
+            if (ss + 1 < 8) {
+                na = *reinterpret_cast<const bf16x8_t*>(base + 32 * (ss + 1));
+                nb = *reinterpret_cast<const bf16x8_t*>(base + 32 * KROW + 32 * (ss + 1));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ss], ss == 0 ? negm : s[0], 0, 0, 0);
+            s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[ss], ss == 0 ? negm : s[1], 0, 0, 0);
+            if (ss + 1 < 8) {
+                ka = na;
+                kb = nb;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // PV(prev) with the fast softmax of the current tile interleaved: the 4 MFMAs of k-step ks read
+    // pk[ks] before the two chunks that overwrite it with P(i)
+    // V^T fragments of k-step ks (4 B operands, one per 32-column block dt of O^T)
+    auto read_vt = [&](const char* base, int ks, bf16x8_t* vf) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            const char* a0 = base + vrd + ks * 16 * VROW + 64 * dt;
+            const i16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_t*)(a0));
+            const i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_t*)(a0 + 8 * VROW));
+            vf[dt] = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, v0), __builtin_bit_cast(bf16x4_t, v1),
+                                             0, 1, 2, 3, 4, 5, 6, 7);
+        }
+    };
+    // PV(prev) with the fast softmax of the current tile interleaved: the 4 MFMAs of k-step ks read
+    // pk[ks] before the two chunks that overwrite it with P(i); V^T fragments one k-step ahead
+    auto pv_softmax = [&](int slot, bool with_pv) {
+        const char* base = smem + 2 * KT + slot * VT;
+        rs0 = 0.f;
+        rs1 = 0.f;
+        bf16x8_t va[4], vb[4];
+        if (with_pv) read_vt(base, 0, va);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            bf16x8_t* cur = (ks & 1) ? vb : va;
+            bf16x8_t* nxt = (ks & 1) ? va : vb;
+            if (with_pv) {
+                if (ks + 1 < 4) read_vt(base, ks + 1, nxt);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[dt], __builtin_bit_cast(bf16x8_t, pk[ks]),
+                                                                    o[dt], 0, 0, 0);
+            }
+            p_chunk(2 * ks);
+            p_chunk(2 * ks + 1);
+            // pure VALU floats freely in the DAG (a sched_barrier alone does not hold it): tie the
+            // chunk's sums to this point so its exps land in this k-step's MFMA region
+            asm volatile("" : "+v"(rs0), "+v"(rs1));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    auto pv_last = [&](int slot) {
+        const char* base = smem + 2 * KT + slot * VT;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const char* a0 = base + vrd + ks * 16 * VROW + 64 * dt;
+                const i16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_t*)(a0));
+                const i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_t*)(a0 + 8 * VROW));
+                const bf16x8_t vf = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, v0),
+                                                            __builtin_bit_cast(bf16x4_t, v1), 0, 1, 2, 3,
+                                                            4, 5, 6, 7);
+                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, __builtin_bit_cast(bf16x8_t, pk[ks]), o[dt], 0, 0, 0);
+            }
+    };
+    auto exact = [&](bool first) {
+        float mx = s[0][0];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[t][i]);
+        // S = c*qk - m, so the row's scaled max is max(S) + m
+        mx = fmaxf(mx, __shfl_xor(mx, 32)) + m;
+        const float mnew = first ? mx : fmaxf(m, mx);
+        const float delta = m - mnew;           // <= 0 after the first tile
+        // first tile: O and l are still 0 and delta is unbounded (exp2 may be inf): scale by 0
+        const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(delta);
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+        m = mnew;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[t][i] += delta;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) negm[i] = -mnew;
+        rs0 = 0.f;
+        rs1 = 0.f;
+#pragma unroll
+        for (int ss = 0; ss < 8; ++ss) p_chunk(ss);
+    };
+
+    auto phase_bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    __syncthreads();
+    const int grp = wave >> 2;
+    if (grp == 1) phase_bar();
+    for (int it = 0; it < nkv; ++it) {
+        // ---- B_{it-1}
+        load_v(it * BKV);
+        qk(it & 1);
+        if (it + 1 < nkv) store_k((it + 1) & 1);
+        phase_bar();
+        // ---- A_it
+        if (it + 2 < nkv) load_k((it + 2) * BKV);
+        if ((it + 1) * BKV > Skv) {
+            asm volatile("");
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int key = it * BKV + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
+                    if (key >= Skv) s[t][i] = -INFINITY;
+                }
+        }
+        if (it > 0)
+            pv_softmax((it - 1) & 1, true);
+        else
+            pv_softmax(0, false);
+        if (__any(rs0 + rs1 > SUM_THR) || it == 0) exact(it == 0);
+        l += rs0 + rs1;
+        store_v(it & 1);
+        phase_bar();
+    }
+    // ---- B_{nkv-1}: the last tile's PV.  Group 0 first waits for group 1's half of V(nkv-1)
+    // (stored in group 1's A_{nkv-1}, one phase later): the extra barrier that balances the count
+    if (grp == 0) phase_bar();
+    pv_last((nkv - 1) & 1);
+
+    const float lt = l + __shfl_xor(l, 32);
+    const float inv = 1.f / lt;
+    // lane (r, hh) holds columns 32dt + 8gi + 4hh .. +3 of row q0+r; pair groups (gi, gi+1) through
+    // one permlane32_swap per dword so each lane stores 16 contiguous bytes
+    u32x4_t w[8];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int gp = 0; gp < 2; ++gp) {
+            const int gi = 2 * gp;
+            const unsigned ax = pack2(o[dt][4 * gi] * inv, o[dt][4 * gi + 1] * inv);
+            const unsigned ay = pack2(o[dt][4 * gi + 2] * inv, o[dt][4 * gi + 3] * inv);
+            const unsigned bx = pack2(o[dt][4 * gi + 4] * inv, o[dt][4 * gi + 5] * inv);
+            const unsigned by = pack2(o[dt][4 * gi + 6] * inv, o[dt][4 * gi + 7] * inv);
+            const auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+            const auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+            w[2 * dt + gp][0] = sx[0];
+            w[2 * dt + gp][1] = sy[0];
+            w[2 * dt + gp][2] = sx[1];
+            w[2 * dt + gp][3] = sy[1];
+        }
+    if (q0 + r < Sq) {
+        bf16_t* op = O + (long long)b * bso + (long long)(q0 + r) * ldo + h * HD + 8 * hh;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) *reinterpret_cast<u32x4_t*>(op + 16 * k) = w[k];
+    }
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
@@ -302,14 +598,18 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
     const int nqb = (sq + BQ - 1) / BQ;
     const long long nwg = (long long)nqb * heads * batch;
     if (nwg > 0x7fffffff) return VS_E_INVALID;
-    static bool attr_set = false;
-    if (!attr_set) {
+    // VS_ATTN_IMPL=1 selects the v1 kernel (A/B measurements); default v2
+    static int impl = -1;
+    if (impl < 0) {
+        const char* e = getenv("VS_ATTN_IMPL");
+        impl = (e && e[0] == '1') ? 1 : 2;
         (void)hipFuncSetAttribute((const void*)attn_fwd_d128, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            LDS_BYTES);
-        attr_set = true;
+                                  LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)attn_fwd_d128_v2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS_BYTES);
     }
     const float c = scale * 1.4426950408889634f;
-    hipLaunchKernelGGL(attn_fwd_d128, dim3((unsigned)nwg), dim3(NTHR), LDS_BYTES,
+    hipLaunchKernelGGL(impl == 1 ? attn_fwd_d128 : attn_fwd_d128_v2, dim3((unsigned)nwg), dim3(NTHR), LDS_BYTES,
                        (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                        (bf16_t*)o, sq, skv, heads, ldq, ldk, ldv, ldo, bsq, bsk, bsv, bso, c, nqb);
     VS_CHECK_LAUNCH();
