@@ -280,10 +280,50 @@ def vace_forward(x, vace_context, ctx, t_mod, freqs, W, vace_layers, num_heads, 
     return hints
 
 
+class TeaCacheOracle:
+    """TeaCache, wan_video_new.py:1154-1203 (check / store / update on bf16 CPU tensors)."""
+    COEFFICIENTS = {
+        "Wan2.1-T2V-1.3B": [-5.21862437e+04, 9.23041404e+03, -5.28275948e+02, 1.36987616e+01, -4.99875664e-02],
+        "Wan2.1-T2V-14B": [-3.03318725e+05, 4.90537029e+04, -2.65530556e+03, 5.87365115e+01, -3.15583525e-01],
+        "Wan2.1-I2V-14B-480P": [2.57151496e+05, -3.54229917e+04, 1.40286849e+03, -1.35890334e+01, 1.32517977e-01],
+        "Wan2.1-I2V-14B-720P": [8.10705460e+03, 2.13393892e+03, -3.72934672e+02, 1.66203073e+01, -4.17769401e-02],
+    }
+
+    def __init__(self, num_inference_steps, rel_l1_thresh, model_id):
+        self.n, self.thresh, self.coef = num_inference_steps, rel_l1_thresh, self.COEFFICIENTS[model_id]
+        self.step, self.acc, self.prev_mod, self.prev_hidden, self.residual = 0, 0, None, None, None
+        self.decisions = []
+
+    def check(self, x, t_mod):
+        import numpy as np
+        mod = t_mod.clone()
+        if self.step == 0 or self.step == self.n - 1:
+            calc, self.acc = True, 0
+        else:
+            self.acc += np.poly1d(self.coef)(((mod - self.prev_mod).abs().mean() / self.prev_mod.abs().mean()).item())
+            calc = not self.acc < self.thresh
+            if calc:
+                self.acc = 0
+        self.prev_mod = mod
+        self.step = (self.step + 1) % self.n
+        if calc:
+            self.prev_hidden = x.clone()
+        self.decisions.append(calc)
+        return not calc
+
+    def store(self, x):
+        self.residual = x - self.prev_hidden
+        self.prev_hidden = None
+
+    def update(self, x):
+        return x + self.residual
+
+
 def model_fn(W, cfg, latents, timestep, context, vace_context=None, vace_scale=1.0, num_layers=None,
-             skip_blocks=()):
-    """model_fn_wan_video, wan_video_new.py:1338-1468 (non-S2V, non-animate, no TeaCache,
-    no sliding window, no SP).  `timestep` is the (B,) bf16 tensor of wan_video_new.py:526.
+             skip_blocks=(), tea_cache=None):
+    """model_fn_wan_video, wan_video_new.py:1338-1468 (non-S2V, non-animate, no sliding window,
+    no SP; TeaCache as :1398-1402,1418-1419,1455-1456).  `timestep` is the (B,) bf16 tensor of
+    wan_video_new.py:526.
     skip_blocks: skip-layer guidance of config 5 (ComfyUI WanVideoSLG, external): the listed main
     blocks -- and the VACE hint added after them -- are skipped."""
     D, H, eps = cfg["dim"], cfg["num_heads"], cfg["eps"]
@@ -294,28 +334,36 @@ def model_fn(W, cfg, latents, timestep, context, vace_context=None, vace_scale=1
     freqs = rope_freqs(f, h, w, D // H)
     hints = None
     vmap = {}
-    if vace_context is not None:
-        hints = vace_forward(x, vace_context, ctx, t_mod, freqs, W, cfg["vace_layers"], H, eps)
-        vmap = {layer: n for n, layer in enumerate(cfg["vace_layers"])}
-    for i in range(L):
-        if i in skip_blocks:
-            continue
-        x = dit_block(x, ctx, t_mod, freqs, W, f"blocks.{i}.", H, eps)
-        if hints is not None and i in vmap:                       # :1445-1450
-            x = add(x, bf(hints[vmap[i]].float() * vace_scale))
+    tea_update = tea_cache.check(x, t_mod) if tea_cache is not None else False
+    if tea_update:                                                # :1418-1419
+        x = tea_cache.update(x)
+    else:
+        if vace_context is not None:
+            hints = vace_forward(x, vace_context, ctx, t_mod, freqs, W, cfg["vace_layers"], H, eps)
+            vmap = {layer: n for n, layer in enumerate(cfg["vace_layers"])}
+        for i in range(L):
+            if i in skip_blocks:
+                continue
+            x = dit_block(x, ctx, t_mod, freqs, W, f"blocks.{i}.", H, eps)
+            if hints is not None and i in vmap:                   # :1445-1450
+                x = add(x, bf(hints[vmap[i]].float() * vace_scale))
+        if tea_cache is not None:
+            tea_cache.store(x)                                    # :1455-1456
     x = head(x, t, W, eps)
     return unpatchify(x, (f, h, w), cfg["out_dim"])
 
 
 def denoise(W, cfg, latents, context_pos, context_neg, vace_context=None, num_inference_steps=2,
-            cfg_scale=5.0, sigma_shift=5.0, vace_scale=1.0, num_layers=None):
-    """WanVideoPipeline.__call__ denoise loop, wan_video_new.py:484,515-542 (cfg_merge=False)."""
+            cfg_scale=5.0, sigma_shift=5.0, vace_scale=1.0, num_layers=None, tea_caches=None):
+    """WanVideoPipeline.__call__ denoise loop, wan_video_new.py:484,515-542 (cfg_merge=False).
+    tea_caches: (posi, nega) TeaCacheOracle pair -- one per prompt, as WanVideoUnit_TeaCache."""
     sigmas, timesteps = set_timesteps(num_inference_steps, 1.0, sigma_shift)
+    tp, tn = tea_caches if tea_caches is not None else (None, None)
     for i, ts in enumerate(timesteps):
         t = ts.unsqueeze(0).to(BF16)                                 # :526
-        vp = model_fn(W, cfg, latents, t, context_pos, vace_context, vace_scale, num_layers)
+        vp = model_fn(W, cfg, latents, t, context_pos, vace_context, vace_scale, num_layers, tea_cache=tp)
         if cfg_scale != 1.0:
-            vn = model_fn(W, cfg, latents, t, context_neg, vace_context, vace_scale, num_layers)
+            vn = model_fn(W, cfg, latents, t, context_neg, vace_context, vace_scale, num_layers, tea_cache=tn)
             latents = cfg_euler(vp, vn, latents, cfg_scale, euler_delta(sigmas, i))
         else:
             latents = bf(latents.float() + bf(vp.float() * euler_delta(sigmas, i)).float())

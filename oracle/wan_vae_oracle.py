@@ -438,9 +438,28 @@ def preprocess_video(frames_u8, min_value=-1.0, max_value=1.0):
     return x.permute(3, 0, 1, 2).unsqueeze(0)
 
 
+def encode_list(videos, W, tiled=False, tile_size=(34, 34), tile_stride=(18, 16), cfg=VAE_CONFIG):
+    """WanVideoVAE.encode over a list of (3, T, H, W) videos (wan_video_vae.py:1218-1232) -> stacked
+    latents.  Reproduces the reference's in-loop `tile_size = tile_size * upsampling_factor`
+    (:1224-1225): the j-th video of the list is tiled with tile_size/stride x 8^j (latent units)."""
+    outs = []
+    ts, st = tuple(tile_size), tuple(tile_stride)
+    for v in videos:
+        v = v.unsqueeze(0)
+        if tiled:
+            outs.append(tiled_encode(v, W, ts, st, cfg)[0])
+            ts, st = (ts[0] * 8, ts[1] * 8), (st[0] * 8, st[1] * 8)
+        else:
+            outs.append(vae_encode(v, W, cfg)[0])
+    return torch.stack(outs)
+
+
 def vace_context(W, vace_video=None, vace_video_mask=None, num_frames=None, height=None, width=None,
-                 tiled=True, tile_size=(30, 52), tile_stride=(15, 26), cfg=VAE_CONFIG):
-    """WanVideoUnit_VACE.process without reference images: returns (1, 96, T', H/8, W/8)."""
+                 tiled=True, tile_size=(30, 52), tile_stride=(15, 26), cfg=VAE_CONFIG, vace_reference_image=None):
+    """WanVideoUnit_VACE.process (wan_video_new.py:875-920): returns (1, 96, f + T', H/8, W/8), f = the
+    number of reference images (preprocessed bf16 (1, 3, f, H, W) or None).  Reference images:
+    each frame is encoded as its own video (:903-909), concatenated with 16 zero channels, and
+    prepended along time to the video latents; the mask latents get f zero frames (:911-912)."""
     if vace_video is None:
         vace_video = torch.zeros((1, 3, num_frames, height, width), dtype=BF16)
     if vace_video_mask is None:
@@ -454,6 +473,13 @@ def vace_context(W, vace_video=None, vace_video_mask=None, num_frames=None, heig
     T, H, Wd = m.shape
     m = m.reshape(T, H // 8, 8, Wd // 8, 8).permute(2, 4, 0, 1, 3).reshape(1, 64, T, H // 8, Wd // 8)
     m = F.interpolate(m, size=((T + 3) // 4, H // 8, Wd // 8), mode="nearest-exact")
+    if vace_reference_image is not None:
+        f = vace_reference_image.shape[2]
+        refs = [vace_reference_image[0, :, j:j + 1] for j in range(f)]
+        rl = encode_list(refs, W, tiled, tile_size, tile_stride, cfg)              # (f, 16, 1, h, w)
+        rl = torch.cat((rl, torch.zeros_like(rl)), dim=1)
+        lat = torch.cat((*[u.unsqueeze(0) for u in rl], lat), dim=2)
+        m = torch.cat((torch.zeros_like(m[:, :, :f]), m), dim=2)
     return torch.cat((lat, m), dim=1)
 
 

@@ -89,6 +89,76 @@ def test_vace_context_vs_oracle(with_mask):
     assert rel <= 1.5 * frel + 1e-3 and mx <= 1.5 * fmx + 1e-2
 
 
+@pytest.mark.parametrize("nref", [1, 2])
+def test_vace_context_reference_images_vs_oracle(nref):
+    """WanVideoUnit_VACE.process with vace_reference_image (wan_video_new.py:896-912): each reference
+    frame encoded as its own video -- the second one with the reference's compounded x8 tile size
+    (wan_video_vae.py:1224-1225) -- and prepended along time; mask latents get zero frames."""
+    from vstyler.vae import vace_context
+    Wv = V.random_vae_weights(TINY_VAE, seed=33)
+    T, H, W = 5, 64, 96
+    video = _frames(T, H, W, 6)
+    refs = _frames(nref, H, W, 7)
+    vin = V.preprocess_video(video)
+    rin = V.preprocess_video(refs)
+
+    def ref_fn():
+        return V.vace_context(Wv, vin, None, tiled=True, tile_size=TS, tile_stride=ST, cfg=TINY_VAE,
+                              vace_reference_image=rin)
+
+    old = O.ACC_DTYPE
+    O.ACC_DTYPE = torch.float64
+    r64 = ref_fn()
+    O.ACC_DTYPE = old
+    ref = ref_fn()
+    got = vace_context(_vae_model(Wv), video, None, tiled=True, tile_size=TS, tile_stride=ST,
+                       vace_reference_image=[f.numpy() for f in refs])
+    assert got.shape == ref.shape == (1, 96, nref + 2, 8, 12)
+    assert torch.equal(got[:, 16:32, :nref].cpu(), ref[:, 16:32, :nref]) and not got[:, 16:32, :nref].any()
+    assert torch.equal(got[:, 32:].cpu(), ref[:, 32:])
+    fmx, frel = err(r64[:, :32], ref[:, :32])
+    mx, rel = err(got[:, :32], ref[:, :32])
+    print(f"vace_context + {nref} ref: max-abs {mx:.4g} rel-L2 {rel:.4g} (floor {fmx:.4g} / {frel:.4g})")
+    assert rel <= 1.5 * frel + 1e-3 and mx <= 1.5 * fmx + 1e-2
+
+
+def test_pipeline_reference_image_latents():
+    """__call__ with vace_reference_image: rolled noise over T'+1 latent frames, the reference frame
+    dropped after denoising (wan_video_new.py:545-550, 578-587)."""
+    from vstyler import WanVideoPipeline
+    cfg = O.WAN_CONFIGS["tiny"]
+    W = O.random_weights(cfg, seed=5)
+    Wv = V.random_vae_weights(TINY_VAE, seed=34)
+    T, H, Wd = 5, 64, 96
+    video, refimg = _frames(T, H, Wd, 8), _frames(1, H, Wd, 9)
+    _, cp, cn, _ = O.synthetic_inputs(cfg, T, H, Wd)
+    pipe = WanVideoPipeline(device="cuda")
+    pipe.dit, pipe.vace = build(cfg, W)
+    pipe.vae = _vae_model(Wv)
+    got = pipe(prompt_emb=cp, negative_prompt_emb=cn, vace_video=list(video.numpy()),
+               vace_reference_image=refimg[0].numpy(), seed=3, height=H, width=Wd, num_frames=T,
+               num_inference_steps=2, tile_size=TS, tile_stride=ST, output_type="latents")
+    t_lat = (T - 1) // 4 + 1
+    assert got.shape == (1, 16, t_lat, H // 8, Wd // 8)
+
+    def chain():
+        vc = V.vace_context(Wv, V.preprocess_video(video), None, tiled=True, tile_size=TS, tile_stride=ST,
+                            cfg=TINY_VAE, vace_reference_image=V.preprocess_video(refimg))
+        lat = O.generate_noise((1, 16, t_lat + 1, H // 8, Wd // 8), 3)
+        lat = torch.cat((lat[:, :, -1:], lat[:, :, :-1]), dim=2)
+        return O.denoise(W, cfg, lat, cp, cn, vc, num_inference_steps=2)[:, :, 1:]
+
+    ref = chain()
+    old = O.ACC_DTYPE
+    O.ACC_DTYPE = torch.float64
+    ref64 = chain()
+    O.ACC_DTYPE = old
+    fmx, frel = err(ref64, ref)
+    mx, rel = err(got, ref)
+    print(f"ref-image latents: max-abs {mx:.4g} rel-L2 {rel:.4g} (floor {fmx:.4g} / {frel:.4g})")
+    assert rel <= 1.5 * frel + 2e-3 and mx <= 1.5 * fmx + 2e-2
+
+
 def test_pipeline_end_to_end_tiny():
     """WanVideoPipeline.__call__(vace_video=PIL frames, ...) -> PIL frames, vs the oracle chain."""
     from PIL import Image
@@ -124,3 +194,41 @@ def test_pipeline_end_to_end_tiny():
     print(f"e2e uint8: mean |d| {d.mean().item():.3f} max {d.max().item():.0f}; oracle fp32-vs-fp64 floor: "
           f"mean {f.mean().item():.3f} max {f.max().item():.0f}")
     assert d.mean().item() <= 1.5 * f.mean().item() + 0.1 and d.max().item() <= 2 * f.max().item() + 4
+
+
+def test_teacache_decisions_and_latents_vs_oracle():
+    """TeaCache (wan_video_new.py:1154-1203): same skip decisions as the restated reference cache and
+    latents within the fp32/fp64 noise floor.  The tiny random model's t_mod changes ~50 % per step
+    (real checkpoints: a few %); a +0.25 shift of the time_projection bias brings the relative L1 to
+    ~1.5-1.9 % per step, where the T2V-1.3B polynomial gives ~0.07 per step, and th = 0.2 then
+    computes every third step: [T, F, F, T, F, F, T, T] with >= 0.016 margin at every decision."""
+    from vstyler import WanVideoPipeline
+    from vstyler.teacache import TeaCache
+    cfg = O.WAN_CONFIGS["tiny"]
+    W = dict(O.random_weights(cfg, seed=5))
+    W["time_projection.1.bias"] = (W["time_projection.1.bias"].float() + 0.25).to(BF16)
+    T, H, Wd = 5, 64, 96
+    lat0, cp, cn, vc = O.synthetic_inputs(cfg, T, H, Wd)
+    n, th, mid = 8, 0.2, "Wan2.1-T2V-1.3B"
+
+    def oracle():
+        caches = (O.TeaCacheOracle(n, th, mid), O.TeaCacheOracle(n, th, mid))
+        out = O.denoise(W, cfg, lat0.clone(), cp, cn, vc, num_inference_steps=n, tea_caches=caches)
+        assert caches[0].decisions == caches[1].decisions
+        return out, caches[0].decisions
+
+    ref, dec = oracle()
+    assert dec == [True, False, False, True, False, False, True, True], dec
+    pipe = WanVideoPipeline(device="cuda")
+    pipe.dit, pipe.vace = build(cfg, W)
+    tc = TeaCache(n, th, mid)
+    got = pipe.denoise(lat0.cuda(), cp.cuda(), cn.cuda(), vc.cuda(), num_inference_steps=n, tea_cache=tc)
+    assert tc.decisions == dec, (tc.decisions, dec)
+    old = O.ACC_DTYPE
+    O.ACC_DTYPE = torch.float64
+    ref64, _ = oracle()
+    O.ACC_DTYPE = old
+    fmx, frel = err(ref64, ref)
+    mx, rel = err(got, ref)
+    print(f"teacache th={th} decisions {dec}: max-abs {mx:.4g} rel-L2 {rel:.4g} (floor {fmx:.4g} / {frel:.4g})")
+    assert rel <= 1.5 * frel + 2e-3 and mx <= 1.5 * fmx + 2e-2

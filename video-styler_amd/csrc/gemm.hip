@@ -431,6 +431,182 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
 
 
 // ---------------------------------------------------------------------------------------------
+// 256x256 tile, 4 waves (one per SIMD), 128x128 output per wave: the accumulators (256 fp32 per
+// lane) live in AGPRs, which the MFMAs read and write directly, so a wave owns 64 MFMAs
+// (16x16x32) per 32-deep K half-step against 16 fragment reads (vs 32 against 12 in the 8-wave
+// ping-pong kernel).  Same LDS ring (RING x 32 KB slots, LDS-DMA three half-steps ahead, 64-B rows,
+// chunk swizzle) as gemm_bf16_tn_256.  Per half-step h, every wave runs
+//   [vmcnt: own DMA of h+1 landed; s_barrier] [DMA h+RING-1 -> slot of h-1] [frags(h+1) -> other
+//   register set] [64 MFMAs(h)]
+// one barrier per half-step: passing it proves (a) every wave's pieces of h+1 have landed (RAW)
+// and (b) every wave has consumed frags(h-1) (their lgkmcnt wait precedes MFMAs(h-1)), so slot
+// (h-1) % RING is free for the DMA issued right after it (WAR).
+// ---------------------------------------------------------------------------------------------
+constexpr int NTHR4 = 256;
+
+__global__ __launch_bounds__(NTHR4, 1) void gemm_bf16_tn_w4(
+    const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
+    bf16_t* C, long long ldc, int M, int N, int K, const bf16_t* __restrict__ A2, long long lda2,
+    const bf16_t* __restrict__ W2, long long ldw2, int K2, Epi ep, int ntm, int ntn) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int pid = xcd_remap(blockIdx.x, gridDim.x);
+    constexpr int GM = VS_GEMM_GM;
+    const int per_group = GM * ntn;
+    const int group = pid / per_group;
+    const int first_m = group * GM;
+    const int gsz = min(ntm - first_m, GM);
+    const int in_g = pid % per_group;
+    const int tm = first_m + in_g % gsz;
+    const int tn = in_g / gsz;
+    const int m0 = tm * BT, n0 = tn * BT;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+
+    f32x4_t acc[8][8];
+
+    // LDS-DMA: a half-step is 32 pieces of 1 KB (16 rows x 64 B); wave w issues A rows
+    // 64w..64w+63 (pieces 4w..4w+3 of the A half) and W rows 64w..64w+63.  Lane L -> row
+    // 16j + L/4 of its piece, physical chunk L%4, logical chunk (L%4) ^ ((3*((L/4)>>2))&3).
+    const int prow = lane >> 2;
+    const int pch = (lane & 3) ^ ((3 * (prow >> 2)) & 3);
+    const int nh1 = K / HK;
+    const int nh = nh1 + K2 / HK;
+    const int arow = m0 + wave * 64 + prow, wrow = n0 + wave * 64 + prow;
+    const int alim = M - 1, wlim = N - 1;
+    // buffer-addressed DMA (host guarantees every byte offset fits 32 bits): the per-lane row
+    // offsets are 8 loop-invariant VGPRs, the K offset of a half-step goes to soffset
+    auto rsrc = [](const void* base) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t ra = rsrc(A), rw = rsrc(W);
+    unsigned voa[4], vow[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        voa[j] = (unsigned)min(arow + j * 16, alim) * (unsigned)(lda * 2) + pch * 16;
+        vow[j] = (unsigned)min(wrow + j * 16, wlim) * (unsigned)(ldw * 2) + pch * 16;
+    }
+    int issued = -1;
+    auto issue = [&](int h) {
+        char* dst = smem + (h % RING) * SLOT + wave * 4 * 1024;
+        if (h < nh1) {
+            const unsigned ko = (unsigned)h * HK * 2;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(dst + j * 1024), 16, voa[j], ko, 0, 0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (LDS_AS void*)(dst + BT * 64 + j * 1024), 16, vow[j], ko,
+                                                         0, 0);
+        } else {
+            // second K phase (un-merged LoRA): A2 . W2^T
+            const unsigned ko = (unsigned)(h - nh1) * HK * 2;
+            const __amdgpu_buffer_rsrc_t ra2 = rsrc(A2), rw2 = rsrc(W2);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    ra2, (LDS_AS void*)(dst + j * 1024), 16,
+                    (unsigned)min(arow + j * 16, alim) * (unsigned)(lda2 * 2) + pch * 16, ko, 0, 0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rw2, (LDS_AS void*)(dst + BT * 64 + j * 1024), 16,
+                    (unsigned)min(wrow + j * 16, wlim) * (unsigned)(ldw2 * 2) + pch * 16, ko, 0, 0);
+        }
+        issued = h;
+    };
+    // barrier after this wave's DMA of half-step `need` has landed (8 pieces per half-step)
+    auto bar_for = [&](int need) {
+        const int after = issued - need;
+        __builtin_amdgcn_sched_barrier(0);
+        if (after >= 2)
+            asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+        else if (after == 1)
+            asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    const int frow = lane & 15, fch = lane >> 4;
+    auto read_frags = [&](int h, bf16x8_t* af, bf16x8_t* wf) {
+        const char* As = smem + (h % RING) * SLOT;
+        const char* Bs = As + BT * 64;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            wf[j] = *reinterpret_cast<const bf16x8_t*>(Bs + h_off(wn * 128 + j * 16 + frow, fch));
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            af[i] = *reinterpret_cast<const bf16x8_t*>(As + h_off(wm * 128 + i * 16 + frow, fch));
+    };
+    // accumulators pinned to AGPRs ("+a"), fragments in VGPRs: left to itself hipcc splits the
+    // 512-register file badly (fragments in AGPRs, ~1200 accvgpr copies and 355 spilled registers)
+    // accumulators live in AGPRs ("+a"; born there from the srcC = 0 form of the first half-step),
+    // fragments and addresses in VGPRs.  Left to itself hipcc splits the 512-register file badly
+    // (fragments in AGPRs and ~1200 accvgpr copies per tile, or accumulators spilled to AGPRs).
+    auto mfmas = [&](const bf16x8_t* af, const bf16x8_t* wf) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(wf[j]), "v"(af[i]));
+    };
+    auto mfmas_first = [&](const bf16x8_t* af, const bf16x8_t* wf) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc[i][j]) : "v"(wf[j]), "v"(af[i]));
+    };
+
+    bf16x8_t a0[8], w0[8], a1[8], w1[8];
+#pragma unroll
+    for (int j = 0; j < RING - 1; ++j)
+        if (j < nh) issue(j);
+    bar_for(0);
+    read_frags(0, a0, w0);
+    // half-step 0 (peeled: it creates the accumulators)
+    if (1 < nh) bar_for(1);
+    if (RING - 1 < nh) issue(RING - 1);
+    if (1 < nh) read_frags(1, a1, w1);
+    mfmas_first(a0, w0);
+    for (int h = 1; h < nh; h += 2) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int hc = h + e;
+            if (hc >= nh) break;
+            if (hc + 1 < nh) bar_for(hc + 1);
+            if (hc + RING - 1 < nh) issue(hc + RING - 1);
+            if (e == 0) {
+                if (hc + 1 < nh) read_frags(hc + 1, a0, w0);
+                mfmas(a1, w1);
+            } else {
+                if (hc + 1 < nh) read_frags(hc + 1, a1, w1);
+                mfmas(a0, w0);
+            }
+        }
+    }
+
+    // the last inline-asm MFMAs' results are read by VALU (accvgpr reads): the hazard recognizer
+    // does not see through inline asm, so wait out the 16x16x32 pipeline explicitly
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int n = n0 + wn * 128 + j * 16 + 4 * (lane >> 4);
+            if (n >= N) continue;
+            epilogue_store(acc[i][j], m, n, C, ldc, ep);
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------------
 // fp8 e4m3 (OCP) GEMM for the fp8 path (config 5; AutoWrappedLinear.fp8_linear,
 // diffsynth/vram_management/layers.py:115-151): C = epilogue(scale_a[m] * (A8 . W8^T)) with the
 // activations quantised per row by vs_quant_fp8_rows and unscaled fp8 weights (scale_b = 1).
@@ -660,11 +836,26 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
                           : k >= 4096 && (long long)((m + BT - 1) / BT) * ((n + BT - 1) / BT) >= 240;
     if (big) {
         const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
-        static bool attr256 = false;
-        if (!attr256) {
+        static int impl = -1;
+        if (impl < 0) {
             (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_256,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, RING * SLOT);
-            attr256 = true;
+            (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_w4,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, RING * SLOT);
+            const char* e = getenv("VS_GEMM_IMPL");     // 4: one-wave-per-SIMD kernel (A/B)
+            impl = (e && e[0] == '4') ? 4 : 8;
+        }
+        const bool fits32 = (long long)(m - 1) * lda * 2 + (long long)k * 2 < 0x7fffffffLL &&
+                            (long long)(n - 1) * ldw * 2 + (long long)k * 2 < 0x7fffffffLL &&
+                            (k2 == 0 || ((long long)(m - 1) * lda2 * 2 + (long long)k2 * 2 < 0x7fffffffLL &&
+                                         (long long)(n - 1) * ldw2 * 2 + (long long)k2 * 2 < 0x7fffffffLL));
+        if (impl == 4 && fits32) {
+            hipLaunchKernelGGL(gemm_bf16_tn_w4, dim3((unsigned)(tm * tn)), dim3(NTHR4), RING * SLOT,
+                               (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw,
+                               (bf16_t*)c, ldc, m, n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2,
+                               k2, ep, tm, tn);
+            VS_CHECK_LAUNCH();
+            return VS_OK;
         }
         hipLaunchKernelGGL(gemm_bf16_tn_256, dim3((unsigned)(tm * tn)), dim3(NTHR8), RING * SLOT,
                            (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw,

@@ -31,13 +31,13 @@ def _workspace(device):
 
 _UNSUPPORTED = ("clip_feature", "y", "reference_latents", "audio_embeds", "motion_latents", "s2v_pose_latents",
                 "motion_bucket_id", "pose_latents", "face_pixel_values", "control_camera_latents_input",
-                "sliding_window_size", "tea_cache")
+                "sliding_window_size")
 
 
 def model_fn_wan_video(dit: WanModel, motion_controller=None, vace: VaceWanModel = None, animate_adapter=None,
                        latents: torch.Tensor = None, timestep: torch.Tensor = None, context: torch.Tensor = None,
                        vace_context=None, vace_scale=1.0, use_unified_sequence_parallel: bool = False,
-                       sp_group=None, slg_blocks=(), **kwargs):
+                       sp_group=None, slg_blocks=(), tea_cache=None, **kwargs):
     """One DiT(+VACE) forward (wan_video_new.py:1338-1468) -> [B,16,T,H,W] bf16 velocity.
 
     slg_blocks: skip-layer guidance (config 5, ComfyUI WanVideoSLG): the listed main blocks are
@@ -80,15 +80,24 @@ def model_fn_wan_video(dit: WanModel, motion_controller=None, vace: VaceWanModel
             vc = vc.expand(B, *vc.shape[1:])
         vace_x, _ = vace.vace_patch_embedding(vc.contiguous(), ws, "vace")
 
+    # TeaCache (wan_video_new.py:1398-1402): decided on one prompt's t_mod before the blocks
+    tea_skip = tea_cache.check(dit, x, t_mod[0:1]) if tea_cache is not None else False
     if sp is not None:
         x, vace_x, rc = sp.shard_tokens(x, vace_x, rc)
 
-    hints = vace(x, vace_x, t_mod, rc) if vace_x is not None else None
-    vmap = vace.vace_layers_mapping if hints is not None else {}
-    for i, blk in enumerate(dit.blocks):
-        hint = hints[vmap[i]] if i in vmap else None
-        skip = B > 1 and i in slg_blocks
-        blk(x, t_mod, rc, hint=hint, hint_scale=float(vace_scale), only_batch=0 if skip else None)
+    if tea_skip:
+        tea_cache.update(x)                                     # :1418-1419 (VACE not needed)
+    else:
+        if tea_cache is not None:
+            tea_cache.begin(x)
+        hints = vace(x, vace_x, t_mod, rc) if vace_x is not None else None
+        vmap = vace.vace_layers_mapping if hints is not None else {}
+        for i, blk in enumerate(dit.blocks):
+            hint = hints[vmap[i]] if i in vmap else None
+            skip = B > 1 and i in slg_blocks
+            blk(x, t_mod, rc, hint=hint, hint_scale=float(vace_scale), only_batch=0 if skip else None)
+        if tea_cache is not None:
+            tea_cache.store(x)                                  # :1455-1456
     out = dit.head(x, t, rc)
     if sp is not None:
         out = sp.gather_tokens(out, rc)
@@ -270,7 +279,7 @@ class WanVideoPipeline:
     # ---------------------------------------------------------------- denoise
     def denoise(self, latents, context_posi, context_nega, vace_context=None, vace_scale=1.0, cfg_scale=5.0,
                 num_inference_steps=50, sigma_shift=5.0, denoising_strength=1.0, progress_bar_cmd=None,
-                use_graph=None):
+                use_graph=None, tea_cache=None):
         """The loop of wan_video_new.py:515-542 (cfg_merge batched), returns the final latents.
 
         Step 0 runs eagerly (it also sizes the Workspace); the whole step -- model_fn (DiT + VACE,
@@ -284,7 +293,8 @@ class WanVideoPipeline:
         use_cfg = cfg_scale != 1.0
         if use_graph is None:
             use_graph = os.environ.get("VSTYLER_GRAPH", "1") != "0"
-        use_graph = use_graph and not self.use_unified_sequence_parallel and n_steps > 1
+        # TeaCache decides per step on the host (wan_video_new.py:1173-1192): eager steps
+        use_graph = use_graph and not self.use_unified_sequence_parallel and n_steps > 1 and tea_cache is None
         ctx = torch.cat([context_posi, context_nega], 0) if use_cfg else context_posi
         latents = latents.to(device=self.device, dtype=BF16).contiguous().clone()
         ts = self.scheduler.timesteps.to(dtype=BF16).to(self.device)                     # :526
@@ -295,7 +305,7 @@ class WanVideoPipeline:
             v = self.model_fn(dit=self.dit, vace=self.vace, latents=latents, timestep=t_buf, context=ctx,
                               vace_context=vace_context, vace_scale=vace_scale,
                               use_unified_sequence_parallel=self.use_unified_sequence_parallel,
-                              sp_group=self.sp_group)
+                              sp_group=self.sp_group, tea_cache=tea_cache)
             K.cfg_euler_dev(v[0:1], v[1:2] if use_cfg else None, latents, cfg_scale, d_buf)
 
         stepper = DenoiseStepper(step, ts, ds, use_graph)
@@ -354,24 +364,38 @@ class WanVideoPipeline:
                  prompt_emb=None, negative_prompt_emb=None, vace_context=None, output_type="video", **kwargs):
         """wan_video_new.py:416-560 for the Ditto path (T2V/VACE, no image/audio/camera inputs)."""
         for name, val in (("input_image", input_image), ("end_image", end_image), ("input_video", input_video),
-                          ("motion_bucket_id", motion_bucket_id), ("sliding_window_size", sliding_window_size),
-                          ("tea_cache_l1_thresh", tea_cache_l1_thresh), ("vace_reference_image", vace_reference_image)):
+                          ("motion_bucket_id", motion_bucket_id), ("sliding_window_size", sliding_window_size)):
             if val is not None:
                 raise NotImplementedError(f"{name} is outside the Ditto hot path of this build")
         height, width, num_frames = self.check_resize_height_width(height, width, num_frames)
         T = (num_frames - 1) // 4 + 1
-        noise = self.generate_noise((1, 16, T, height // 8, width // 8), seed=seed, rand_device=rand_device)
+        # WanVideoUnit_NoiseInitializer (wan_video_new.py:578-587): f reference images add f latent
+        # frames, and the noise is rolled so the last f frames come first
+        nref = 0
+        if vace_reference_image is not None:
+            nref = len(vace_reference_image) if isinstance(vace_reference_image, (list, tuple)) else 1
+        noise = self.generate_noise((1, 16, T + nref, height // 8, width // 8), seed=seed, rand_device=rand_device)
+        if nref:
+            noise = torch.cat((noise[:, :, -nref:], noise[:, :, :-nref]), dim=2)
         if prompt_emb is None:
             prompt_emb = self.encode_prompt(prompt)
         if negative_prompt_emb is None and cfg_scale != 1.0:
             negative_prompt_emb = self.encode_prompt(negative_prompt)
-        if vace_context is None and (vace_video is not None or vace_video_mask is not None):
+        if vace_context is None and (vace_video is not None or vace_video_mask is not None or nref):
             vace_context = self.encode_vace(vace_video, vace_video_mask, height, width, num_frames, tiled,
-                                            tile_size, tile_stride)
+                                            tile_size, tile_stride, vace_reference_image)
+        tea_cache = None
+        if tea_cache_l1_thresh is not None:                # WanVideoUnit_TeaCache (:936-947)
+            from .teacache import TeaCache
+            tea_cache = TeaCache(num_inference_steps, rel_l1_thresh=tea_cache_l1_thresh, model_id=tea_cache_model_id)
         latents = self.denoise(noise, prompt_emb.to(self.device), None if negative_prompt_emb is None else
                                negative_prompt_emb.to(self.device),
                                None if vace_context is None else vace_context.to(self.device), vace_scale,
-                               cfg_scale, num_inference_steps, sigma_shift, denoising_strength, progress_bar_cmd)
+                               cfg_scale, num_inference_steps, sigma_shift, denoising_strength, progress_bar_cmd,
+                               tea_cache=tea_cache)
+        self.last_tea_cache = tea_cache
+        if nref:                                            # :545-550
+            latents = latents[:, :, nref:].contiguous()
         if output_type == "latents":
             return latents
         if self.vae is None:
@@ -384,8 +408,10 @@ class WanVideoPipeline:
             raise NotImplementedError("T5 text encoder not loaded: pass prompt_emb=/negative_prompt_emb=")
         return self.prompter.encode_prompt(prompt, device=self.device)
 
-    def encode_vace(self, vace_video, vace_video_mask, height, width, num_frames, tiled, tile_size, tile_stride):
-        """WanVideoUnit_VACE (wan_video_new.py:861-920): 2 tiled VAE encodes + mask latents."""
+    def encode_vace(self, vace_video, vace_video_mask, height, width, num_frames, tiled, tile_size, tile_stride,
+                    vace_reference_image=None):
+        """WanVideoUnit_VACE (wan_video_new.py:861-920): 2 tiled VAE encodes + mask latents (+ one
+        encode per reference image)."""
         if self.vae is None:
             raise RuntimeError("VACE video encoding requires a loaded Wan2.1 VAE (or pass vace_context=)")
         from .vae import vace_context
@@ -394,7 +420,7 @@ class WanVideoPipeline:
         if vace_video_mask is not None and not isinstance(vace_video_mask, torch.Tensor):
             vace_video_mask = list(vace_video_mask)[:num_frames]
         return vace_context(self.vae, vace_video, vace_video_mask, num_frames, height, width, tiled, tile_size,
-                            tile_stride)
+                            tile_stride, vace_reference_image)
 
     def vae_output_to_video(self, vae_output, output_type="video"):
         """BasePipeline.vae_output_to_video (utils/__init__.py:76-91): uint8 conversion on the GPU;

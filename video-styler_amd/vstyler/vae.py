@@ -464,7 +464,16 @@ class WanVideoVAE:
 
     # ---------------------------------------------------------------- reference API (:1218-1247)
     def encode(self, videos, device=None, tiled=False, tile_size=(34, 34), tile_stride=(18, 16)):
-        return torch.stack([self._encode_one(v, tiled, tile_size, tile_stride) for v in videos])
+        # the reference rebinds tile_size/tile_stride x upsampling_factor inside its loop (:1224-1225),
+        # so the j-th video of a list is tiled 8^j times coarser; reproduced for drop-in results
+        outs = []
+        ts, st = tuple(tile_size), tuple(tile_stride)
+        for v in videos:
+            outs.append(self._encode_one(v, tiled, ts, st))
+            if tiled:
+                f = self.upsampling_factor
+                ts, st = (ts[0] * f, ts[1] * f), (st[0] * f, st[1] * f)
+        return torch.stack(outs)
 
     def decode(self, hidden_states, device=None, tiled=False, tile_size=(34, 34), tile_stride=(18, 16)):
         return torch.stack([self._decode_one(z, tiled, tile_size, tile_stride) for z in hidden_states])
@@ -495,9 +504,11 @@ def frames_to_u8(frames, device):
 
 
 def vace_context(vae, vace_video=None, vace_video_mask=None, num_frames=None, height=None, width=None,
-                 tiled=True, tile_size=(30, 52), tile_stride=(15, 26)):
-    """WanVideoUnit_VACE.process (wan_video_new.py:861-920) without reference images:
-    -> vace_context (1, 96, (T+3)//4, H/8, W/8) bf16 = [encode(inactive) | encode(reactive) | mask latents]."""
+                 tiled=True, tile_size=(30, 52), tile_stride=(15, 26), vace_reference_image=None):
+    """WanVideoUnit_VACE.process (wan_video_new.py:861-920)
+    -> vace_context (1, 96, f + (T+3)//4, H/8, W/8) bf16 = [encode(inactive) | encode(reactive) | mask latents],
+    preceded along time by f reference-image frames [encode(ref_j) | 0 | 0] (:896-912) when
+    vace_reference_image (one image or a list of f images, each H x W) is given."""
     dev = vae.device
     v = None if vace_video is None else frames_to_u8(vace_video, dev)
     m = None if vace_video_mask is None else frames_to_u8(vace_video_mask, dev)
@@ -515,8 +526,34 @@ def vace_context(vae, vace_video=None, vace_video_mask=None, num_frames=None, he
     _lib.check(lib.vs_vace_prepare(None if v is None else v.data_ptr(), None if m is None else m.data_ptr(),
                                    inactive.data_ptr(), reactive.data_ptr(), mask0.data_ptr(), T, H, W, st))
     t_lat = (T + 3) // 4
-    out = torch.empty((1, 96, t_lat, H // 8, W // 8), dtype=BF16, device=dev)
-    out[:, 0:16] = vae.encode(inactive, dev, tiled=tiled, tile_size=tile_size, tile_stride=tile_stride)
-    out[:, 16:32] = vae.encode(reactive, dev, tiled=tiled, tile_size=tile_size, tile_stride=tile_stride)
-    _lib.check(lib.vs_vace_mask_latents(mask0.data_ptr(), out[0, 32:].data_ptr(), T, H, W, t_lat, st))
+    nref = 0
+    if vace_reference_image is not None:
+        if isinstance(vace_reference_image, torch.Tensor) and vace_reference_image.dim() == 4:
+            refs = vace_reference_image                     # (f, H, W, 3) uint8
+        elif isinstance(vace_reference_image, (list, tuple)):
+            refs = vace_reference_image
+        else:
+            refs = [vace_reference_image]
+        r = frames_to_u8(refs, dev)
+        nref = r.shape[0]
+        if r.shape[1:3] != (H, W):
+            raise ValueError(f"vace_reference_image must be {H}x{W}, got {tuple(r.shape[1:3])}")
+        # preprocess_video of the references = the reactive output of vs_vace_prepare with mask ones
+        # (v*1 + 0*0 is exact in bf16)
+        r_pre = torch.empty((1, 3, nref, H, W), dtype=BF16, device=dev)
+        r_tmp = torch.empty_like(r_pre)
+        r_m = torch.empty((nref, H, W), dtype=BF16, device=dev)
+        _lib.check(lib.vs_vace_prepare(r.data_ptr(), None, r_tmp.data_ptr(), r_pre.data_ptr(), r_m.data_ptr(),
+                                       nref, H, W, st))
+    out = torch.empty((1, 96, nref + t_lat, H // 8, W // 8), dtype=BF16, device=dev)
+    if nref:
+        rl = vae.encode([r_pre[0, :, j:j + 1] for j in range(nref)], dev, tiled=tiled, tile_size=tile_size,
+                        tile_stride=tile_stride)                                      # (f, 16, 1, h, w)
+        out[0, 0:16, :nref] = rl[:, :, 0].transpose(0, 1)
+        out[:, 16:, :nref] = 0
+    out[:, 0:16, nref:] = vae.encode(inactive, dev, tiled=tiled, tile_size=tile_size, tile_stride=tile_stride)
+    out[:, 16:32, nref:] = vae.encode(reactive, dev, tiled=tiled, tile_size=tile_size, tile_stride=tile_stride)
+    mlat = torch.empty((64, t_lat, H // 8, W // 8), dtype=BF16, device=dev)
+    _lib.check(lib.vs_vace_mask_latents(mask0.data_ptr(), mlat.data_ptr(), T, H, W, t_lat, st))
+    out[0, 32:, nref:] = mlat
     return out
