@@ -403,8 +403,12 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
 #pragma nounroll
     for (int h = 0; h < nh; ++h) {
         STAMP(0);
+#ifndef VS_GEMM_DIAG_NOREADS      // diagnostics only (wrong results): time without fragment reads
         load_frags(h);
+#endif
+#ifndef VS_GEMM_DIAG_NODMA        // diagnostics only (wrong results): time without in-loop LDS-DMA
         if (h + RING - 1 < nh) issue(h + RING - 1);
+#endif
         STAMP(1);
         bar();
         STAMP(2);
