@@ -261,6 +261,7 @@ __device__ unsigned long long g_gemm_stamps[2][5 * 32];
 #define STAMP(slot) do {} while (0)
 #endif
 
+template <bool BUF>
 __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
     const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
     bf16_t* C, long long ldc, int M, int N, int K, const bf16_t* __restrict__ A2, long long lda2,
@@ -305,15 +306,33 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
     const int dst_off = wm * (BT * 64) + wn * 4 * 1024;
     const int rbase = r0 + wn * 64 + prow;
     int issued = -1;                                // highest half-step this wave has issued
+    // BUF (every byte offset of the operands fits 31 bits; host-checked): buffer-addressed DMA with
+    // the 4 row offsets loop-invariant in VGPRs and the half-step's K offset in soffset.  Otherwise
+    // 64-bit flat addresses, recomputed per piece (2 v_mul_lo_u32 + v_mad_u64_u32 each: ~4x the
+    // issue cost of the DMA itself).
+    unsigned vo[4] = {0, 0, 0, 0};
+    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Pm), 0, 0x7fffffff,
+                                                                        0x00020000);
+    if constexpr (BUF) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) vo[j] = (unsigned)min(rbase + j * 16, lim) * (unsigned)(ldm * 2) + pch * 16;
+    }
     auto issue = [&](int h) {
         char* dst = smem + (h % RING) * SLOT + dst_off;
         const bool lora = h >= nh1;
-        const bf16_t* P = (lora ? Pl : Pm) + (lora ? h - nh1 : h) * HK + pch * 8;
-        const long long ld = lora ? ldl : ldm;
+        if (BUF && !lora) {
+            const unsigned ko = (unsigned)h * HK * 2;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            __builtin_amdgcn_global_load_lds((const GLB_AS void*)(P + (long long)min(rbase + j * 16, lim) * ld),
-                                             (LDS_AS void*)(dst + j * 1024), 16, 0, 0);
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (LDS_AS void*)(dst + j * 1024), 16, vo[j], ko, 0, 0);
+        } else {
+            const bf16_t* P = (lora ? Pl : Pm) + (lora ? h - nh1 : h) * HK + pch * 8;
+            const long long ld = lora ? ldl : ldm;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_global_load_lds((const GLB_AS void*)(P + (long long)min(rbase + j * 16, lim) * ld),
+                                                 (LDS_AS void*)(dst + j * 1024), 16, 0, 0);
+        }
         issued = h;
     };
 
@@ -622,6 +641,7 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_bf16_tn_w4(
 // ---------------------------------------------------------------------------------------------
 typedef int i32x8_t __attribute__((ext_vector_type(8)));
 
+template <bool BUF>
 __global__ __launch_bounds__(NTHR8, 2) void gemm_fp8_tn_256(
     const uint8_t* __restrict__ A, long long lda, const float* __restrict__ scale_a,
     const uint8_t* __restrict__ W, long long ldw, bf16_t* C, long long ldc, int M, int N, int K, Epi ep,
@@ -662,13 +682,28 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_fp8_tn_256(
     const int dst_off = wm * (BT * 64) + wn * 4 * 1024;
     const int rbase = r0 + wn * 64 + prow;
     int issued = -1;
+    // BUF: buffer-addressed DMA with loop-invariant 32-bit row offsets (see gemm_bf16_tn_256)
+    unsigned vo[4] = {0, 0, 0, 0};
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(P), 0, 0x7fffffff,
+                                                                        0x00020000);
+    if constexpr (BUF) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) vo[j] = (unsigned)min(rbase + j * 16, lim) * (unsigned)ld + pch * 16;
+    }
     auto issue = [&](int h) {
         char* dst = smem + (h % RING) * SLOT + dst_off;
-        const uint8_t* src = P + (long long)h * HB + pch * 16;
+        if constexpr (BUF) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            __builtin_amdgcn_global_load_lds((const GLB_AS void*)(src + (long long)min(rbase + j * 16, lim) * ld),
-                                             (LDS_AS void*)(dst + j * 1024), 16, 0, 0);
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, (LDS_AS void*)(dst + j * 1024), 16, vo[j],
+                                                         (unsigned)h * HB, 0, 0);
+        } else {
+            const uint8_t* src = P + (long long)h * HB + pch * 16;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_global_load_lds((const GLB_AS void*)(src + (long long)min(rbase + j * 16, lim) * ld),
+                                                 (LDS_AS void*)(dst + j * 1024), 16, 0, 0);
+        }
         issued = h;
     };
 
@@ -842,7 +877,9 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
         const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
         static int impl = -1;
         if (impl < 0) {
-            (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_256,
+            (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_256<true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, RING * SLOT);
+            (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_256<false>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, RING * SLOT);
             (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_w4,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, RING * SLOT);
@@ -861,10 +898,21 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
             VS_CHECK_LAUNCH();
             return VS_OK;
         }
-        hipLaunchKernelGGL(gemm_bf16_tn_256, dim3((unsigned)(tm * tn)), dim3(NTHR8), RING * SLOT,
-                           (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw,
-                           (bf16_t*)c, ldc, m, n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2,
-                           k2, ep, tm, tn);
+        static int buf_ok = -1;
+        if (buf_ok < 0) {
+            const char* e = getenv("VS_GEMM_FLAT_DMA");   // 1: flat-address DMA (A/B)
+            buf_ok = !(e && e[0] == '1');
+        }
+        if (buf_ok && fits32)
+            hipLaunchKernelGGL(gemm_bf16_tn_256<true>, dim3((unsigned)(tm * tn)), dim3(NTHR8), RING * SLOT,
+                               (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw,
+                               (bf16_t*)c, ldc, m, n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2,
+                               k2, ep, tm, tn);
+        else
+            hipLaunchKernelGGL(gemm_bf16_tn_256<false>, dim3((unsigned)(tm * tn)), dim3(NTHR8), RING * SLOT,
+                               (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw,
+                               (bf16_t*)c, ldc, m, n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2,
+                               k2, ep, tm, tn);
         VS_CHECK_LAUNCH();
         return VS_OK;
     }
@@ -898,13 +946,21 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
     const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)gemm_fp8_tn_256, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)gemm_fp8_tn_256<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  RING * SLOT);
+        (void)hipFuncSetAttribute((const void*)gemm_fp8_tn_256<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   RING * SLOT);
         attr = true;
     }
-    hipLaunchKernelGGL(gemm_fp8_tn_256, dim3((unsigned)(tm * tn)), dim3(NTHR8), RING * SLOT, (hipStream_t)stream,
-                       (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c, ldc, m, n, k, ep, tm,
-                       tn);
+    const bool fits32 = (long long)(m - 1) * lda + k < 0x7fffffffLL && (long long)(n - 1) * ldw + k < 0x7fffffffLL;
+    if (fits32)
+        hipLaunchKernelGGL(gemm_fp8_tn_256<true>, dim3((unsigned)(tm * tn)), dim3(NTHR8), RING * SLOT,
+                           (hipStream_t)stream, (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c,
+                           ldc, m, n, k, ep, tm, tn);
+    else
+        hipLaunchKernelGGL(gemm_fp8_tn_256<false>, dim3((unsigned)(tm * tn)), dim3(NTHR8), RING * SLOT,
+                           (hipStream_t)stream, (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c,
+                           ldc, m, n, k, ep, tm, tn);
     VS_CHECK_LAUNCH();
     return VS_OK;
 }
