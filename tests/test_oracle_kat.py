@@ -90,3 +90,21 @@ def test_t5_relative_position_buckets():
     assert b.min() == 0 and b.max() == 31
     assert b[0, 0] == 0 and b[0, 1] == 17 and b[1, 0] == 1 and b[0, 7] == 23 and b[7, 0] == 7
     assert b[0, 511] == 31 and b[511, 0] == 15
+
+
+def test_loader_normalizes_comfyui_kijai_layouts():
+    """loader.normalize_keys: 'model.diffusion_model.' / 'diffusion_model.' prefixes stripped, fp8
+    weights with '.scale_weight' folded (exact upcast, then the scale), so the reference's md5
+    key-layout hash of the stripped file equals the plain layout's."""
+    import torch
+    from vstyler.loader import hash_state_dict_keys, normalize_keys
+    w8 = torch.tensor([[1.5, -2.0], [0.25, 448.0]]).to(torch.float8_e4m3fn)
+    plain = {"blocks.0.self_attn.q.weight": torch.zeros(2, 2), "head.head.bias": torch.zeros(2)}
+    comfy = {"model.diffusion_model.blocks.0.self_attn.q.weight": w8,
+             "model.diffusion_model.blocks.0.self_attn.q.scale_weight": torch.tensor(0.5),
+             "model.diffusion_model.head.head.bias": torch.zeros(2), "scaled_fp8": torch.zeros(1)}
+    n = normalize_keys(comfy)
+    assert set(n) == set(plain)
+    assert hash_state_dict_keys(n) == hash_state_dict_keys(plain)
+    assert torch.equal(n["blocks.0.self_attn.q.weight"].float(), w8.float() * 0.5)
+    assert set(normalize_keys({"diffusion_model.x.weight": torch.zeros(1)})) == {"x.weight"}

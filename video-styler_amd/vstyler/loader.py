@@ -59,6 +59,31 @@ def load_state_dict(path, device="cpu", torch_dtype=None):
     return sd
 
 
+_PREFIXES = ("model.diffusion_model.", "diffusion_model.")
+
+
+def normalize_keys(state_dict):
+    """ComfyUI / Kijai WanVideo checkpoints (the config-5 workflow's model files) carry the Wan key
+    layout under a 'model.diffusion_model.' or 'diffusion_model.' prefix, fp8 e4m3fn linear weights
+    and, in their '_scaled' variants, per-tensor '<name>.scale_weight' factors.  Strip the prefix and
+    fold scale_weight into its weight (exact fp8 -> bf16 upcast, then the scale) so the reference's
+    md5 key-layout detection applies unchanged.  Other layouts pass through."""
+    sd = {}
+    for k, v in state_dict.items():
+        for pre in _PREFIXES:
+            if k.startswith(pre):
+                k = k[len(pre):]
+                break
+        sd[k] = v
+    for k in [k for k in sd if k.endswith(".scale_weight")]:
+        base = k[: -len(".scale_weight")] + ".weight"
+        s = sd.pop(k)
+        if base in sd:
+            sd[base] = (sd[base].to(torch.float32) * s.to(torch.float32)).to(torch.bfloat16)
+    sd.pop("scaled_fp8", None)
+    return sd
+
+
 def build_dit(state_dict, device):
     sd = {k: v for k, v in state_dict.items() if not k.startswith("vace")}
     h = hash_state_dict_keys(sd)
@@ -111,7 +136,7 @@ def load_models(paths, device="cuda"):
     """Returns {'wan_video_dit': WanModel, 'wan_video_vace': VaceWanModel, ...} for the files given."""
     out = {}
     for path in paths:
-        sd = load_state_dict(path, device="cpu")
+        sd = normalize_keys(load_state_dict(path, device="cpu"))
         vae = build_vae(sd, device)
         if vae is not None:
             out["wan_video_vae"] = vae
@@ -119,6 +144,10 @@ def load_models(paths, device="cuda"):
         te = build_text_encoder(sd, device)
         if te is not None:
             out["wan_video_text_encoder"] = te
+            continue
+        if sd and all(k.startswith("vace") for k in sd):
+            # a VACE-module-only file (the ComfyUI workflow's WanVideoVACEModelSelect input)
+            out["wan_video_vace"] = build_vace(sd, device)
             continue
         dit = build_dit(sd, device)
         if dit is not None:
