@@ -224,9 +224,19 @@ class WanVideoPipeline:
         if pipe.text_encoder is not None:
             from .t5 import WanPrompter
             tok = None
-            if tokenizer_config is not None:
+            if tokenizer_config is None:
+                # the reference's default (wan_video_new.py:346): ./models/Wan-AI/Wan2.1-T2V-1.3B/google/*
+                tokenizer_config = ModelConfig(model_id="Wan-AI/Wan2.1-T2V-1.3B", origin_file_pattern="google/*")
+                try:
+                    tokenizer_config.download_if_necessary()
+                    tok = tokenizer_config.path
+                except FileNotFoundError:
+                    tok = None   # no local tokenizer: prompts need encode_ids / prompt_emb=
+            else:
                 tokenizer_config.download_if_necessary()
                 tok = tokenizer_config.path
+            if isinstance(tok, list):
+                tok = os.path.dirname(tok[0])
             pipe.prompter = WanPrompter(tokenizer_path=tok)
             pipe.prompter.fetch_models(pipe.text_encoder)
         if use_usp:
