@@ -131,6 +131,27 @@ def test_attention_rescale_many(K):
     assert mx < 3e-2 and rl < 1e-2, (mx, rl)
 
 
+def test_attention_kv_slab_beyond_4gb(K):
+    """K/V rows of stride 32768 so one (batch, head) slab spans 4.6 GB: the buffer descriptors are
+    rebased per 64-key tile (the 1280x720x121 config's fused q|k|v rows span 3.4 GB).  Checked
+    against a torch fp32 softmax(QK^T/sqrt(d))V on the GPU (test-side reference)."""
+    Sq, Skv, ld = 256, 70000, 32768
+    g = torch.Generator(device="cuda").manual_seed(60)
+    q = torch.randn(Sq, 128, device="cuda", generator=g).to(BF16)
+    k = torch.empty(Skv, ld, device="cuda", dtype=BF16)
+    v = torch.empty(Skv, ld, device="cuda", dtype=BF16)
+    k[:, :128] = torch.randn(Skv, 128, device="cuda", generator=g).to(BF16)
+    v[:, :128] = torch.randn(Skv, 128, device="cuda", generator=g).to(BF16)
+    k[:, 128:256] = 1e4          # neighbouring columns must never be read
+    out = torch.empty(Sq, 128, dtype=BF16, device="cuda")
+    K.attention(q, k[:, :128], v[:, :128], out, 1, 1)
+    s = (q.float() @ k[:, :128].float().t()) * 128 ** -0.5
+    ref = torch.softmax(s, -1) @ v[:, :128].float()
+    del k, v
+    mx = (out.float() - ref).abs().max().item()
+    assert mx < 3e-2, mx
+
+
 def test_attention_strided_views(K):
     # q/k/v as column slices of a fused [M, 3D] buffer (row stride 3D)
     B, S, H = 1, 200, 2

@@ -5,22 +5,18 @@
 // 512 T5 context tokens.
 //
 // Structure (one workgroup = 8 waves = 256 query rows of one (batch, head)):
-//  * each wave owns 32 query rows; its Q slice (32 x 128 bf16) lives in 32 VGPRs for the whole
-//    key sweep, in the B-operand layout of v_mfma_f32_32x32x16_bf16;
-//  * K/V tiles of 64 keys (2 x 16 KB) are register-staged global->LDS, double-buffered: the
-//    global loads of tile i+1 are issued before the MFMAs of tile i and written to LDS after
-//    them (issue-early / write-late), one barrier per tile;
-//  * S^T = K Q^T (swapped product): every lane holds 32 scores of ONE query row, so the online
-//    softmax row max needs a single lane^32 exchange and the row sum stays lane-partial;
-//  * O^T = V^T P: the S^T accumulator is directly the B operand of the PV MFMA (no LDS round
-//    trip for P), V^T fragments come from LDS with ds_read_b64_tr_b16 (hardware transpose), and
-//    the O accumulator of a lane also belongs to its own query row, so the rescale is lane-local;
-//  * K/V LDS image: 256-B rows with the 16-B chunk XOR swizzle that keeps both the ds_read_b128
-//    row reads (K) and the transposed reads (V) bank-conflict free;
+//  * each wave owns 32 query rows; its Q slice (32 x 128 bf16, pre-scaled by log2(e)/sqrt(d))
+//    lives in 32 VGPRs for the whole key sweep, in the B-operand layout of v_mfma_f32_32x32x16_bf16;
+//  * K/V tiles of 64 keys are register-staged global->LDS through 2-slot rings (buffer loads
+//    issued two phases before their LDS writes), rows padded to 272 / 320 B so the K row reads
+//    (ds_read_b128) and the V transposed reads (ds_read_b64_tr_b16) are bank-conflict free;
+//  * S^T = K Q^T (swapped product): every lane holds 32 scores of ONE query row;
+//    O^T = V^T P with P packed to bf16 in registers as the B operand; the O accumulator of a
+//    lane belongs to its own query row, so every rescale is lane-local;
+//  * two phases per tile with the two wave halves one barrier apart (kernel comment below);
 //  * workgroup ids are remapped so each XCD works through contiguous (batch, head) ranges: the
 //    K/V of one head is streamed by the 32 CUs of one XCD together and served from its L2.
 #include "common.h"
-#include <stdlib.h>
 
 namespace {
 
@@ -33,7 +29,6 @@ constexpr int VROW = 320;        // LDS row pitch of the V tile (256 B + 64): tr
 constexpr int KT = BKV * KROW;   // 17408
 constexpr int VT = BKV * VROW;   // 20480
 constexpr int LDS_BYTES = 2 * (KT + VT);   // K ring 2 x 17408 + V ring 2 x 20480
-constexpr float RESCALE_THR = 8.0f;   // lazy rescale (exp2 domain): skip while the max grows <= 2^8
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
@@ -42,6 +37,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Two phases per 64-key tile, the two wave halves one barrier apart, one S tile live:
+//   B_{i-1}: [load V(i)]   S = K(i) Q^T (16 MFMA)                     ; store K(i+1) -> slot (i+1)&1
+//   A_i:     [load K(i+2)] O^T += V(i-1)^T P(i-1) (16 MFMA) || softmax(S) -> P(i) ; store V(i) -> slot i&1
+// and the softmax is a max-free fast path: p = exp2(c*s - m) against the current reference max m,
+// packed to bf16 at once, and a lane's tile partial sum rs checked once per tile.  Every p <= rs,
+// so rs <= SUM_THR (= 2^8) guarantees P <= 2^8 -- the bound of v1's lazy rescale (CDNA guide T13).
+// When any lane of the wave exceeds it (always on the first tile; later only when a row's max has
+// grown), the exact path runs after the tile's PV(i-1) MFMAs: row max, m' = max(m, max), O (which
+// already holds P(i-1)V(i-1) at the old scale) and l scaled by exp2(m - m'), P(i) recomputed.
+// Ring hazards (group 0 runs B_{i-1} at phase 2i and A_i at 2i+1, group 1 one phase later):
+// K(i+1) is written at 2i / 2i+1 into the slot K(i-1) was read from at 2i-2 / 2i-1 and first read
+// at 2i+2; V(i) is written at 2i+1 / 2i+2 into the slot V(i-2) was read from at 2i-1 / 2i and first
+// read at 2i+3.  Per-tile VALU ~460 issue cycles (the previous structure, with a max pass, a
+// shuffle and a two-deep S ring: ~850).  Epilogue: permlane32_swap pairs -> 16-B stores (T21).
+constexpr float SUM_THR = 256.0f;
+
+template <bool REBASE>
 __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     bf16_t* __restrict__ O, int Sq, int Skv, int H, long long ldq, long long ldk, long long ldv,
@@ -61,283 +74,44 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     const bf16_t* Kb = K + (long long)b * bsk + h * HD;
     const bf16_t* Vb = V + (long long)b * bsv + h * HD;
 
-    // Q slice as the B operand of S^T = K Q^T: lane (r, hh) holds Q[q0+r][16s + 8hh .. +7].
-    bf16x8_t qf[8];
-    {
-        const int qrow = min(q0 + r, Sq - 1);
-        const bf16_t* qp = Qb + (long long)qrow * ldq + 8 * hh;
-#pragma unroll
-        for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8_t*>(qp + 16 * s);
-    }
-
-    f32x16_t o[4];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
-    float m = -1e30f, l = 0.f;
-
-    // buffer descriptors over this (batch, head)'s K/V rows; per-lane byte offset constant, the
-    // tile's row offset goes to the scalar soffset
-    const unsigned kbytes = (unsigned)min((long long)(Skv - 1) * ldk * 2 + HD * 2, 0xffffffffLL);
-    const unsigned vbytes = (unsigned)min((long long)(Skv - 1) * ldv * 2 + HD * 2, 0xffffffffLL);
-    const __amdgpu_buffer_rsrc_t krs = make_rsrc(Kb, kbytes), vrs = make_rsrc(Vb, vbytes);
-    const int srow = tid >> 4, sch = tid & 15;            // chunk tid -> row srow (and srow+32)
-    const unsigned kvo0 = (unsigned)(srow * ldk * 2 + sch * 16), kvo1 = kvo0 + (unsigned)(32 * ldk * 2);
-    const unsigned vvo0 = (unsigned)(srow * ldv * 2 + sch * 16), vvo1 = vvo0 + (unsigned)(32 * ldv * 2);
-    const int kw = srow * KROW + sch * 16, vw = srow * VROW + sch * 16;
-
-    // K ring (2 slots) runs one tile ahead of the V ring (2 slots): iteration i reads K(i+1)
-    // (for the next S^T) and V(i) (for this tile's PV), and stages K(i+2), V(i+1).
-    i32x4_t kst[2], vst[2];
-    auto load_k = [&](int kv0) {
-        const int ks = kv0 * (int)ldk * 2;
-        kst[0] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo0, ks, 0);
-        kst[1] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo1, ks, 0);
-    };
-    auto load_v = [&](int kv0) {
-        const int vs = kv0 * (int)ldv * 2;
-        vst[0] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo0, vs, 0);
-        vst[1] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo1, vs, 0);
-    };
-    auto store_k = [&](int slot) {
-        char* base = smem + slot * KT;
-        *reinterpret_cast<i32x4_t*>(base + kw) = kst[0];
-        *reinterpret_cast<i32x4_t*>(base + kw + 32 * KROW) = kst[1];
-    };
-    auto store_v = [&](int slot) {
-        char* base = smem + 2 * KT + slot * VT;
-        *reinterpret_cast<i32x4_t*>(base + vw) = vst[0];
-        *reinterpret_cast<i32x4_t*>(base + vw + 32 * VROW) = vst[1];
-    };
-
-    // per-lane LDS read bases (everything else is an immediate offset)
-    const int krd = r * KROW + 16 * hh;                   // + t*32*KROW + 32*ss
-    const int g4 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
-    const int vrd = (4 * (g4 >> 1) + q4) * VROW + 32 * (g4 & 1) + 8 * p4;   // + ks*16*VROW + 64*dt (+8 rows)
-
-    // S^T for keys 0-31 (t=0) and 32-63 (t=1) as two interleaved accumulation chains; K fragments
-    // are read two d-steps ahead of their MFMAs so LDS latency hides under the chain.
-    auto qk = [&](int slot, f32x16_t* s) {
-        const char* base = smem + slot * KT + krd;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            s[0][i] = 0.f;
-            s[1][i] = 0.f;
-        }
-        bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(base);
-        bf16x8_t kb = *reinterpret_cast<const bf16x8_t*>(base + 32 * KROW);
-#pragma unroll
-        for (int ss = 0; ss < 8; ++ss) {
-            bf16x8_t na, nb;
-            if (ss + 1 < 8) {
-                na = *reinterpret_cast<const bf16x8_t*>(base + 32 * (ss + 1));
-                nb = *reinterpret_cast<const bf16x8_t*>(base + 32 * KROW + 32 * (ss + 1));
-            }
-            // keep the next fragments' LDS reads issued ahead of this step's MFMAs
-            __builtin_amdgcn_sched_barrier(0);
-            s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ss], s[0], 0, 0, 0);
-            s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[ss], s[1], 0, 0, 0);
-            if (ss + 1 < 8) {
-                ka = na;
-                kb = nb;
-            }
-        }
-    };
-    // online softmax in the exp2 domain (c = scale*log2 e) with a lazy rescale: the reference max
-    // m only moves when some row's max exceeds it by more than RESCALE_THR, so P <= 2^THR.
-    // Runs after the previous tile's PV has been issued and before this tile's PV (T13 order).
-    auto softmax = [&](f32x16_t* s, int kv0, bool mask) {
-        if (mask) {
-            asm volatile("");     // keep this a real (uniform) branch: never if-convert into every tile
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int key = kv0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
-                    if (key >= Skv) s[t][i] = -INFINITY;
-                }
-        }
-        float mx = s[0][0];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[t][i]);
-        mx = fmaxf(mx, __shfl_xor(mx, 32)) * c;
-        if (__any(mx > m + RESCALE_THR)) {
-            const float mnew = fmaxf(m, mx);
-            const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-            m = mnew;
-            l *= alpha;
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
-        }
-        float rs = 0.f;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const float p = __builtin_amdgcn_exp2f(fmaf(s[t][i], c, -m));
-                s[t][i] = p;
-                rs += p;
-            }
-        l += rs;
-    };
-    // O^T += V^T P over 4 k-steps of 16 keys
-    auto pv = [&](int slot, const f32x16_t* s) {
-        const char* base = smem + 2 * KT + slot * VT;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            const int t = ks >> 1, u = ks & 1;
-            bf16x8_t pf;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) pf[j] = (__bf16)s[t][8 * u + j];
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt) {
-                const char* a0 = base + vrd + ks * 16 * VROW + 64 * dt;
-                const i16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_t*)(a0));
-                const i16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_t*)(a0 + 8 * VROW));
-                const bf16x8_t vf = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, v0),
-                                                            __builtin_bit_cast(bf16x4_t, v1), 0, 1, 2, 3,
-                                                            4, 5, 6, 7);
-                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
-            }
-        }
-    };
-
-    const int nkv = (Skv + BKV - 1) / BKV;
-    // prologue: K(0), K(1), V(0) in LDS; S(0) computed by every wave; K(2) in flight to registers
-    load_k(0);
-    load_v(0);
-    store_k(0);
-    store_v(0);
-    if (nkv > 1) {
-        load_k(BKV);
-        store_k(1);
-    }
-    __syncthreads();
-    f32x16_t sa[2], sb[2];
-    qk(0, sa);
-    if (nkv > 2) load_k(2 * BKV);
-    __syncthreads();      // every wave has read K slot 0 before it is restaged with K(2)
-
-    // Staggered two-phase loop.  Per tile i every wave runs
-    //   A_i: [load V(i+1)] QK(i+1) (MFMA) + softmax(i) (VALU) ; store K(i+2) -> K slot i&1
-    //   B_i: [load K(i+3)] PV(i) (MFMA)                      ; store V(i+1) -> V slot (i+1)&1
-    // with a barrier after each phase.  Waves 4-7 pass one extra barrier first, so on every SIMD
-    // one wave's softmax overlaps its partner's MFMAs.  Ring hazards (phase index of group 0 /
-    // group 1 = 2i / 2i+1 for A_i, 2i+1 / 2i+2 for B_i): K(i+2) is written in phases 2i..2i+1
-    // after its slot's last read (qk(i), phases 2i-2..2i-1) and before its first read (qk(i+2),
-    // phases 2i+2..2i+3); V(i+1) is written in 2i+1..2i+2, after pv(i-1) (2i-1..2i) and before
-    // pv(i+1) (2i+3..2i+4).
-    auto phase_bar = [&]() {
-        __builtin_amdgcn_sched_barrier(0);
-        __syncthreads();
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    const int grp = wave >> 2;
-    // static priority for the younger half (waves 4-7): it loses VALU arbitration to the older
-    // half on every segment otherwise (CDNA guide T5 static form; readfirstlane keeps it scalar)
-#ifdef VS_ATTN_YOUNG_PRIO  // measured -1.2 % on MI355X (1067 vs 1080 TF/s): off
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
-    if (grp == 1) phase_bar();
-    auto body = [&](int it, f32x16_t* cur, f32x16_t* nxt) {
-        const bool has1 = it + 1 < nkv, has2 = it + 2 < nkv, has3 = it + 3 < nkv;
-        // ---- phase A
-        if (has1) load_v((it + 1) * BKV);
-        if (has1) qk((it + 1) & 1, nxt);
-        softmax(cur, it * BKV, (it + 1) * BKV > Skv);
-        if (has2) store_k(it & 1);
-        phase_bar();
-        // ---- phase B
-        if (has3) load_k((it + 3) * BKV);
-        pv(it & 1, cur);
-        if (has1) store_v((it + 1) & 1);
-        phase_bar();
-    };
-    int it = 0;
-    for (; it + 1 < nkv; it += 2) {
-        body(it, sa, sb);
-        body(it + 1, sb, sa);
-    }
-    if (it < nkv) body(it, sa, sb);
-    if (grp == 0) phase_bar();
-
-    const float lt = l + __shfl_xor(l, 32);
-    const float inv = 1.f / lt;
-    if (q0 + r < Sq) {
-        bf16_t* op = O + (long long)b * bso + (long long)(q0 + r) * ldo + h * HD;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-            for (int gi = 0; gi < 4; ++gi) {
-                const int d = 32 * dt + 8 * gi + 4 * hh;
-                u32x2_t w;
-                w[0] = pack2(o[dt][4 * gi] * inv, o[dt][4 * gi + 1] * inv);
-                w[1] = pack2(o[dt][4 * gi + 2] * inv, o[dt][4 * gi + 3] * inv);
-                *reinterpret_cast<u32x2_t*>(op + d) = w;
-            }
-    }
-}
-
-
-// ---------------------------------------------------------------------------------------------
-// v2: same tiles, rings and two-group stagger as v1, re-phased so one S tile is live:
-//   B_{i-1}: [load V(i)]   S = K(i) Q^T (16 MFMA)                     ; store K(i+1) -> slot (i+1)&1
-//   A_i:     [load K(i+2)] O^T += V(i-1)^T P(i-1) (16 MFMA) || softmax(S) -> P(i) ; store V(i) -> slot i&1
-// and the softmax is a max-free fast path: p = exp2(c*s - m) against the current reference max m,
-// packed to bf16 at once, and a lane's tile partial sum rs checked once per tile.  Every p <= rs,
-// so rs <= SUM_THR (= 2^8) guarantees P <= 2^8 -- the bound of v1's lazy rescale (CDNA guide T13).
-// When any lane of the wave exceeds it (always on the first tile; later only when a row's max has
-// grown), the exact path runs after the tile's PV(i-1) MFMAs: row max, m' = max(m, max), O (which
-// already holds P(i-1)V(i-1) at the old scale) and l scaled by exp2(m - m'), P(i) recomputed.
-// Ring hazards (group 0 runs B_{i-1} at phase 2i and A_i at 2i+1, group 1 one phase later):
-// K(i+1) is written at 2i / 2i+1 into the slot K(i-1) was read from at 2i-2 / 2i-1 and first read
-// at 2i+2; V(i) is written at 2i+1 / 2i+2 into the slot V(i-2) was read from at 2i-1 / 2i and first
-// read at 2i+3.  Per-tile VALU ~580 issue cycles (v1 ~850: max tree + shuffle + a 32-register copy
-// of its two-deep S ring).  Epilogue: permlane32_swap pairs -> 16-B stores (CDNA guide T21).
-constexpr float SUM_THR = 256.0f;
-
-__global__ __launch_bounds__(NTHR) void attn_fwd_d128_v2(
-    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-    bf16_t* __restrict__ O, int Sq, int Skv, int H, long long ldq, long long ldk, long long ldv,
-    long long ldo, long long bsq, long long bsk, long long bsv, long long bso, float c, int nqb) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-
-    const int g = xcd_remap(blockIdx.x, gridDim.x);
-    const int qb = g % nqb;
-    const int bh = g / nqb;
-    const int h = bh % H, b = bh / H;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int r = lane & 31, hh = lane >> 5;
-    const int q0 = qb * BQ + wave * 32;
-
-    const bf16_t* Qb = Q + (long long)b * bsq + h * HD;
-    const bf16_t* Kb = K + (long long)b * bsk + h * HD;
-    const bf16_t* Vb = V + (long long)b * bsv + h * HD;
-
-    const unsigned kbytes = (unsigned)min((long long)(Skv - 1) * ldk * 2 + HD * 2, 0xffffffffLL);
-    const unsigned vbytes = (unsigned)min((long long)(Skv - 1) * ldv * 2 + HD * 2, 0xffffffffLL);
-    const __amdgpu_buffer_rsrc_t krs = make_rsrc(Kb, kbytes), vrs = make_rsrc(Vb, vbytes);
+    // buffer descriptors over this (batch, head)'s K/V rows: per-lane byte offset constant, the
+    // tile's row offset in soffset.  REBASE (a slab beyond 2^31 bytes, e.g. 1280x720x121 with the
+    // fused q|k|v row layout: 111600 rows x 30 KB): the descriptor is rebuilt per tile on a 64-bit
+    // base (1.6 % slower, so only when needed).  Rows past Skv read as 0 (masked anyway).
     const int srow = tid >> 4, sch = tid & 15;
     const unsigned kvo0 = (unsigned)(srow * ldk * 2 + sch * 16), kvo1 = kvo0 + (unsigned)(32 * ldk * 2);
     const unsigned vvo0 = (unsigned)(srow * ldv * 2 + sch * 16), vvo1 = vvo0 + (unsigned)(32 * ldv * 2);
     const int kw = srow * KROW + sch * 16, vw = srow * VROW + sch * 16;
 
     i32x4_t kst[2], vst[2];
+    const int ldk32 = (int)ldk, ldv32 = (int)ldv;   // host: 64 * ld * 2 < 2^31
+    const __amdgpu_buffer_rsrc_t krs = make_rsrc(Kb, REBASE ? 0u : (unsigned)((Skv - 1) * ldk32 * 2 + HD * 2));
+    const __amdgpu_buffer_rsrc_t vrs = make_rsrc(Vb, REBASE ? 0u : (unsigned)((Skv - 1) * ldv32 * 2 + HD * 2));
+    auto tile_rsrc = [&](const bf16_t* base, int ld, int kv0) {
+        const int rows = min(BKV, Skv - kv0);
+        return make_rsrc(base + (long long)kv0 * ld, (unsigned)((rows - 1) * ld * 2 + HD * 2));
+    };
     auto load_k = [&](int kv0) {
-        const int ks = kv0 * (int)ldk * 2;
-        kst[0] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo0, ks, 0);
-        kst[1] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo1, ks, 0);
+        if constexpr (REBASE) {
+            const __amdgpu_buffer_rsrc_t rs = tile_rsrc(Kb, ldk32, kv0);
+            kst[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, kvo0, 0, 0);
+            kst[1] = __builtin_amdgcn_raw_buffer_load_b128(rs, kvo1, 0, 0);
+        } else {
+            const int ks = kv0 * ldk32 * 2;
+            kst[0] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo0, ks, 0);
+            kst[1] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo1, ks, 0);
+        }
     };
     auto load_v = [&](int kv0) {
-        const int vs = kv0 * (int)ldv * 2;
-        vst[0] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo0, vs, 0);
-        vst[1] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo1, vs, 0);
+        if constexpr (REBASE) {
+            const __amdgpu_buffer_rsrc_t rs = tile_rsrc(Vb, ldv32, kv0);
+            vst[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, vvo0, 0, 0);
+            vst[1] = __builtin_amdgcn_raw_buffer_load_b128(rs, vvo1, 0, 0);
+        } else {
+            const int vs = kv0 * ldv32 * 2;
+            vst[0] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo0, vs, 0);
+            vst[1] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo1, vs, 0);
+        }
     };
     auto store_k = [&](int slot) {
         char* base = smem + slot * KT;
@@ -593,24 +367,23 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
         return VS_E_INVALID;
     if ((ldq | ldk | ldv | ldo | bsq | bsk | bsv | bso) & 7) return VS_E_INVALID;
     if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o)) return VS_E_INVALID;
-    // buffer addressing: one (batch, head) K/V slab and a tile's row offset must fit 32 bits
-    if ((long long)skv * ldk * 2 >= (1LL << 31) || (long long)skv * ldv * 2 >= (1LL << 31)) return VS_E_UNSUPPORTED;
+    // buffer addressing: a 64-row tile's span must fit the 32-bit per-lane offset
+    if ((long long)BKV * ldk * 2 >= (1LL << 31) || (long long)BKV * ldv * 2 >= (1LL << 31)) return VS_E_UNSUPPORTED;
     const int nqb = (sq + BQ - 1) / BQ;
     const long long nwg = (long long)nqb * heads * batch;
     if (nwg > 0x7fffffff) return VS_E_INVALID;
-    // VS_ATTN_IMPL=1 selects the v1 kernel (A/B measurements); default v2
-    static int impl = -1;
-    if (impl < 0) {
-        const char* e = getenv("VS_ATTN_IMPL");
-        impl = (e && e[0] == '1') ? 1 : 2;
-        (void)hipFuncSetAttribute((const void*)attn_fwd_d128, hipFuncAttributeMaxDynamicSharedMemorySize,
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)attn_fwd_d128<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)attn_fwd_d128_v2, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)attn_fwd_d128<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   LDS_BYTES);
+        attr_set = true;
     }
     const float c = scale * 1.4426950408889634f;
-    hipLaunchKernelGGL(impl == 1 ? attn_fwd_d128 : attn_fwd_d128_v2, dim3((unsigned)nwg), dim3(NTHR), LDS_BYTES,
-                       (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+    const bool rebase = (long long)skv * ldk * 2 >= (1LL << 31) || (long long)skv * ldv * 2 >= (1LL << 31);
+    hipLaunchKernelGGL(rebase ? attn_fwd_d128<true> : attn_fwd_d128<false>, dim3((unsigned)nwg), dim3(NTHR),
+                       LDS_BYTES, (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                        (bf16_t*)o, sq, skv, heads, ldq, ldk, ldv, ldo, bsq, bsk, bsv, bso, c, nqb);
     VS_CHECK_LAUNCH();
     return VS_OK;
