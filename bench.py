@@ -169,6 +169,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=1024)
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
+    ap.add_argument("--progress", action="store_true", help="sync + stderr line after every timed step")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end sec/video components")
     ap.add_argument("--config", default="bf16", choices=("bf16", "fp8"),
                     help="bf16: BASELINE config (50-step Euler, CFG 5); fp8: config 5 (fp8 block linears, "
@@ -258,6 +259,8 @@ def main():
         stepper = DenoiseStepper(step_fn, ts, ds, use_graph=use_graph)
         for i in range(args.warmup):
             stepper(i)
+            torch.cuda.synchronize()
+            print(f"[bench] warmup step {i} done", file=sys.stderr, flush=True)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -267,6 +270,9 @@ def main():
         t0 = time.perf_counter()
         for i in range(args.warmup, n_total):
             stepper(i)
+            if args.progress:
+                torch.cuda.synchronize()
+                print(f"[bench] step {i} done", file=sys.stderr, flush=True)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -284,6 +290,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
 
+    default_shape = (args.model, args.width, args.height, args.frames) == ("14B", 832, 480, 73)
     ms_per_step = 1000 * elapsed / args.steps
     value = args.steps / elapsed
     fl_step = step_flops(m, S)
@@ -291,8 +298,7 @@ def main():
     attn_flops = 4.0 * S * S * m["dim"] * 2 / world
     achieved = attn_flops / (attn_ms / 1000) / 1e12
     out = {
-        "metric": ("denoising steps/sec, Wan2.1-VACE-14B 832x480x73" if args.model == "14B" else
-                   f"denoising steps/sec, Wan2.1-VACE-{args.model} {args.width}x{args.height}x{args.frames}")
+        "metric": f"denoising steps/sec, Wan2.1-VACE-{args.model} {args.width}x{args.height}x{args.frames}"
                   + (" [config 5: fp8 e4m3 block linears, UniPC, CFG 1.2, SLG]" if args.config == "fp8" else ""),
         "value": round(value, 5), "unit": "steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
@@ -313,7 +319,8 @@ def main():
         "roofline": {"kernel": "attn_fwd_d128 (self-attention)", "bound": "mfma",
                      "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                     "traffic": pmc_traffic() if world == 1 else None,
+                     # the committed PMC measurement is of the default workload (14B 832x480x73)
+                     "traffic": pmc_traffic() if world == 1 and default_shape else None,
                      "traffic_source": "rocprofv3 --pmc FETCH_SIZE*2+WRITE_SIZE per launch, profiles/r1/pmc_attn_v2 "
                                        "(same kernel, same shape; algorithmic Q+K+V+O = 2.43e9 B)",
                      "avg_launch_ms": round(attn_ms, 3), "launches": attn_n,
