@@ -54,6 +54,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
 // shuffle and a two-deep S ring: ~850).  Epilogue: permlane32_swap pairs -> 16-B stores (T21).
 constexpr float SUM_THR = 256.0f;
 
+#ifdef VS_ATTN_STAMPS
+// debug build: s_memtime at the 4 phase boundaries of tiles 2..33 for wave 0 (group 0) and wave 4
+// (group 1) of workgroup 0, kept in an LDS tail during the loop (no loop-carried registers) and
+// copied out after it.  The stamp's lgkmcnt wait sits next to a barrier that drains LDS anyway.
+__device__ unsigned long long g_attn_stamps[2][4 * 32];
+constexpr int STAMP_LDS = 8 * 4 * 32 * 8;
+#define ATTN_STAMP(slot)                                                                          \
+    do {                                                                                          \
+        unsigned long long t_;                                                                    \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_));                          \
+        *reinterpret_cast<volatile unsigned long long*>(                                          \
+            smem + LDS_BYTES + 8 * (wave * 128 + 8 * (stamp_it & 15) + (slot))) = t_;             \
+    } while (0)
+#else
+#define ATTN_STAMP(slot) do {} while (0)
+#endif
+
 template <bool REBASE>
 __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
@@ -177,24 +194,31 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
         pk[ks][j + 1] = __builtin_bit_cast(unsigned, w1);
         // pin the chunk here: without it LLVM sinks the whole softmax below the PV MFMAs
     };
+    // S^T = K Q^T over 8 d-steps, two chains (keys 0-31 / 32-63).  K fragments are read
+    // VS_ATTN_KDEPTH d-steps ahead (default 3): with one step of look-ahead the QK burst stalls on
+    // LDS latency and holds the SIMD's matrix pipe for ~2x its 16 MFMAs while the partner wave's
+    // PV+softmax phase starves (measured with -DVS_ATTN_STAMPS).
+#ifndef VS_ATTN_KDEPTH
+#define VS_ATTN_KDEPTH 3
+#endif
     auto qk = [&](int slot) {
         const char* base = smem + slot * KT + krd;
-        bf16x8_t ka = *reinterpret_cast<const bf16x8_t*>(base);
-        bf16x8_t kb = *reinterpret_cast<const bf16x8_t*>(base + 32 * KROW);
+        constexpr int DEP = VS_ATTN_KDEPTH;
+        bf16x8_t ka[8], kb[8];
+#pragma unroll
+        for (int ss = 0; ss < DEP; ++ss) {
+            ka[ss] = *reinterpret_cast<const bf16x8_t*>(base + 32 * ss);
+            kb[ss] = *reinterpret_cast<const bf16x8_t*>(base + 32 * KROW + 32 * ss);
+        }
 #pragma unroll
         for (int ss = 0; ss < 8; ++ss) {
-            bf16x8_t na, nb;
-            if (ss + 1 < 8) {
-                na = *reinterpret_cast<const bf16x8_t*>(base + 32 * (ss + 1));
-                nb = *reinterpret_cast<const bf16x8_t*>(base + 32 * KROW + 32 * (ss + 1));
+            if (ss + DEP < 8) {
+                ka[ss + DEP] = *reinterpret_cast<const bf16x8_t*>(base + 32 * (ss + DEP));
+                kb[ss + DEP] = *reinterpret_cast<const bf16x8_t*>(base + 32 * KROW + 32 * (ss + DEP));
             }
             __builtin_amdgcn_sched_barrier(0);
-            s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ss], ss == 0 ? negm : s[0], 0, 0, 0);
-            s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb, qf[ss], ss == 0 ? negm : s[1], 0, 0, 0);
-            if (ss + 1 < 8) {
-                ka = na;
-                kb = nb;
-            }
+            s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[ss], qf[ss], ss == 0 ? negm : s[0], 0, 0, 0);
+            s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb[ss], qf[ss], ss == 0 ? negm : s[1], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -213,6 +237,9 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     };
     // PV(prev) with the fast softmax of the current tile interleaved: the 4 MFMAs of k-step ks read
     // pk[ks] before the two chunks that overwrite it with P(i); V^T fragments one k-step ahead
+#ifdef VS_ATTN_STAMPS
+    int stamp_it = 0;
+#endif
     auto pv_softmax = [&](int slot, bool with_pv) {
         const char* base = smem + 2 * KT + slot * VT;
         rs0 = 0.f;
@@ -237,6 +264,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
             // chunk's sums to this point so its exps land in this k-step's MFMA region
             asm volatile("" : "+v"(rs0), "+v"(rs1));
             __builtin_amdgcn_sched_barrier(0);
+            if (with_pv) ATTN_STAMP(3 + ks);
         }
     };
     auto pv_last = [&](int slot) {
@@ -293,11 +321,17 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     const int grp = wave >> 2;
     if (grp == 1) phase_bar();
     for (int it = 0; it < nkv; ++it) {
+#ifdef VS_ATTN_STAMPS
+        stamp_it = it;
+#endif
+        ATTN_STAMP(0);
         // ---- B_{it-1}
         load_v(it * BKV);
         qk(it & 1);
         if (it + 1 < nkv) store_k((it + 1) & 1);
+        ATTN_STAMP(1);
         phase_bar();
+        ATTN_STAMP(2);
         // ---- A_it
         if (it + 2 < nkv) load_k((it + 2) * BKV);
         if ((it + 1) * BKV > Skv) {
@@ -317,8 +351,17 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
         if (__any(rs0 + rs1 > SUM_THR) || it == 0) exact(it == 0);
         l += rs0 + rs1;
         store_v(it & 1);
+        ATTN_STAMP(7);
         phase_bar();
     }
+#ifdef VS_ATTN_STAMPS
+    // stamps of tiles (nkv-32) .. nkv-1 (ring of 32), copied out by workgroup 0's waves 0 and 4
+    if (blockIdx.x == 0 && (wave & 3) == 0) {
+        for (int i = lane; i < 128; i += 64)
+            g_attn_stamps[wave >> 2][i] =
+                *reinterpret_cast<volatile unsigned long long*>(smem + LDS_BYTES + 8 * (wave * 128 + i));
+    }
+#endif
     // ---- B_{nkv-1}: the last tile's PV.  Group 0 first waits for group 1's half of V(nkv-1)
     // (stored in group 1's A_{nkv-1}, one phase later): the extra barrier that balances the count
     if (grp == 0) phase_bar();
@@ -356,6 +399,12 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 
 }  // namespace
 
+#ifdef VS_ATTN_STAMPS
+extern "C" int vs_debug_attn_stamps(unsigned long long* host_out) {
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps)) == hipSuccess ? 0 : 2;
+}
+#endif
+
 extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o, int batch, int sq,
                            int skv, int heads, int head_dim, long long ldq, long long ldk,
                            long long ldv, long long ldo, long long bsq, long long bsk,
@@ -382,8 +431,15 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
     }
     const float c = scale * 1.4426950408889634f;
     const bool rebase = (long long)skv * ldk * 2 >= (1LL << 31) || (long long)skv * ldv * 2 >= (1LL << 31);
+#ifdef VS_ATTN_STAMPS
+    const int lds = LDS_BYTES + STAMP_LDS;
+    (void)hipFuncSetAttribute((const void*)attn_fwd_d128<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_d128<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+#else
+    const int lds = LDS_BYTES;
+#endif
     hipLaunchKernelGGL(rebase ? attn_fwd_d128<true> : attn_fwd_d128<false>, dim3((unsigned)nwg), dim3(NTHR),
-                       LDS_BYTES, (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                       lds, (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                        (bf16_t*)o, sq, skv, heads, ldq, ldk, ldv, ldo, bsq, bsk, bsv, bso, c, nqb);
     VS_CHECK_LAUNCH();
     return VS_OK;
