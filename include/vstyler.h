@@ -82,6 +82,13 @@ int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
                 float scale, void* stream);
 
 /*
+ * The split-tail plan vs_attn_fwd uses on a device with `cus` compute units: out[0] = whole-item
+ * workgroups, out[1] = tail items split over key ranges, out[2] = pieces per tail item,
+ * out[3] = 64-key tiles per piece (out[1] = 0: no split).  Host-only, no device call.
+ */
+int vs_attn_split_plan(int batch, int sq, int skv, int heads, int cus, int* out);
+
+/*
  * out = bf16(LN(x)) [affine: weight/bias] then, if shift/scale given, modulate:
  * bf16(bf16(n * bf16(1+scale)) + shift) with shift/scale rows selected per batch.
  * Replaces WanAutoCastLayerNorm (layers.py:63-92) + modulate (wan_video_dit.py:64-65,225,228,268).

@@ -87,3 +87,25 @@ def test_lora_key_layouts():
     assert list(names) == ["blocks.3.cross_attn.o"]
     b, a = norm[names["blocks.3.cross_attn.o"][0]], norm[names["blocks.3.cross_attn.o"][1]]
     assert a.shape == (32, 16) and torch.allclose(b, torch.full((16, 32), 1.0))   # 2 * 16/32
+
+
+def test_attention_split_plan_host_only():
+    """vs_attn_split_plan is host arithmetic (no device call): the 14B 832x480x73 self-attention
+    grid (9280 items) on 256 CUs splits its last 64 items 4 ways; SP=8 (5 heads per rank) splits
+    136 items 7 ways; cross-attention (8 key tiles) and exact multiples are never split."""
+    from vstyler import _lib
+    lib = _lib.load()
+    out = (ctypes.c_int * 4)()
+    cases = [((2, 29640, 29640, 40, 256), (9216, 64, 4, 116)),
+             ((2, 29640, 29640, 5, 256), (1024, 136, 7, 67)),
+             ((2, 29640, 512, 40, 256), (9280, 0, 1, 0)),
+             ((1, 256 * 256, 4096, 1, 256), (256, 0, 1, 0)),
+             ((2, 29640, 29640, 40, 0), (9280, 0, 1, 0))]
+    for args, want in cases:
+        assert lib.vs_attn_split_plan(*args, out) == 0
+        assert tuple(out) == want, (args, tuple(out))
+        nmain, ntail, nsplit, tiles = want
+        if ntail:
+            nkv = (args[2] + 63) // 64
+            assert (nsplit - 1) * tiles < nkv <= nsplit * tiles
+    assert lib.vs_attn_split_plan(0, 1, 1, 1, 256, out) == 1

@@ -152,6 +152,40 @@ def test_attention_kv_slab_beyond_4gb(K):
     assert mx < 3e-2, mx
 
 
+def test_attention_split_tail(K, monkeypatch):
+    """Split tail: 270 items on 256 CUs leave 14 items that run as 3 key ranges of 21 tiles each
+    (the last ending in a partial tile) and are merged by the combine kernel.  Rows of whole and
+    split items against a torch fp32 reference, and the split result against the unsplit grid."""
+    B, Sq, Skv, H = 1, 23040, 4000, 3
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    plan = K.attention_split_plan(B, Sq, Skv, H, cus)
+    if cus == 256:
+        assert plan == (256, 14, 3, 21), plan
+    g = torch.Generator(device="cuda").manual_seed(70)
+    q = torch.randn(Sq, H * 128, device="cuda", generator=g).to(BF16)
+    k = torch.randn(Skv, H * 128, device="cuda", generator=g).to(BF16)
+    v = torch.randn(Skv, H * 128, device="cuda", generator=g).to(BF16)
+    out = torch.empty_like(q)
+    K.attention(q, k, v, out, H, B)
+    monkeypatch.setenv("VS_ATTN_NO_SPLIT", "1")
+    whole = torch.empty_like(q)
+    K.attention(q, k, v, whole, H, B)
+    monkeypatch.delenv("VS_ATTN_NO_SPLIT")
+    torch.cuda.synchronize()
+    # items 256..269 = head 2, q-blocks 76..89 (rows 19456..23039) are the split tail
+    rows = torch.cat([torch.arange(0, Sq, 997), torch.arange(19456, Sq, 61), torch.tensor([Sq - 1])]).cuda()
+    for h in range(H):
+        qs = q[rows, h * 128:(h + 1) * 128].float()
+        ref = torch.softmax(qs @ k[:, h * 128:(h + 1) * 128].float().t() * 128 ** -0.5, -1) @ \
+            v[:, h * 128:(h + 1) * 128].float()
+        mx = (out[rows, h * 128:(h + 1) * 128].float() - ref).abs().max().item()
+        assert mx < 3e-2, (h, mx)
+    d = (out.float() - whole.float()).abs()
+    assert d.max().item() < 2e-2, d.max().item()
+    assert torch.equal(out[:19456], whole[:19456])        # whole items are untouched by the split
+    assert torch.equal(out[:, :256], whole[:, :256])
+
+
 def test_attention_strided_views(K):
     # q/k/v as column slices of a fused [M, 3D] buffer (row stride 3D)
     B, S, H = 1, 200, 2

@@ -126,3 +126,53 @@ def test_ulysses_sp2_model_bit_identical_on_one_gpu():
         p.join(60)
     for rank, same, mx in res:
         assert same is True, res
+
+
+def _rccl_worker(port, q):
+    """World size 1 over the 'nccl' backend (RCCL): the product UlyssesGroup's device-side
+    all_to_all_single (async, waited on the current stream) and all_gather_into_tensor run for real.
+    Multi-rank RCCL needs one GPU per rank, which the 8-GPU scaling bench covers."""
+    try:
+        import sys
+        for p in (ROOT, os.path.join(ROOT, "video-styler_amd"), os.path.join(ROOT, "tests")):
+            if p not in sys.path:
+                sys.path.insert(0, p)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                          LOCAL_RANK="0")
+        from oracle import wan_oracle as O
+        from vstyler import model_fn_wan_video
+        from vstyler.usp import UlyssesGroup, init_distributed
+        from test_model_gpu import build
+        init_distributed()
+        assert torch.distributed.get_backend() == "nccl"
+        cfg = O.WAN_CONFIGS["tiny"]
+        W = O.random_weights(cfg, seed=5)
+        dit, vace = build(cfg, W, "cuda:0")
+        lat, cp, cn, vc = O.synthetic_inputs(cfg, 5, 128, 128)
+        t = torch.tensor([833.3333]).to(torch.bfloat16).cuda()
+        ctx = torch.cat([cp, cn]).cuda()
+        single = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx, vace_context=vc.cuda())
+        same = True
+        for overlap in (True, False):
+            sp = UlyssesGroup()
+            sp.overlap = overlap
+            par = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx,
+                                     vace_context=vc.cuda(), use_unified_sequence_parallel=True, sp_group=sp)
+            torch.cuda.synchronize()
+            same = same and torch.equal(single.cpu(), par.cpu())
+        torch.distributed.destroy_process_group()
+        q.put(same)
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(traceback.format_exc())
+
+
+@pytest.mark.gpu
+def test_ulysses_rccl_world1_bit_identical():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_port(), q))
+    p.start()
+    res = q.get(timeout=600)
+    p.join(60)
+    assert res is True, res

@@ -18,6 +18,10 @@
 //    K/V of one head is streamed by the 32 CUs of one XCD together and served from its L2.
 #include "common.h"
 
+#include <cstdlib>
+#include <map>
+#include <mutex>
+
 namespace {
 
 constexpr int HD = 128;          // head dim
@@ -29,8 +33,10 @@ constexpr int VROW = 320;        // LDS row pitch of the V tile (256 B + 64): tr
 constexpr int KT = BKV * KROW;   // 17408
 constexpr int VT = BKV * VROW;   // 20480
 constexpr int LDS_BYTES = 2 * (KT + VT);   // K ring 2 x 17408 + V ring 2 x 20480
+constexpr int PROW = HD + 4;     // split-tail partial row: 128 fp32 O, m, l, 2 pad (16-B aligned)
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
     // raw buffer descriptor; out-of-range loads return 0 (rows past Skv, masked anyway)
@@ -74,11 +80,24 @@ constexpr int STAMP_LDS = 8 * 4 * 32 * 8;
 template <bool REBASE>
 __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-    bf16_t* __restrict__ O, int Sq, int Skv, int H, long long ldq, long long ldk, long long ldv,
-    long long ldo, long long bsq, long long bsk, long long bsv, long long bso, float c, int nqb) {
+    bf16_t* __restrict__ O, int Sq, int Skv_all, int H, long long ldq, long long ldk, long long ldv,
+    long long ldo, long long bsq, long long bsk, long long bsv, long long bso, float c, int nqb,
+    int nmain, int nsplit, int piece_tiles, float* __restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
-    const int g = xcd_remap(blockIdx.x, gridDim.x);
+    // blocks [0, nmain) each run one whole (q-block, batch, head) item, XCD-remapped; the blocks
+    // after them run the last items of the grid as nsplit key ranges of piece_tiles tiles each
+    // (split tail, see vs_attn_fwd) and leave unnormalised partials for attn_combine
+    int g, piece = -1, kv_begin = 0, Skv = Skv_all;
+    if ((int)blockIdx.x < nmain) {
+        g = xcd_remap(blockIdx.x, nmain);
+    } else {
+        const int t = blockIdx.x - nmain;
+        g = nmain + t / nsplit;
+        piece = t % nsplit;
+        kv_begin = piece * piece_tiles * BKV;
+        Skv = min(Skv_all - kv_begin, piece_tiles * BKV);
+    }
     const int qb = g % nqb;
     const int bh = g / nqb;
     const int h = bh % H, b = bh / H;
@@ -88,8 +107,8 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     const int q0 = qb * BQ + wave * 32;
 
     const bf16_t* Qb = Q + (long long)b * bsq + h * HD;
-    const bf16_t* Kb = K + (long long)b * bsk + h * HD;
-    const bf16_t* Vb = V + (long long)b * bsv + h * HD;
+    const bf16_t* Kb = K + (long long)b * bsk + (long long)kv_begin * ldk + h * HD;
+    const bf16_t* Vb = V + (long long)b * bsv + (long long)kv_begin * ldv + h * HD;
 
     // buffer descriptors over this (batch, head)'s K/V rows: per-lane byte offset constant, the
     // tile's row offset in soffset.  REBASE (a slab beyond 2^31 bytes, e.g. 1280x720x121 with the
@@ -179,15 +198,41 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
 
     f32x16_t s[2];        // S^T of the current tile: keys 32t + (i&3) + 8(i>>2) + 4hh, row q0 + r
     u32x4_t pk[4];        // P as the PV B operands (bf16 pairs): keys 16ks .. 16ks+15 of this lane's row
+    // row-sum partials.  VS_ATTN_RSINIT: the tile's first chunk initialises them (no 0 + p adds);
+    // VS_ATTN_PKSUM: one packed pair summed with v_pk_add_f32 (implies RSINIT)
+#ifdef VS_ATTN_PKSUM
+#define VS_ATTN_RSINIT 1
+    f32x2_t rsv;
+#define RS_TOTAL (rsv.x + rsv.y)
+#define RS_RESET()
+#define RS_PIN() asm volatile("" : "+v"(rsv))
+#else
     float rs0, rs1;
+#define RS_TOTAL (rs0 + rs1)
+#ifdef VS_ATTN_RSINIT
+#define RS_RESET()
+#else
+#define RS_RESET() (rs0 = 0.f, rs1 = 0.f)
+#endif
+#define RS_PIN() asm volatile("" : "+v"(rs0), "+v"(rs1))
+#endif
     auto p_chunk = [&](int ss) {   // elements 4ss..4ss+3 (flat 16t + i) of the tile's 32 scores
         const int t = ss >> 2, i0 = 4 * (ss & 3);
         const float p0 = __builtin_amdgcn_exp2f(s[t][i0]);
         const float p1 = __builtin_amdgcn_exp2f(s[t][i0 + 1]);
         const float p2 = __builtin_amdgcn_exp2f(s[t][i0 + 2]);
         const float p3 = __builtin_amdgcn_exp2f(s[t][i0 + 3]);
+#if defined(VS_ATTN_PKSUM)
+        const f32x2_t pa = {p0, p2}, pb = {p1, p3};
+        if (ss == 0) rsv = pa + pb;
+        else rsv += pa + pb;
+#elif defined(VS_ATTN_RSINIT)
+        if (ss == 0) { rs0 = p0 + p1; rs1 = p2 + p3; }
+        else { rs0 += p0 + p1; rs1 += p2 + p3; }
+#else
         rs0 += p0 + p1;
         rs1 += p2 + p3;
+#endif
         const int ks = 2 * t + (i0 >> 3), j = (i0 & 7) >> 1;
         const bf16x2_t w0 = {(__bf16)p0, (__bf16)p1}, w1 = {(__bf16)p2, (__bf16)p3};
         pk[ks][j] = __builtin_bit_cast(unsigned, w0);
@@ -242,8 +287,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
 #endif
     auto pv_softmax = [&](int slot, bool with_pv) {
         const char* base = smem + 2 * KT + slot * VT;
-        rs0 = 0.f;
-        rs1 = 0.f;
+        RS_RESET();
         bf16x8_t va[4], vb[4];
         if (with_pv) read_vt(base, 0, va);
 #pragma unroll
@@ -262,7 +306,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
             p_chunk(2 * ks + 1);
             // pure VALU floats freely in the DAG (a sched_barrier alone does not hold it): tie the
             // chunk's sums to this point so its exps land in this k-step's MFMA region
-            asm volatile("" : "+v"(rs0), "+v"(rs1));
+            RS_PIN();
             __builtin_amdgcn_sched_barrier(0);
             if (with_pv) ATTN_STAMP(3 + ks);
         }
@@ -306,8 +350,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
             for (int i = 0; i < 16; ++i) s[t][i] += delta;
 #pragma unroll
         for (int i = 0; i < 16; ++i) negm[i] = -mnew;
-        rs0 = 0.f;
-        rs1 = 0.f;
+        RS_RESET();
 #pragma unroll
         for (int ss = 0; ss < 8; ++ss) p_chunk(ss);
     };
@@ -348,8 +391,8 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
             pv_softmax((it - 1) & 1, true);
         else
             pv_softmax(0, false);
-        if (__any(rs0 + rs1 > SUM_THR) || it == 0) exact(it == 0);
-        l += rs0 + rs1;
+        if (__any(RS_TOTAL > SUM_THR) || it == 0) exact(it == 0);
+        l += RS_TOTAL;
         store_v(it & 1);
         ATTN_STAMP(7);
         phase_bar();
@@ -368,6 +411,18 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     pv_last((nkv - 1) & 1);
 
     const float lt = l + __shfl_xor(l, 32);
+    if (piece >= 0) {
+        // split-tail piece: O unnormalised (fp32, natural column order) + the row's (m, l)
+        float* pp = part + ((long long)(g - nmain) * nsplit + piece) * BQ * PROW + (wave * 32 + r) * PROW;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int gi = 0; gi < 4; ++gi)
+                *reinterpret_cast<f32x4_t*>(pp + 32 * dt + 8 * gi + 4 * hh) =
+                    f32x4_t{o[dt][4 * gi], o[dt][4 * gi + 1], o[dt][4 * gi + 2], o[dt][4 * gi + 3]};
+        if (hh == 0) *reinterpret_cast<f32x2_t*>(pp + HD) = f32x2_t{m, lt};
+        return;
+    }
     const float inv = 1.f / lt;
     // lane (r, hh) holds columns 32dt + 8gi + 4hh .. +3 of row q0+r; pair groups (gi, gi+1) through
     // one permlane32_swap per dword so each lane stores 16 contiguous bytes
@@ -395,7 +450,86 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     }
 }
 
+// Split-tail combine: one thread per (item, row, 4 columns).  A row's pieces j hold O_j and l_j
+// against their own reference max m_j (exp2 domain): O = sum_j 2^(m_j - M) O_j / sum_j 2^(m_j - M) l_j.
+__global__ __launch_bounds__(256) void attn_combine(const float* __restrict__ part, bf16_t* __restrict__ O,
+                                                    int ntail, int nmain, int nsplit, int Sq, int H, int nqb,
+                                                    long long ldo, long long bso) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int c4 = (int)(idx & 31);
+    const long long rowid = idx >> 5;              // item * BQ + row
+    if (rowid >= (long long)ntail * BQ) return;
+    const int it = (int)(rowid / BQ), row = (int)(rowid % BQ);
+    const int g = nmain + it;
+    const int qb = g % nqb, bh = g / nqb, h = bh % H, b = bh / H;
+    const int q = qb * BQ + row;
+    if (q >= Sq) return;
+    const float* base = part + (long long)it * nsplit * BQ * PROW + (long long)row * PROW;
+    float M = -INFINITY;
+    for (int j = 0; j < nsplit; ++j) M = fmaxf(M, base[(long long)j * BQ * PROW + HD]);
+    f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+    float lsum = 0.f;
+    for (int j = 0; j < nsplit; ++j) {
+        const float* pj = base + (long long)j * BQ * PROW;
+        const float w = __builtin_amdgcn_exp2f(pj[HD] - M);
+        lsum += w * pj[HD + 1];
+        acc += w * *reinterpret_cast<const f32x4_t*>(pj + 4 * c4);
+    }
+    const float inv = 1.f / lsum;
+    bf16_t* op = O + (long long)b * bso + (long long)q * ldo + h * HD + 4 * c4;
+    const unsigned lo = pack2(acc[0] * inv, acc[1] * inv), hi = pack2(acc[2] * inv, acc[3] * inv);
+    *reinterpret_cast<uint2*>(op) = make_uint2(lo, hi);
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// Split tail.  One workgroup fills a CU (2 waves per SIMD), so a grid of n items runs in
+// ceil(n / CUs) rounds and the last, partial round leaves CUs idle (the 14B 832x480x73 self-
+// attention: 9280 items = 36.25 rounds on 256 CUs; under Ulysses SP=8 1160 = 4.53).  The last
+// n % CUs items instead run as nsplit key ranges each, chosen to minimise the tail's length in
+// item units (ceil(tail * nsplit / CUs) / nsplit), then one combine launch.  Partials live in a
+// per-device workspace allocated once, outside any graph capture (graph capture without it
+// falls back to the unsplit grid).
+constexpr int MAX_PIECES = 1024;
+struct SplitPlan { int nmain = 0, ntail = 0, nsplit = 1, piece_tiles = 0; };
+
+SplitPlan plan_split(long long nwg, int nkv, int cus) {
+    SplitPlan p;
+    p.nmain = (int)nwg;
+    if (cus <= 0 || nkv < 32) return p;
+    const int tail = (int)(nwg % cus);
+    if (tail == 0 || nwg < cus) return p;
+    double best = 1.0;
+    int bf = 1;
+    for (int f = 2; f <= 16 && tail * f <= MAX_PIECES && nkv / f >= 16; ++f) {
+        const double cost = (double)((tail * f + cus - 1) / cus) / f + 0.01 * f;   // + per-piece overhead
+        if (cost < best - 0.05) { best = cost; bf = f; }
+    }
+    if (bf == 1) return p;
+    p.ntail = tail;
+    p.nmain = (int)(nwg - tail);
+    p.piece_tiles = (nkv + bf - 1) / bf;
+    p.nsplit = (nkv + p.piece_tiles - 1) / p.piece_tiles;
+    return p;
+}
+
+// one workspace per (device, stream): launches on concurrent streams never share partials.
+// may_alloc is false while the stream is being captured (no hipMalloc inside a capture).
+float* split_workspace(int dev, hipStream_t stream, bool may_alloc) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, float*> ws;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = ws.find({dev, stream});
+    if (it != ws.end()) return it->second;
+    if (!may_alloc) return nullptr;
+    void* ptr = nullptr;
+    if (hipMalloc(&ptr, (size_t)MAX_PIECES * BQ * PROW * sizeof(float)) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    ws[{dev, stream}] = (float*)ptr;
+    return (float*)ptr;
+}
 
 }  // namespace
 
@@ -438,9 +572,45 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
 #else
     const int lds = LDS_BYTES;
 #endif
-    hipLaunchKernelGGL(rebase ? attn_fwd_d128<true> : attn_fwd_d128<false>, dim3((unsigned)nwg), dim3(NTHR),
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    static int cus_by_dev[64] = {};
+    if (dev >= 0 && dev < 64 && cus_by_dev[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = -1;
+        cus_by_dev[dev] = n;
+    }
+    const int cus = (dev >= 0 && dev < 64 && !getenv("VS_ATTN_NO_SPLIT")) ? cus_by_dev[dev] : 0;
+    SplitPlan sp = plan_split(nwg, (skv + BKV - 1) / BKV, cus);
+    float* part = nullptr;
+    if (sp.ntail) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        (void)hipStreamIsCapturing((hipStream_t)stream, &cs);
+        part = split_workspace(dev, (hipStream_t)stream, cs == hipStreamCaptureStatusNone);
+        if (!part) sp = SplitPlan{(int)nwg, 0, 1, 0};
+    }
+    const long long grid = (long long)sp.nmain + (long long)sp.ntail * sp.nsplit;
+    hipLaunchKernelGGL(rebase ? attn_fwd_d128<true> : attn_fwd_d128<false>, dim3((unsigned)grid), dim3(NTHR),
                        lds, (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                       (bf16_t*)o, sq, skv, heads, ldq, ldk, ldv, ldo, bsq, bsk, bsv, bso, c, nqb);
+                       (bf16_t*)o, sq, skv, heads, ldq, ldk, ldv, ldo, bsq, bsk, bsv, bso, c, nqb,
+                       sp.nmain, sp.nsplit, sp.piece_tiles, part);
     VS_CHECK_LAUNCH();
+    if (sp.ntail) {
+        const long long threads = (long long)sp.ntail * BQ * 32;
+        hipLaunchKernelGGL(attn_combine, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                           part, (bf16_t*)o, sp.ntail, sp.nmain, sp.nsplit, sq, heads, nqb, ldo, bso);
+        VS_CHECK_LAUNCH();
+    }
+    return VS_OK;
+}
+
+extern "C" int vs_attn_split_plan(int batch, int sq, int skv, int heads, int cus, int* out) {
+    if (!out || batch <= 0 || sq <= 0 || skv <= 0 || heads <= 0 || cus < 0) return VS_E_INVALID;
+    const long long nwg = (long long)((sq + BQ - 1) / BQ) * heads * batch;
+    const SplitPlan p = plan_split(nwg, (skv + BKV - 1) / BKV, cus);
+    out[0] = p.nmain;
+    out[1] = p.ntail;
+    out[2] = p.nsplit;
+    out[3] = p.piece_tiles;
     return VS_OK;
 }

@@ -3,6 +3,8 @@
 PyTorch is used only for device memory and streams; every computation below is a kernel of
 libvstyler.so.  Wrappers validate dtype/device/layout and raise ValueError before launching.
 """
+import ctypes
+
 import torch
 
 from . import _lib
@@ -128,6 +130,13 @@ def attention(q, k, v, out, num_heads, batch, scale=None):
                                        skv, num_heads, hd, ldq, ldk, ldv, ldo, sq * ldq, skv * ldk,
                                        skv * ldv, sq * ldo, float(scale), _stream(q)))
     return out
+
+
+def attention_split_plan(batch, sq, skv, heads, cus):
+    """(whole-item workgroups, split tail items, pieces per item, tiles per piece) of vs_attn_fwd."""
+    out = (ctypes.c_int * 4)()
+    _lib.check(_lib.load().vs_attn_split_plan(batch, sq, skv, heads, cus, out))
+    return tuple(out)
 
 
 def layernorm_modulate(x, out, eps=1e-6, shift=None, scale=None, mod_bstride=0, rows_per_batch=0,
