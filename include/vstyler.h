@@ -3,8 +3,12 @@
  *
  * The library replaces the GPU operators of the Wan2.1(-VACE) denoising path of the reference
  * (Ditto / DiffSynth-Studio 1.1.8, paths relative to the reference root).  Every entry point is
- * stream-ordered, allocation-free and graph-capturable; pointers are caller-owned device buffers
+ * stream-ordered and graph-capturable; pointers are caller-owned device buffers
  * (bf16 unless stated, row-major), sizes/strides are in ELEMENTS.  No C++ types cross the ABI.
+ *
+ * Allocation: none per call.  vs_gemm and vs_attn_fwd keep one fp32 split-tail workspace per
+ * (device, stream), allocated on first need outside graph capture (inside a capture without one
+ * they launch unsplit); see vs_gemm_split_plan / vs_attn_split_plan.
  *
  * Error convention: every call returns 0 (VS_OK) or a VS_E_* code; shape/alignment violations are
  * rejected up front with VS_E_INVALID before anything is launched.  vs_strerror() names a code.
@@ -55,6 +59,13 @@ typedef struct vs_epilogue {
 int vs_gemm(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc,
             int m, int n, int k, int epilogue, const vs_epilogue* epi,
             const void* a2, long long lda2, const void* w2, long long ldw2, int k2, void* stream);
+
+/*
+ * The split-tail plan vs_gemm uses for its 256x256 schedule on a device with `cus` compute units
+ * (no LoRA second phase): out[0] = whole-tile workgroups, out[1] = tail tiles split along K,
+ * out[2] = K pieces per tail tile, out[3] = K per piece (out[1] = 0: no split).  Host-only.
+ */
+int vs_gemm_split_plan(int m, int n, int k, int cus, int* out);
 
 /*
  * fp8 path (config 5; AutoWrappedLinear.fp8_linear, diffsynth/vram_management/layers.py:115-151):

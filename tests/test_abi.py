@@ -109,3 +109,27 @@ def test_attention_split_plan_host_only():
             nkv = (args[2] + 63) // 64
             assert (nsplit - 1) * tiles < nkv <= nsplit * tiles
     assert lib.vs_attn_split_plan(0, 1, 1, 1, 256, out) == 1
+
+
+def test_gemm_split_plan_host_only():
+    """vs_gemm_split_plan (host arithmetic, measured cost model): the 14B N=5120 GEMMs (4640 tiles)
+    split their last 32 tiles 8 ways along K; under SP=8 (7410 rows) 580 tiles -> 68 split 3 ways;
+    FFN-up (12528 tiles, tail 240), a 136-tile tail at K=5120 (where the partial-tile traffic
+    costs more than it saves) and grids below one round are not split."""
+    from vstyler import _lib
+    lib = _lib.load()
+    out = (ctypes.c_int * 4)()
+    cases = [((59280, 5120, 5120, 256), (4608, 32, 8, 640)),
+             ((59280, 5120, 13824, 256), (4608, 32, 8, 1728)),
+             ((7410, 5120, 5120, 256), (512, 68, 3, 1728)),
+             ((59280, 13824, 5120, 256), (12528, 0, 1, 0)),
+             ((14820, 5120, 5120, 256), (1160, 0, 1, 0)),
+             ((1024, 1024, 4096, 256), (16, 0, 1, 0)),
+             ((59280, 5120, 5120, 0), (4640, 0, 1, 0))]
+    for args, want in cases:
+        assert lib.vs_gemm_split_plan(*args, out) == 0
+        assert tuple(out) == want, (args, tuple(out))
+        nmain, ntail, ks, pk = want
+        if ntail:
+            assert pk % 32 == 0 and (ks - 1) * pk < args[2] <= ks * pk
+    assert lib.vs_gemm_split_plan(64, 64, 100, 256, out) == 1

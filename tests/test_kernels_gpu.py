@@ -79,6 +79,48 @@ def test_gemm_epilogues(K):
     assert err(x, O.add(res, O.bf(0.5 * y.float())))[1] < 4e-3
 
 
+def test_gemm_split_tail_exact(K, monkeypatch):
+    """Split tail of the 256x256 schedule: 18 x 16 = 288 tiles (last row and column partial) on
+    256 CUs run 256 whole tiles and 32 tail tiles as 8 K pieces (7 x 544 + 352), summed and finished by the
+    combine kernel.  Integer operands keep every fp32 sum exact, so the result must equal the
+    exact product and, for every epilogue, the unsplit grid bit for bit."""
+    M, N, Kd = 4452, 4000, 4160
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    if cus == 256:
+        assert K.gemm_split_plan(M, N, Kd, cus) == (256, 32, 8, 544)
+    g = torch.Generator(device="cuda").manual_seed(80)
+    a = torch.randint(-3, 4, (M, Kd), device="cuda", generator=g).to(BF16)
+    w = torch.randint(-3, 4, (N, Kd), device="cuda", generator=g).to(BF16)
+    b = torch.randint(-8, 9, (N,), device="cuda", generator=g).to(BF16)
+    res = torch.randn(M, N, device="cuda", generator=g).to(BF16)
+    gate = (0.25 * torch.randn(2, N, device="cuda", generator=g)).to(BF16)
+    out = torch.empty(M, N, dtype=BF16, device="cuda")
+    K.gemm(a, w, out, bias=b)
+    ref = (a.float() @ w.float().t() + b.float()).to(BF16)
+    assert torch.equal(out, ref)
+
+    def run(split):
+        if split:
+            monkeypatch.delenv("VS_GEMM_NO_SPLIT", raising=False)
+        else:
+            monkeypatch.setenv("VS_GEMM_NO_SPLIT", "1")
+        outs = []
+        y = torch.empty(M, N, dtype=BF16, device="cuda")
+        K.gemm(a, w, y, epilogue=K.VS_EPI_GELU, bias=b)
+        outs.append(y)
+        x = res.clone()
+        K.gemm(a, w, x, epilogue=K.VS_EPI_GATE_RES, bias=b, residual=x, gate=gate, gate_bstride=N,
+               rows_per_batch=M // 2 + 1, hint=res, hint_scale=0.5)
+        outs.append(x)
+        x = res.clone()
+        K.gemm(a, w, x, epilogue=K.VS_EPI_RES, residual=x, alpha=0.125)
+        outs.append(x)
+        return outs
+    for s_, u_ in zip(run(True), run(False)):
+        assert torch.equal(s_, u_)
+    monkeypatch.delenv("VS_GEMM_NO_SPLIT", raising=False)
+
+
 def test_gemm_lora_second_phase(K):
     M, N, Kd, r = 200, 320, 256, 128
     x, w, b = rnd(M, Kd, seed=11), rnd(N, Kd, scale=0.05, seed=12), rnd(N, scale=0.1, seed=13)

@@ -18,10 +18,6 @@
 //    K/V of one head is streamed by the 32 CUs of one XCD together and served from its L2.
 #include "common.h"
 
-#include <cstdlib>
-#include <map>
-#include <mutex>
-
 namespace {
 
 constexpr int HD = 128;          // head dim
@@ -488,7 +484,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 // attention: 9280 items = 36.25 rounds on 256 CUs; under Ulysses SP=8 1160 = 4.53).  The last
 // n % CUs items instead run as nsplit key ranges each, chosen to minimise the tail's length in
 // item units (ceil(tail * nsplit / CUs) / nsplit), then one combine launch.  Partials live in a
-// per-device workspace allocated once, outside any graph capture (graph capture without it
+// per-(device, stream) workspace allocated once, outside any graph capture (graph capture without it
 // falls back to the unsplit grid).
 constexpr int MAX_PIECES = 1024;
 struct SplitPlan { int nmain = 0, ntail = 0, nsplit = 1, piece_tiles = 0; };
@@ -513,23 +509,6 @@ SplitPlan plan_split(long long nwg, int nkv, int cus) {
     return p;
 }
 
-// one workspace per (device, stream): launches on concurrent streams never share partials.
-// may_alloc is false while the stream is being captured (no hipMalloc inside a capture).
-float* split_workspace(int dev, hipStream_t stream, bool may_alloc) {
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, float*> ws;
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = ws.find({dev, stream});
-    if (it != ws.end()) return it->second;
-    if (!may_alloc) return nullptr;
-    void* ptr = nullptr;
-    if (hipMalloc(&ptr, (size_t)MAX_PIECES * BQ * PROW * sizeof(float)) != hipSuccess) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    ws[{dev, stream}] = (float*)ptr;
-    return (float*)ptr;
-}
 
 }  // namespace
 
@@ -572,21 +551,10 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
 #else
     const int lds = LDS_BYTES;
 #endif
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    static int cus_by_dev[64] = {};
-    if (dev >= 0 && dev < 64 && cus_by_dev[dev] == 0) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = -1;
-        cus_by_dev[dev] = n;
-    }
-    const int cus = (dev >= 0 && dev < 64 && !getenv("VS_ATTN_NO_SPLIT")) ? cus_by_dev[dev] : 0;
-    SplitPlan sp = plan_split(nwg, (skv + BKV - 1) / BKV, cus);
+    SplitPlan sp = plan_split(nwg, (skv + BKV - 1) / BKV, vs_cus_for_split("VS_ATTN_NO_SPLIT"));
     float* part = nullptr;
     if (sp.ntail) {
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        (void)hipStreamIsCapturing((hipStream_t)stream, &cs);
-        part = split_workspace(dev, (hipStream_t)stream, cs == hipStreamCaptureStatusNone);
+        part = vs_split_workspace(0, (size_t)MAX_PIECES * BQ * PROW * sizeof(float), (hipStream_t)stream);
         if (!part) sp = SplitPlan{(int)nwg, 0, 1, 0};
     }
     const long long grid = (long long)sp.nmain + (long long)sp.ntail * sp.nsplit;

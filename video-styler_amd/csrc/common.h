@@ -51,3 +51,47 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     do {                                                             \
         if (hipGetLastError() != hipSuccess) return VS_E_LAUNCH;     \
     } while (0)
+
+// ---- host helpers shared by the split-tail launches (attention.hip, gemm.hip) ----------------
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
+
+// compute units of the current device (0 when unknown or when `env_off` is set: no split)
+inline int vs_cus_for_split(const char* env_off) {
+    if (env_off && getenv(env_off)) return 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    static std::mutex mu;
+    static std::map<int, int> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(dev);
+    if (it != cache.end()) return it->second;
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+    cache[dev] = n;
+    return n;
+}
+
+// One fp32 workspace per (tag, device, stream), allocated once with its fixed size: launches on
+// concurrent streams never share partials, and none is allocated while `stream` is being captured
+// into a graph (the caller then launches without a split).  nullptr when unavailable.
+inline float* vs_split_workspace(int tag, size_t bytes, hipStream_t stream) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, hipStream_t>, float*> ws;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = ws.find({tag, dev, stream});
+    if (it != ws.end()) return it->second;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    void* ptr = nullptr;
+    if (hipMalloc(&ptr, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    ws[{tag, dev, stream}] = (float*)ptr;
+    return (float*)ptr;
+}

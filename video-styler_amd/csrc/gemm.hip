@@ -261,23 +261,63 @@ __device__ unsigned long long g_gemm_stamps[2][5 * 32];
 #define STAMP(slot) do {} while (0)
 #endif
 
-template <bool BUF>
-__global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
-    const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
-    bf16_t* C, long long ldc, int M, int N, int K, const bf16_t* __restrict__ A2, long long lda2,
-    const bf16_t* __restrict__ W2, long long ldw2, int K2, Epi ep, int ntm, int ntn) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-
-    const int pid = xcd_remap(blockIdx.x, gridDim.x);
+// tile id -> (tm, tn): raster groups of GM M-tiles sweep all N-tiles, so consecutive ids on one
+// XCD share the weight tile in L2
+__device__ __forceinline__ void tile_of(int pid, int ntm, int ntn, int& tm, int& tn) {
     constexpr int GM = VS_GEMM_GM;
     const int per_group = GM * ntn;
     const int group = pid / per_group;
     const int first_m = group * GM;
     const int gsz = min(ntm - first_m, GM);
     const int in_g = pid % per_group;
-    const int tm = first_m + in_g % gsz;
-    const int tn = in_g / gsz;
+    tm = first_m + in_g % gsz;
+    tn = in_g / gsz;
+}
+
+// Split-tail combine: one thread per (tail tile, row, 4 columns): sum the ksplit fp32 partials in
+// piece order, then the same epilogue as the unsplit kernel
+__global__ __launch_bounds__(256) void gemm_split_combine(const float* __restrict__ part, bf16_t* C, long long ldc,
+                                                          int M, int N, Epi ep, int ntm, int ntn, int nmain,
+                                                          int ntail, int ksplit) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long long)ntail * BT * (BT / 4)) return;
+    const int t = (int)(idx / (BT * (BT / 4)));
+    const int rem = (int)(idx % (BT * (BT / 4)));
+    const int row = rem / (BT / 4), c4 = rem % (BT / 4);
+    int tm, tn;
+    tile_of(nmain + t, ntm, ntn, tm, tn);
+    const int m = tm * BT + row, n = tn * BT + 4 * c4;
+    if (m >= M || n >= N) return;
+    const float* pp = part + (long long)t * ksplit * BT * BT + row * BT + 4 * c4;
+    f32x4_t a = *reinterpret_cast<const f32x4_t*>(pp);
+    for (int j = 1; j < ksplit; ++j) a += *reinterpret_cast<const f32x4_t*>(pp + (long long)j * BT * BT);
+    epilogue_store(a, m, n, C, ldc, ep);
+}
+
+template <bool BUF>
+__global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
+    const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
+    bf16_t* C, long long ldc, int M, int N, int K, const bf16_t* __restrict__ A2, long long lda2,
+    const bf16_t* __restrict__ W2, long long ldw2, int K2, Epi ep, int ntm, int ntn, int nmain, int ksplit,
+    int piece_k, float* __restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    // blocks [0, nmain) own whole tiles (XCD-remapped); the blocks after them run the last tiles
+    // of the grid as ksplit K ranges of piece_k each and leave fp32 partial tiles for
+    // gemm_split_combine (split tail, see vs_gemm; never with a LoRA second phase)
+    int pid, piece = -1;
+    if ((int)blockIdx.x < nmain) {
+        pid = xcd_remap(blockIdx.x, nmain);
+    } else {
+        const int t = blockIdx.x - nmain;
+        pid = nmain + t / ksplit;
+        piece = t % ksplit;
+    }
+    int tm, tn;
+    tile_of(pid, ntm, ntn, tm, tn);
     const int m0 = tm * BT, n0 = tn * BT;
+    const int kb = piece < 0 ? 0 : piece * piece_k;
+    const int Kp = piece < 0 ? K : min(K - kb, piece_k);
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -294,10 +334,10 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
     // wave w issues pieces 4w..4w+3 (waves 0-3: A, waves 4-7: W).
     const int prow = lane >> 2;
     const int pch = (lane & 3) ^ ((3 * (prow >> 2)) & 3);
-    const int nh1 = K / HK;
-    const int nh = nh1 + K2 / HK;
+    const int nh1 = Kp / HK;
+    const int nh = nh1 + (piece < 0 ? K2 / HK : 0);
     // operand this wave streams (group 0: activations A/A2 rows m0.., group 1: weights W/W2 rows n0..)
-    const bf16_t* Pm = wm == 0 ? A : W;
+    const bf16_t* Pm = (wm == 0 ? A : W) + kb;
     const bf16_t* Pl = wm == 0 ? A2 : W2;
     const long long ldm = wm == 0 ? lda : ldw;
     const long long ldl = wm == 0 ? lda2 : ldw2;
@@ -439,6 +479,16 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
     if (wm == 0) bar();
 #endif
 
+    if (piece >= 0) {
+        float* pp = part + ((long long)(pid - nmain) * ksplit + piece) * BT * BT;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                *reinterpret_cast<f32x4_t*>(pp + (wm * 128 + i * 16 + (lane & 15)) * BT + wn * 64 + j * 16 +
+                                            4 * (lane >> 4)) = acc[i][j];
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int m = m0 + wm * 128 + i * 16 + (lane & 15);
@@ -823,6 +873,42 @@ extern "C" int vs_debug_gemm_stamps(unsigned long long* host_out) {
 }
 #endif
 
+// Split tail.  One 256x256 workgroup fills a CU, so a grid of T tiles runs in ceil(T / CUs)
+// rounds and the last, partial one leaves CUs idle: the 14B N=5120 GEMMs on 2 x 29640 tokens are
+// 4640 tiles = 18.1 rounds on 256 CUs, and under Ulysses SP=8 (7410 rows) 580 tiles = 2.27.  The
+// last T % CUs tiles instead run as ksplit K ranges each (fp32 partial tiles in a per-(device,
+// stream) workspace, then one combine launch that applies the epilogue), ksplit chosen by the
+// measured cost model below.
+constexpr int MAX_SPLIT_PIECES = 512;        // 512 x 256 KB fp32 partial tiles
+struct KSplit { int nmain = 0, ntail = 0, ksplit = 1, piece_k = 0; };
+
+KSplit plan_ksplit(int ntiles, int nh, int cus) {
+    // Cost model in microseconds, calibrated on MI355X (tests/probes/split_ab.py): a whole tile
+    // takes t = K * 0.029 us at ~1150 TF/s; a round of pieces costs t/f plus ~18 us (prologue and
+    // the fp32 partial-tile writes, 256 KB per piece); the combine ~5 us + 0.065 us per partial
+    // tile read.  Split only when the tail drops below 0.85 t.
+    KSplit p;
+    p.nmain = ntiles;
+    if (cus <= 0 || ntiles < cus) return p;
+    const int tail = ntiles % cus;
+    if (tail == 0) return p;
+    const double t = nh * HK * 0.029;
+    double best = 0.85 * t;
+    int bf = 1;
+    for (int f = 2; f <= 16 && tail * f <= MAX_SPLIT_PIECES && nh / f >= 16; ++f) {
+        const int rounds = (tail * f + cus - 1) / cus;
+        const double cost = rounds * (t / f + 18.0) + 5.0 + 0.065 * tail * f;
+        if (cost < best) { best = cost; bf = f; }
+    }
+    if (bf == 1) return p;
+    const int piece_h = (nh + bf - 1) / bf;
+    p.ntail = tail;
+    p.nmain = ntiles - tail;
+    p.piece_k = piece_h * HK;
+    p.ksplit = (nh + piece_h - 1) / piece_h;
+    return p;
+}
+
 static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n) {
     if (epilogue < VS_EPI_BIAS || epilogue > VS_EPI_RES) return VS_E_INVALID;
     ep = Epi{};
@@ -903,17 +989,32 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
             const char* e = getenv("VS_GEMM_FLAT_DMA");   // 1: flat-address DMA (A/B)
             buf_ok = !(e && e[0] == '1');
         }
+        KSplit sp = k2 ? KSplit{tm * tn, 0, 1, 0}
+                       : plan_ksplit(tm * tn, k / HK, vs_cus_for_split("VS_GEMM_NO_SPLIT"));
+        float* part = nullptr;
+        if (sp.ntail) {
+            part = vs_split_workspace(1, (size_t)MAX_SPLIT_PIECES * BT * BT * sizeof(float), (hipStream_t)stream);
+            if (!part) sp = KSplit{tm * tn, 0, 1, 0};
+        }
+        const unsigned grid = (unsigned)(sp.nmain + sp.ntail * sp.ksplit);
         if (buf_ok && fits32)
-            hipLaunchKernelGGL(gemm_bf16_tn_256<true>, dim3((unsigned)(tm * tn)), dim3(NTHR8), RING * SLOT,
+            hipLaunchKernelGGL(gemm_bf16_tn_256<true>, dim3(grid), dim3(NTHR8), RING * SLOT,
                                (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw,
                                (bf16_t*)c, ldc, m, n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2,
-                               k2, ep, tm, tn);
+                               k2, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part);
         else
-            hipLaunchKernelGGL(gemm_bf16_tn_256<false>, dim3((unsigned)(tm * tn)), dim3(NTHR8), RING * SLOT,
+            hipLaunchKernelGGL(gemm_bf16_tn_256<false>, dim3(grid), dim3(NTHR8), RING * SLOT,
                                (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw,
                                (bf16_t*)c, ldc, m, n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2,
-                               k2, ep, tm, tn);
+                               k2, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part);
         VS_CHECK_LAUNCH();
+        if (sp.ntail) {
+            const long long threads = (long long)sp.ntail * BT * (BT / 4);
+            hipLaunchKernelGGL(gemm_split_combine, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                               (hipStream_t)stream, part, (bf16_t*)c, ldc, m, n, ep, tm, tn, sp.nmain, sp.ntail,
+                               sp.ksplit);
+            VS_CHECK_LAUNCH();
+        }
         return VS_OK;
     }
     const int ntm = (m + BM - 1) / BM, ntn = (n + BN - 1) / BN;
@@ -973,5 +1074,15 @@ extern "C" int vs_quant_fp8_rows(const void* x, long long ldx, void* x8, long lo
     hipLaunchKernelGGL(quant_fp8_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)x, ldx, (uint8_t*)x8, ld8, scale, rows, cols);
     VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_gemm_split_plan(int m, int n, int k, int cus, int* out) {
+    if (!out || m <= 0 || n <= 0 || k <= 0 || k % BK || cus < 0) return VS_E_INVALID;
+    const KSplit p = plan_ksplit(((m + BT - 1) / BT) * ((n + BT - 1) / BT), k / HK, cus);
+    out[0] = p.nmain;
+    out[1] = p.ntail;
+    out[2] = p.ksplit;
+    out[3] = p.piece_k;
     return VS_OK;
 }

@@ -59,6 +59,7 @@ SIGNATURES = {
     "vs_attn_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _LL, _LL, _LL, _LL, _LL, _LL, _LL, _LL,
                     _F, _P],
     "vs_attn_split_plan": [_I, _I, _I, _I, _I, _P],
+    "vs_gemm_split_plan": [_I, _I, _I, _I, _P],
     "vs_layernorm_modulate": [_P, _LL, _P, _LL, _I, _I, _I, _P, _P, _LL, _P, _P, _F, _P],
     "vs_rmsnorm_rope": [_P, _LL, _I, _I, _I, _P, _F, _P, _I, _I, _I, _I, _I, _I, _P],
     "vs_patchify": [_P, _P, _I, _I, _I, _I, _I, _P],

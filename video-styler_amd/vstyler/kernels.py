@@ -139,6 +139,13 @@ def attention_split_plan(batch, sq, skv, heads, cus):
     return tuple(out)
 
 
+def gemm_split_plan(m, n, k, cus):
+    """(whole-tile workgroups, split tail tiles, K pieces per tile, K per piece) of vs_gemm (256 schedule)."""
+    out = (ctypes.c_int * 4)()
+    _lib.check(_lib.load().vs_gemm_split_plan(m, n, k, cus, out))
+    return tuple(out)
+
+
 def layernorm_modulate(x, out, eps=1e-6, shift=None, scale=None, mod_bstride=0, rows_per_batch=0,
                        weight=None, bias=None):
     M, D, ldx = _rows(x, "x")

@@ -150,12 +150,16 @@ class DenoiseStepper:
     """Runs CFG denoising steps over device-resident state.  `step_fn(t_buf, d_buf)` enqueues one
     whole step (model_fn + fused CFG/Euler) reading the bf16 timestep and the fp32 dsigma from the
     two device slots.  The first call runs eagerly (sizing every Workspace buffer); the step is then
-    captured once into a hipGraph and every later call refreshes the two slots and replays it."""
+    captured once into a hipGraph and every later call refreshes the two slots and replays it.
+    The eager step and the capture run on one dedicated stream, so the split-tail workspaces that
+    libvstyler keeps per (device, stream) and allocates in the eager step are the ones the captured
+    launches use (a capture on a fresh stream could not allocate them and would launch unsplit)."""
 
     def __init__(self, step_fn, timesteps_bf16, dsigmas_f32, use_graph=True, on_replay=None):
         self.step_fn, self.ts, self.ds = step_fn, timesteps_bf16, dsigmas_f32
         self.t_buf, self.d_buf = timesteps_bf16[0:1].clone(), dsigmas_f32[0:1].clone()
         self.use_graph, self.graph, self.on_replay = use_graph, None, on_replay
+        self.stream = torch.cuda.Stream(device=self.t_buf.device) if use_graph else None
 
     def __call__(self, i):
         self.t_buf.copy_(self.ts[i:i + 1])
@@ -165,13 +169,19 @@ class DenoiseStepper:
             if self.on_replay is not None:
                 self.on_replay()
             return
-        self.step_fn(self.t_buf, self.d_buf)
-        if self.use_graph:
+        if not self.use_graph:
+            self.step_fn(self.t_buf, self.d_buf)
+            return
+        cur = torch.cuda.current_stream(self.t_buf.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            self.step_fn(self.t_buf, self.d_buf)
             self.capture()
+        cur.wait_stream(self.stream)
 
     def capture(self):
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, stream=self.stream):
             self.step_fn(self.t_buf, self.d_buf)
         self.graph = g
 
