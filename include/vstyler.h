@@ -6,9 +6,9 @@
  * stream-ordered and graph-capturable; pointers are caller-owned device buffers
  * (bf16 unless stated, row-major), sizes/strides are in ELEMENTS.  No C++ types cross the ABI.
  *
- * Allocation: none per call.  vs_gemm and vs_attn_fwd keep one fp32 split-tail workspace per
- * (device, stream), allocated on first need outside graph capture (inside a capture without one
- * they launch unsplit); see vs_gemm_split_plan / vs_attn_split_plan.
+ * Allocation: none.  vs_gemm and vs_attn_fwd use a caller-owned fp32 split-tail workspace per
+ * (device, stream) bound with vs_split_workspace_bind; on a stream without one they launch
+ * unsplit (same results up to fp32 summation order).
  *
  * Error convention: every call returns 0 (VS_OK) or a VS_E_* code; shape/alignment violations are
  * rejected up front with VS_E_INVALID before anything is launched.  vs_strerror() names a code.
@@ -98,6 +98,15 @@ int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
  * out[3] = 64-key tiles per piece (out[1] = 0: no split).  Host-only, no device call.
  */
 int vs_attn_split_plan(int batch, int sq, int skv, int heads, int cus, int* out);
+
+/*
+ * Split-tail scratch (kind 0: vs_attn_fwd, 1: vs_gemm).  vs_split_workspace_bytes(kind) is the size
+ * that covers every plan; vs_split_workspace_bind(kind, ptr, bytes, stream) registers a caller-owned
+ * device buffer (16-B aligned) for launches of that kind on `stream` of the current device
+ * (ptr = NULL unbinds).  The buffer must stay valid while bound, including in captured graphs.
+ */
+long long vs_split_workspace_bytes(int kind);
+int vs_split_workspace_bind(int kind, void* ptr, long long bytes, void* stream);
 
 /*
  * out = bf16(LN(x)) [affine: weight/bias] then, if shift/scale given, modulate:

@@ -484,8 +484,8 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 // attention: 9280 items = 36.25 rounds on 256 CUs; under Ulysses SP=8 1160 = 4.53).  The last
 // n % CUs items instead run as nsplit key ranges each, chosen to minimise the tail's length in
 // item units (ceil(tail * nsplit / CUs) / nsplit), then one combine launch.  Partials live in a
-// per-(device, stream) workspace allocated once, outside any graph capture (graph capture without it
-// falls back to the unsplit grid).
+// caller-bound per-(device, stream) workspace (vs_split_workspace_bind; without one the grid runs
+// unsplit).
 constexpr int MAX_PIECES = 1024;
 struct SplitPlan { int nmain = 0, ntail = 0, nsplit = 1, piece_tiles = 0; };
 
@@ -554,7 +554,7 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
     SplitPlan sp = plan_split(nwg, (skv + BKV - 1) / BKV, vs_cus_for_split("VS_ATTN_NO_SPLIT"));
     float* part = nullptr;
     if (sp.ntail) {
-        part = vs_split_workspace(0, (size_t)MAX_PIECES * BQ * PROW * sizeof(float), (hipStream_t)stream);
+        part = vs_split_workspace(0, (size_t)sp.ntail * sp.nsplit * BQ * PROW * sizeof(float), (hipStream_t)stream);
         if (!part) sp = SplitPlan{(int)nwg, 0, 1, 0};
     }
     const long long grid = (long long)sp.nmain + (long long)sp.ntail * sp.nsplit;
@@ -580,5 +580,23 @@ extern "C" int vs_attn_split_plan(int batch, int sq, int skv, int heads, int cus
     out[1] = p.ntail;
     out[2] = p.nsplit;
     out[3] = p.piece_tiles;
+    return VS_OK;
+}
+
+extern "C" long long vs_split_workspace_bytes(int kind) {
+    if (kind == 0) return (long long)MAX_PIECES * BQ * PROW * (long long)sizeof(float);
+    if (kind == 1) return vs_gemm_split_workspace_bytes_impl();
+    return -1;
+}
+
+extern "C" int vs_split_workspace_bind(int kind, void* ptr, long long bytes, void* stream) {
+    if ((kind != 0 && kind != 1) || bytes < 0 || (ptr && ((uintptr_t)ptr & 15))) return VS_E_INVALID;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return VS_E_LAUNCH;
+    std::mutex* mu;
+    auto& reg = vs_ws_registry(mu);
+    std::lock_guard<std::mutex> lock(*mu);
+    if (!ptr) reg.erase({kind, dev, (hipStream_t)stream});
+    else reg[{kind, dev, (hipStream_t)stream}] = VsWs{(float*)ptr, bytes};
     return VS_OK;
 }

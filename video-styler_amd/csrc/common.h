@@ -74,24 +74,25 @@ inline int vs_cus_for_split(const char* env_off) {
     return n;
 }
 
-// One fp32 workspace per (tag, device, stream), allocated once with its fixed size: launches on
-// concurrent streams never share partials, and none is allocated while `stream` is being captured
-// into a graph (the caller then launches without a split).  nullptr when unavailable.
-inline float* vs_split_workspace(int tag, size_t bytes, hipStream_t stream) {
+// Split-tail scratch is caller-owned (the library never allocates): the host binds one fp32
+// workspace per (kind, device, stream) with vs_split_workspace_bind; a launch on a stream without
+// one runs unsplit.  kind 0: attention, 1: GEMM.
+struct VsWs { float* ptr; long long bytes; };
+inline std::map<std::tuple<int, int, hipStream_t>, VsWs>& vs_ws_registry(std::mutex*& mu) {
+    static std::mutex m;
+    static std::map<std::tuple<int, int, hipStream_t>, VsWs> reg;
+    mu = &m;
+    return reg;
+}
+inline float* vs_split_workspace(int kind, size_t bytes, hipStream_t stream) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    static std::mutex mu;
-    static std::map<std::tuple<int, int, hipStream_t>, float*> ws;
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = ws.find({tag, dev, stream});
-    if (it != ws.end()) return it->second;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    void* ptr = nullptr;
-    if (hipMalloc(&ptr, bytes) != hipSuccess) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    ws[{tag, dev, stream}] = (float*)ptr;
-    return (float*)ptr;
+    std::mutex* mu;
+    auto& reg = vs_ws_registry(mu);
+    std::lock_guard<std::mutex> lock(*mu);
+    auto it = reg.find({kind, dev, stream});
+    if (it == reg.end() || it->second.bytes < (long long)bytes) return nullptr;
+    return it->second.ptr;
 }
+
+long long vs_gemm_split_workspace_bytes_impl();   // gemm.hip

@@ -876,9 +876,9 @@ extern "C" int vs_debug_gemm_stamps(unsigned long long* host_out) {
 // Split tail.  One 256x256 workgroup fills a CU, so a grid of T tiles runs in ceil(T / CUs)
 // rounds and the last, partial one leaves CUs idle: the 14B N=5120 GEMMs on 2 x 29640 tokens are
 // 4640 tiles = 18.1 rounds on 256 CUs, and under Ulysses SP=8 (7410 rows) 580 tiles = 2.27.  The
-// last T % CUs tiles instead run as ksplit K ranges each (fp32 partial tiles in a per-(device,
-// stream) workspace, then one combine launch that applies the epilogue), ksplit chosen by the
-// measured cost model below.
+// last T % CUs tiles instead run as ksplit K ranges each (fp32 partial tiles in a caller-bound
+// per-(device, stream) workspace, then one combine launch that applies the epilogue), ksplit
+// chosen by the measured cost model below.
 constexpr int MAX_SPLIT_PIECES = 512;        // 512 x 256 KB fp32 partial tiles
 struct KSplit { int nmain = 0, ntail = 0, ksplit = 1, piece_k = 0; };
 
@@ -993,7 +993,7 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
                        : plan_ksplit(tm * tn, k / HK, vs_cus_for_split("VS_GEMM_NO_SPLIT"));
         float* part = nullptr;
         if (sp.ntail) {
-            part = vs_split_workspace(1, (size_t)MAX_SPLIT_PIECES * BT * BT * sizeof(float), (hipStream_t)stream);
+            part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
             if (!part) sp = KSplit{tm * tn, 0, 1, 0};
         }
         const unsigned grid = (unsigned)(sp.nmain + sp.ntail * sp.ksplit);
@@ -1086,3 +1086,5 @@ extern "C" int vs_gemm_split_plan(int m, int n, int k, int cus, int* out) {
     out[3] = p.piece_k;
     return VS_OK;
 }
+
+long long vs_gemm_split_workspace_bytes_impl() { return (long long)MAX_SPLIT_PIECES * BT * BT * (long long)sizeof(float); }

@@ -60,6 +60,8 @@ SIGNATURES = {
                     _F, _P],
     "vs_attn_split_plan": [_I, _I, _I, _I, _I, _P],
     "vs_gemm_split_plan": [_I, _I, _I, _I, _P],
+    "vs_split_workspace_bytes": [_I],
+    "vs_split_workspace_bind": [_I, _P, _LL, _P],
     "vs_layernorm_modulate": [_P, _LL, _P, _LL, _I, _I, _I, _P, _P, _LL, _P, _P, _F, _P],
     "vs_rmsnorm_rope": [_P, _LL, _I, _I, _I, _P, _F, _P, _I, _I, _I, _I, _I, _I, _P],
     "vs_patchify": [_P, _P, _I, _I, _I, _I, _I, _P],
@@ -87,7 +89,7 @@ SIGNATURES = {
     "vs_vae_blend_finish": [_P, _P, _P, _I, _LL, _I, _P],
     "vs_vae_copy_frames": [_P, _LL, _P, _LL, _I, _LL, _P],
 }
-_RESTYPES = {"vs_strerror": ctypes.c_char_p}
+_RESTYPES = {"vs_strerror": ctypes.c_char_p, "vs_split_workspace_bytes": ctypes.c_longlong}
 
 _lib = None
 

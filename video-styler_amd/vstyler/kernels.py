@@ -17,6 +17,24 @@ def _stream(t):
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+_SPLIT_WS = {}
+
+
+def _split_ws(kind, t):
+    """Bind the split-tail workspace of `kind` (0 attention, 1 GEMM) for the current stream of t's
+    device, once, from the torch allocator (vs_split_workspace_bind: the library never allocates).
+    Not inside a graph capture: a stream first seen while capturing launches unsplit."""
+    stream = _stream(t)
+    key = (kind, t.device.index, stream)
+    if key in _SPLIT_WS or torch.cuda.is_current_stream_capturing():
+        return
+    lib = _lib.load()
+    nbytes = lib.vs_split_workspace_bytes(kind)
+    buf = torch.empty(nbytes, dtype=torch.uint8, device=t.device)
+    _lib.check(lib.vs_split_workspace_bind(kind, buf.data_ptr(), nbytes, stream))
+    _SPLIT_WS[key] = buf
+
+
 def _req(t, name):
     if t.dtype != BF16:
         raise ValueError(f"{name}: expected bfloat16, got {t.dtype}")
@@ -78,6 +96,8 @@ def gemm(a, w, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, g
     if a2 is not None:
         _, k2, lda2 = _rows(a2, "a2")
         _, _, ldw2 = _rows(w2, "w2")
+    if k2 == 0:
+        _split_ws(1, a)
     _lib.check(_lib.load().vs_gemm(a.data_ptr(), lda, w.data_ptr(), ldw, out.data_ptr(), ldc, M, N, K,
                                    int(epilogue), ep, _ptr(a2), lda2, _ptr(w2), ldw2, k2, _stream(a)))
     return out
@@ -126,6 +146,7 @@ def attention(q, k, v, out, num_heads, batch, scale=None):
     hd = 128
     if scale is None:
         scale = hd ** -0.5
+    _split_ws(0, q)
     _lib.check(_lib.load().vs_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), batch, sq,
                                        skv, num_heads, hd, ldq, ldk, ldv, ldo, sq * ldq, skv * ldk,
                                        skv * ldv, sq * ldo, float(scale), _stream(q)))
