@@ -121,6 +121,50 @@ def test_gemm_split_tail_exact(K, monkeypatch):
     monkeypatch.delenv("VS_GEMM_NO_SPLIT", raising=False)
 
 
+def test_gemm_hipblaslt_route_exact(K, monkeypatch):
+    """vs_gemm's hipBLASLt route (bf16(A W^T + bias) by hipBLASLt, then gemm_epi_apply) against the
+    MFMA kernels on integer operands: every fp32 sum is exact, so each epilogue (bias, GELU, SiLU,
+    gate-residual with hint, residual) must agree bit for bit -- the route keeps the reference's
+    rounding points."""
+    M, N, Kd = 4452, 4000, 4160
+    g = torch.Generator(device="cuda").manual_seed(81)
+    a = torch.randint(-3, 4, (M, Kd), device="cuda", generator=g).to(BF16)
+    w = torch.randint(-3, 4, (N, Kd), device="cuda", generator=g).to(BF16)
+    b = torch.randint(-8, 9, (N,), device="cuda", generator=g).to(BF16)
+    res = torch.randn(M, N, device="cuda", generator=g).to(BF16)
+    gate = (0.25 * torch.randn(2, N, device="cuda", generator=g)).to(BF16)
+
+    def run(backend):
+        monkeypatch.setenv("VS_GEMM_BACKEND", backend)
+        outs = []
+        for epi in (K.VS_EPI_BIAS, K.VS_EPI_GELU, K.VS_EPI_SILU):
+            y = torch.empty(M, N, dtype=BF16, device="cuda")
+            K.gemm(a, w, y, epilogue=epi, bias=b)
+            outs.append(y)
+        x = res.clone()
+        K.gemm(a, w, x, epilogue=K.VS_EPI_GATE_RES, bias=b, residual=x, gate=gate, gate_bstride=N,
+               rows_per_batch=M // 2 + 1, hint=res, hint_scale=0.5)
+        outs.append(x)
+        x = res.clone()
+        K.gemm(a, w, x, epilogue=K.VS_EPI_RES, residual=x, alpha=0.125)
+        outs.append(x)
+        torch.cuda.synchronize()
+        return outs
+    lt, own = run("lt"), run("vstyler")
+    monkeypatch.delenv("VS_GEMM_BACKEND")
+    assert torch.equal(lt[0], (a.float() @ w.float().t() + b.float()).to(BF16))
+    for i, (x, y) in enumerate(zip(lt, own)):
+        assert torch.equal(x, y), i
+    # random operands: the routes differ only in fp32 summation order
+    a = torch.randn(M, Kd, device="cuda", generator=g).to(BF16)
+    w = (0.05 * torch.randn(N, Kd, device="cuda", generator=g)).to(BF16)
+    lt, own = run("lt"), run("vstyler")
+    monkeypatch.delenv("VS_GEMM_BACKEND")
+    for x, y in zip(lt, own):
+        rel = ((x.float() - y.float()).norm() / y.float().norm()).item()
+        assert rel < 2e-3, rel
+
+
 def test_gemm_lora_second_phase(K):
     M, N, Kd, r = 200, 320, 256, 128
     x, w, b = rnd(M, Kd, seed=11), rnd(N, Kd, scale=0.05, seed=12), rnd(N, scale=0.1, seed=13)

@@ -586,11 +586,12 @@ extern "C" int vs_attn_split_plan(int batch, int sq, int skv, int heads, int cus
 extern "C" long long vs_split_workspace_bytes(int kind) {
     if (kind == 0) return (long long)MAX_PIECES * BQ * PROW * (long long)sizeof(float);
     if (kind == 1) return vs_gemm_split_workspace_bytes_impl();
-    return -1;
+    if (kind == 2) return 128LL << 20;          // hipBLASLt (stream-K partials)
+    return -1;                                  // kind 3: m * n * 2 bytes of the largest routed GEMM
 }
 
 extern "C" int vs_split_workspace_bind(int kind, void* ptr, long long bytes, void* stream) {
-    if ((kind != 0 && kind != 1) || bytes < 0 || (ptr && ((uintptr_t)ptr & 15))) return VS_E_INVALID;
+    if (kind < 0 || kind > 3 || bytes < 0 || (ptr && ((uintptr_t)ptr & 15))) return VS_E_INVALID;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return VS_E_LAUNCH;
     std::mutex* mu;

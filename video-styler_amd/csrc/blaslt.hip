@@ -1,0 +1,110 @@
+// hipBLASLt for the plain part of the block GEMMs (host code only).
+//
+// The task's rule for MI355X: hand-written MFMA kernels for fused hot ops, the vendor library for
+// plain library GEMMs.  Measured on MI355X (profiles/r1/gemm_backend_ab_*.log), hipBLASLt's
+// stream-K 256x256x64 kernels run the 14B block GEMMs at 1240-1500 TF/s where gemm_bf16_tn_256
+// reaches 1040-1210, so vs_gemm routes C = A W^T + bias to hipBLASLt (one bf16 rounding of
+// acc + bias, exactly the first rounding point of every vs_gemm epilogue) and finishes any
+// further epilogue (GELU, SiLU, gate-residual [+ VACE hint], residual) with gemm_epi_apply,
+// which continues from that rounded value with the same code as the fused epilogue -- so both
+// paths have the reference's rounding points and differ only in fp32 summation order.
+//
+// Column-major view: C[m][n] row-major is D = W^T(op T on the [k x n] col-major view of W[n][k])
+// times A (op N on the [k x m] col-major view of A[m][k]): D is n x m col-major with ld = ldc,
+// and the bias runs along D's rows (n), hipBLASLt's BIAS epilogue.
+#include "common.h"
+
+#include <hipblaslt/hipblaslt.h>
+
+namespace {
+
+struct LtKey {
+    int dev, m, n, k;
+    long long lda, ldw, ldc;
+    bool bias;
+    bool operator<(const LtKey& o) const {
+        return std::tie(dev, m, n, k, lda, ldw, ldc, bias) < std::tie(o.dev, o.m, o.n, o.k, o.lda, o.ldw, o.ldc, o.bias);
+    }
+};
+
+struct LtPlan {
+    hipblasLtMatmulDesc_t desc = nullptr;
+    hipblasLtMatrixLayout_t lw = nullptr, la = nullptr, lc = nullptr;
+    hipblasLtMatmulAlgo_t algo;
+    size_t ws_need = 0;
+    bool ok = false;
+};
+
+std::mutex g_mu;
+std::map<int, hipblasLtHandle_t> g_handles;
+std::map<LtKey, LtPlan> g_plans;
+
+hipblasLtHandle_t handle_for(int dev) {
+    auto it = g_handles.find(dev);
+    if (it != g_handles.end()) return it->second;
+    hipblasLtHandle_t h = nullptr;
+    if (hipblasLtCreate(&h) != HIPBLAS_STATUS_SUCCESS) h = nullptr;
+    g_handles[dev] = h;
+    return h;
+}
+
+// builds (once per shape) the descriptor, the layouts and the heuristic's first algorithm that
+// fits `ws_bytes` of workspace
+LtPlan* plan_for(const LtKey& key, size_t ws_bytes) {
+    auto it = g_plans.find(key);
+    if (it != g_plans.end()) return it->second.ok ? &it->second : nullptr;
+    LtPlan& p = g_plans[key];
+    hipblasLtHandle_t h = handle_for(key.dev);
+    if (!h) return nullptr;
+    if (hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return nullptr;
+    const hipblasOperation_t opT = HIPBLAS_OP_T, opN = HIPBLAS_OP_N;
+    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opT, sizeof(opT));
+    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opN, sizeof(opN));
+    if (key.bias) {
+        const hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_BIAS;
+        const hipDataType bt = HIP_R_16BF;
+        hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi));
+        hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
+    }
+    if (hipblasLtMatrixLayoutCreate(&p.lw, HIP_R_16BF, key.k, key.n, key.ldw) != HIPBLAS_STATUS_SUCCESS ||
+        hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, key.k, key.m, key.lda) != HIPBLAS_STATUS_SUCCESS ||
+        hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_16BF, key.n, key.m, key.ldc) != HIPBLAS_STATUS_SUCCESS)
+        return nullptr;
+    hipblasLtMatmulPreference_t pref = nullptr;
+    if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return nullptr;
+    const uint64_t wsb = ws_bytes;
+    hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
+    hipblasLtMatmulHeuristicResult_t res[1];
+    int found = 0;
+    const hipblasStatus_t st =
+        hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.lw, p.la, p.lc, p.lc, pref, 1, res, &found);
+    hipblasLtMatmulPreferenceDestroy(pref);
+    if (st != HIPBLAS_STATUS_SUCCESS || found < 1) return nullptr;
+    p.algo = res[0].algo;
+    p.ws_need = res[0].workspaceSize;
+    p.ok = true;
+    return &p;
+}
+
+}  // namespace
+
+// C[m][n] (ld ldc) = bf16(A W^T + bias) on `stream` with hipBLASLt; 0 on success, VS_E_UNSUPPORTED
+// when hipBLASLt has no algorithm for the shape or the bound workspace (kind 2) is too small.
+int vs_lt_gemm_bias(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc, int m,
+                    int n, int k, const void* bias, hipStream_t stream) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return VS_E_LAUNCH;
+    long long ws_bytes = 0;
+    float* ws = vs_bound_workspace(2, dev, stream, &ws_bytes);
+    if (!ws) return VS_E_UNSUPPORTED;
+    std::lock_guard<std::mutex> lock(g_mu);
+    const LtKey key{dev, m, n, k, lda, ldw, ldc, bias != nullptr};
+    LtPlan* p = plan_for(key, (size_t)ws_bytes);
+    if (!p || p->ws_need > (size_t)ws_bytes) return VS_E_UNSUPPORTED;
+    if (bias)
+        hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
+    const float alpha = 1.f, beta = 0.f;
+    const hipblasStatus_t st = hipblasLtMatmul(handle_for(dev), p->desc, &alpha, w, p->lw, a, p->la, &beta, c, p->lc,
+                                               c, p->lc, &p->algo, ws, (size_t)ws_bytes, stream);
+    return st == HIPBLAS_STATUS_SUCCESS ? VS_OK : VS_E_LAUNCH;
+}

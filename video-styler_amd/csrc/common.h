@@ -76,7 +76,8 @@ inline int vs_cus_for_split(const char* env_off) {
 
 // Split-tail scratch is caller-owned (the library never allocates): the host binds one fp32
 // workspace per (kind, device, stream) with vs_split_workspace_bind; a launch on a stream without
-// one runs unsplit.  kind 0: attention, 1: GEMM.
+// one runs unsplit.  kind 0: attention split tail, 1: GEMM split tail, 2: hipBLASLt workspace,
+// 3: bf16 staging for epilogues finished after a hipBLASLt GEMM (gate-residual / residual).
 struct VsWs { float* ptr; long long bytes; };
 inline std::map<std::tuple<int, int, hipStream_t>, VsWs>& vs_ws_registry(std::mutex*& mu) {
     static std::mutex m;
@@ -84,15 +85,23 @@ inline std::map<std::tuple<int, int, hipStream_t>, VsWs>& vs_ws_registry(std::mu
     mu = &m;
     return reg;
 }
-inline float* vs_split_workspace(int kind, size_t bytes, hipStream_t stream) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+inline float* vs_bound_workspace(int kind, int dev, hipStream_t stream, long long* bytes) {
     std::mutex* mu;
     auto& reg = vs_ws_registry(mu);
     std::lock_guard<std::mutex> lock(*mu);
     auto it = reg.find({kind, dev, stream});
-    if (it == reg.end() || it->second.bytes < (long long)bytes) return nullptr;
+    if (it == reg.end()) return nullptr;
+    if (bytes) *bytes = it->second.bytes;
     return it->second.ptr;
+}
+inline float* vs_split_workspace(int kind, size_t bytes, hipStream_t stream) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    long long have = 0;
+    float* p = vs_bound_workspace(kind, dev, stream, &have);
+    return (p && have >= (long long)bytes) ? p : nullptr;
 }
 
 long long vs_gemm_split_workspace_bytes_impl();   // gemm.hip
+int vs_lt_gemm_bias(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc, int m,
+                    int n, int k, const void* bias, hipStream_t stream);   // blaslt.hip

@@ -294,6 +294,20 @@ __global__ __launch_bounds__(256) void gemm_split_combine(const float* __restric
     epilogue_store(a, m, n, C, ldc, ep);
 }
 
+// Epilogue continuation after a hipBLASLt GEMM: y = bf16(acc + bias) is already materialised in
+// Y; feed it to the fused epilogue with no bias (rbf(y + 0) == y) so GELU / SiLU / gate-residual
+// [+ hint] / residual round exactly as in the fused kernels.  One thread per 4 columns.
+__global__ __launch_bounds__(256) void gemm_epi_apply(const bf16_t* Y, long long ldy, bf16_t* C, long long ldc,
+                                                      int M, int N, Epi ep) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int n4 = N / 4;
+    if (idx >= (long long)M * n4) return;
+    const int m = (int)(idx / n4), n = 4 * (int)(idx % n4);
+    float v[4];
+    load4(Y + (long long)m * ldy + n, v);
+    epilogue_store(f32x4_t{v[0], v[1], v[2], v[3]}, m, n, C, ldc, ep);
+}
+
 template <bool BUF>
 __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
     const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
@@ -909,6 +923,19 @@ KSplit plan_ksplit(int ntiles, int nh, int cus) {
     return p;
 }
 
+// Which GEMMs go to hipBLASLt (VS_GEMM_BACKEND=vstyler|lt overrides).  Measured per block GEMM
+// of the 14B model with its real epilogue (profiles/r1/gemm_backend_ab_r1g.log): at 2 x 29640 rows
+// (4640-13920 tiles of 256^2) hipBLASLt + epilogue pass is 1.14-1.35x the MFMA kernels on all six,
+// staged gate-residual / residual included; at the SP=8 row count (7410) it wins only the >= 1566-
+// tile GEMMs (qkv 1.12x, FFN-up 1.05x) and loses the 580-tile ones (0.85-0.97x).  So: hipBLASLt
+// when the grid holds >= 1024 tiles (4 full rounds on 256 CUs).
+static bool lt_route(int m, int n) {
+    const char* e = getenv("VS_GEMM_BACKEND");
+    const int mode = !e ? 2 : (e[0] == 'v' ? 0 : (e[0] == 'l' ? 1 : 2));   // 0 never, 1 always, 2 auto
+    if (mode != 2) return mode == 1;
+    return (long long)((m + 255) / 256) * ((n + 255) / 256) >= 1024;
+}
+
 static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n) {
     if (epilogue < VS_EPI_BIAS || epilogue > VS_EPI_RES) return VS_E_INVALID;
     ep = Epi{};
@@ -959,6 +986,28 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
     }
     const bool big = force ? force == 256
                           : k >= 4096 && (long long)((m + BT - 1) / BT) * ((n + BT - 1) / BT) >= 240;
+    if (big && k2 == 0 && lt_route(m, n)) {
+        // hipBLASLt for A W^T + bias, then the rest of the epilogue (see blaslt.hip).  Falls through
+        // to the MFMA kernels when no workspace is bound or hipBLASLt declines the shape.
+        const bool staged = epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES;
+        bf16_t* y = (bf16_t*)c;
+        long long ldy = ldc;
+        if (staged) {
+            y = (bf16_t*)vs_split_workspace(3, (size_t)m * n * 2, (hipStream_t)stream);
+            ldy = n;
+        }
+        if (y && vs_lt_gemm_bias(a, lda, w, ldw, y, ldy, m, n, k, ep.bias, (hipStream_t)stream) == VS_OK) {
+            if (epilogue != VS_EPI_BIAS) {
+                Epi e2 = ep;
+                e2.bias = nullptr;
+                const long long threads = (long long)m * (n / 4);
+                hipLaunchKernelGGL(gemm_epi_apply, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                                   (hipStream_t)stream, y, ldy, (bf16_t*)c, ldc, m, n, e2);
+                VS_CHECK_LAUNCH();
+            }
+            return VS_OK;
+        }
+    }
     if (big) {
         const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
         static int impl = -1;

@@ -20,18 +20,24 @@ def _stream(t):
 _SPLIT_WS = {}
 
 
-def _split_ws(kind, t):
-    """Bind the split-tail workspace of `kind` (0 attention, 1 GEMM) for the current stream of t's
-    device, once, from the torch allocator (vs_split_workspace_bind: the library never allocates).
-    Not inside a graph capture: a stream first seen while capturing launches unsplit."""
+def _split_ws(kind, t, nbytes=None):
+    """Bind library scratch of `kind` (0 attention split tail, 1 GEMM split tail, 2 hipBLASLt
+    workspace, 3 epilogue staging of `nbytes`) for the current stream of t's device from the torch
+    allocator (vs_split_workspace_bind: the library never allocates).  Re-bound larger when a
+    bigger one is needed; never inside a graph capture (the library then takes its fallback)."""
     stream = _stream(t)
     key = (kind, t.device.index, stream)
-    if key in _SPLIT_WS or torch.cuda.is_current_stream_capturing():
+    have = _SPLIT_WS.get(key)
+    if nbytes is None:
+        if have is not None:
+            return
+        nbytes = _lib.load().vs_split_workspace_bytes(kind)
+    elif have is not None and have.numel() >= nbytes:
         return
-    lib = _lib.load()
-    nbytes = lib.vs_split_workspace_bytes(kind)
+    if torch.cuda.is_current_stream_capturing():
+        return
     buf = torch.empty(nbytes, dtype=torch.uint8, device=t.device)
-    _lib.check(lib.vs_split_workspace_bind(kind, buf.data_ptr(), nbytes, stream))
+    _lib.check(_lib.load().vs_split_workspace_bind(kind, buf.data_ptr(), nbytes, stream))
     _SPLIT_WS[key] = buf
 
 
@@ -98,6 +104,9 @@ def gemm(a, w, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, g
         _, _, ldw2 = _rows(w2, "w2")
     if k2 == 0:
         _split_ws(1, a)
+        _split_ws(2, a)
+        if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES) and K >= 4096:
+            _split_ws(3, a, M * N * 2)       # staging for the hipBLASLt route (vs_gemm decides)
     _lib.check(_lib.load().vs_gemm(a.data_ptr(), lda, w.data_ptr(), ldw, out.data_ptr(), ldc, M, N, K,
                                    int(epilogue), ep, _ptr(a2), lda2, _ptr(w2), ldw2, k2, _stream(a)))
     return out
