@@ -55,6 +55,11 @@ typedef struct vs_epilogue {
  * (diffsynth/vram_management/layers.py:173-188) incl. the un-merged LoRA term out + x A^T B^T
  * (layers.py:180-182): pass A2 = alpha * x A^T (computed by a previous vs_gemm) and W2 = B.
  * K and K2 must be multiples of 64, lda/ldw/lda2/ldw2 multiples of 8, N a multiple of 4.
+ * Execution: grids of >= 1024 256x256 tiles without a LoRA phase run bf16(A W^T + bias) on
+ * hipBLASLt (needs a kind-2 workspace bound on the stream) and finish the epilogue with the same
+ * code as the fused kernels (gate-residual / residual stage y in a kind-3 buffer of M*N*2 bytes);
+ * otherwise, or when those are not bound, the MFMA kernels (with the kind-1 split tail).  Every
+ * route has the same rounding points; results differ only in fp32 summation order.
  */
 int vs_gemm(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc,
             int m, int n, int k, int epilogue, const vs_epilogue* epi,
@@ -100,8 +105,10 @@ int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
 int vs_attn_split_plan(int batch, int sq, int skv, int heads, int cus, int* out);
 
 /*
- * Split-tail scratch (kind 0: vs_attn_fwd, 1: vs_gemm).  vs_split_workspace_bytes(kind) is the size
- * that covers every plan; vs_split_workspace_bind(kind, ptr, bytes, stream) registers a caller-owned
+ * Library scratch (kind 0: vs_attn_fwd split tail, 1: vs_gemm split tail, 2: vs_gemm's hipBLASLt
+ * workspace, 3: vs_gemm epilogue staging, M*N*2 bytes of the largest staged GEMM).
+ * vs_split_workspace_bytes(kind) is the size that covers every plan of kinds 0-2 (-1 for kind 3);
+ * vs_split_workspace_bind(kind, ptr, bytes, stream) registers a caller-owned
  * device buffer (16-B aligned) for launches of that kind on `stream` of the current device
  * (ptr = NULL unbinds).  The buffer must stay valid while bound, including in captured graphs.
  */
