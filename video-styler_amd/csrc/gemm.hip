@@ -928,7 +928,8 @@ KSplit plan_ksplit(int ntiles, int nh, int cus) {
 // (4640-13920 tiles of 256^2) hipBLASLt + epilogue pass is 1.14-1.35x the MFMA kernels on all six,
 // staged gate-residual / residual included; at the SP=8 row count (7410) it wins only the >= 1566-
 // tile GEMMs (qkv 1.12x, FFN-up 1.05x) and loses the 580-tile ones (0.85-0.97x).  So: hipBLASLt
-// when the grid holds >= 1024 tiles (4 full rounds on 256 CUs).
+// when the grid holds >= 1024 tiles (4 full rounds on 256 CUs), at any K (the 1.3B model's K = 1536
+// GEMMs: 1217-1300 TF/s against 707-797 on the 128^2 kernel, profiles/r1/gemm_bench_r1f.log).
 static bool lt_route(int m, int n) {
     const char* e = getenv("VS_GEMM_BACKEND");
     const int mode = !e ? 2 : (e[0] == 'v' ? 0 : (e[0] == 'l' ? 1 : 2));   // 0 never, 1 always, 2 auto
@@ -986,7 +987,7 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
     }
     const bool big = force ? force == 256
                           : k >= 4096 && (long long)((m + BT - 1) / BT) * ((n + BT - 1) / BT) >= 240;
-    if (big && k2 == 0 && lt_route(m, n)) {
+    if (k2 == 0 && lt_route(m, n)) {
         // hipBLASLt for A W^T + bias, then the rest of the epilogue (see blaslt.hip).  Falls through
         // to the MFMA kernels when no workspace is bound or hipBLASLt declines the shape.
         const bool staged = epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES;

@@ -105,7 +105,7 @@ def gemm(a, w, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, g
     if k2 == 0:
         _split_ws(1, a)
         _split_ws(2, a)
-        if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES) and K >= 4096:
+        if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES) and ((M + 255) // 256) * ((N + 255) // 256) >= 1024:
             _split_ws(3, a, M * N * 2)       # staging for the hipBLASLt route (vs_gemm decides)
     _lib.check(_lib.load().vs_gemm(a.data_ptr(), lda, w.data_ptr(), ldw, out.data_ptr(), ldc, M, N, K,
                                    int(epilogue), ep, _ptr(a2), lda2, _ptr(w2), ldw2, k2, _stream(a)))
