@@ -201,6 +201,21 @@ def test_attention_online_rescale_spike(K):
     assert mx < 3e-2, mx
 
 
+def test_attention_overflow_spike(K):
+    """Scores that jump by far more than 128 in the exp2 domain (exp2 overflows to inf before the
+    exact path runs): in the first tile, in a later tile's first and second 32-key halves."""
+    B, S, H = 1, 512, 1
+    q, k, v = rnd(B, S, 128, seed=33), rnd(B, S, 128, seed=34), rnd(B, S, 128, seed=35)
+    for row, key in ((3, 10), (5, 300), (9, 360), (200, 511)):
+        q[0, row] = 6.0
+        k[0, key] = 6.0
+    ref = O.attention(q, k, v, H)
+    out = torch.empty(S, 128, dtype=BF16, device="cuda")
+    K.attention(q.cuda().view(S, 128), k.cuda().view(S, 128), v.cuda().view(S, 128), out, H, B)
+    mx, rl = err(out.view(B, S, 128), ref)
+    assert mx < 3e-2, mx
+
+
 def test_attention_rescale_many(K):
     """Exact-path (rescale) decisions in the middle of the key sweep for many rows: row 7's max is
     raised three times in three different tiles, other rows once each, at keys spread over the
