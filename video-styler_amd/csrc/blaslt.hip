@@ -16,6 +16,9 @@
 
 #include <hipblaslt/hipblaslt.h>
 
+#include <cstdlib>
+#include <vector>
+
 namespace {
 
 struct LtKey {
@@ -32,7 +35,9 @@ struct LtPlan {
     hipblasLtMatrixLayout_t lw = nullptr, la = nullptr, lc = nullptr;
     hipblasLtMatmulAlgo_t algo;
     size_t ws_need = 0;
-    bool ok = false;
+    bool ok = false, tuned = false;
+    int pick = 0;                                       // index of the algorithm in use in cand
+    std::vector<hipblasLtMatmulHeuristicResult_t> cand;
 };
 
 std::mutex g_mu;
@@ -74,16 +79,59 @@ LtPlan* plan_for(const LtKey& key, size_t ws_bytes) {
     if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return nullptr;
     const uint64_t wsb = ws_bytes;
     hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
-    hipblasLtMatmulHeuristicResult_t res[1];
+    constexpr int NCAND = 16;
+    hipblasLtMatmulHeuristicResult_t res[NCAND];
     int found = 0;
     const hipblasStatus_t st =
-        hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.lw, p.la, p.lc, p.lc, pref, 1, res, &found);
+        hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.lw, p.la, p.lc, p.lc, pref, NCAND, res, &found);
     hipblasLtMatmulPreferenceDestroy(pref);
     if (st != HIPBLAS_STATUS_SUCCESS || found < 1) return nullptr;
+    p.cand.assign(res, res + found);
     p.algo = res[0].algo;
     p.ws_need = res[0].workspaceSize;
     p.ok = true;
     return &p;
+}
+
+// Autotune (once per shape, on its first eager call): time every candidate of the heuristic's
+// list on the call's own operands and keep the fastest.  The heuristic's first pick is not the
+// fastest on every block shape (profiles/r1/gemm_lt_tune_*.log).  Skipped while the stream is
+// being captured into a graph (no host sync possible) and with VS_LT_TUNE=0.
+void autotune(LtPlan& p, hipblasLtHandle_t h, const void* a, const void* w, void* c, float* ws, size_t ws_bytes,
+              hipStream_t stream) {
+    p.tuned = true;
+    if (p.cand.size() < 2) return;
+    const char* env = std::getenv("VS_LT_TUNE");
+    if (env && env[0] == '0') return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess) return;
+    if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return; }
+    const float alpha = 1.f, beta = 0.f;
+    float best = 1e30f;
+    size_t bi = 0;
+    for (size_t i = 0; i < p.cand.size(); ++i) {
+        if (p.cand[i].workspaceSize > ws_bytes) continue;
+        auto run = [&]() {
+            return hipblasLtMatmul(h, p.desc, &alpha, w, p.lw, a, p.la, &beta, c, p.lc, c, p.lc, &p.cand[i].algo, ws,
+                                   ws_bytes, stream);
+        };
+        if (run() != HIPBLAS_STATUS_SUCCESS) continue;
+        (void)hipEventRecord(e0, stream);
+        bool ok = true;
+        for (int r = 0; r < 3 && ok; ++r) ok = run() == HIPBLAS_STATUS_SUCCESS;
+        (void)hipEventRecord(e1, stream);
+        if (!ok || hipEventSynchronize(e1) != hipSuccess) continue;
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        if (ms < best) { best = ms; bi = i; }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    p.algo = p.cand[bi].algo;
+    p.ws_need = p.cand[bi].workspaceSize;
+    p.pick = (int)bi;
 }
 
 }  // namespace
@@ -103,6 +151,7 @@ int vs_lt_gemm_bias(const void* a, long long lda, const void* w, long long ldw, 
     if (!p || p->ws_need > (size_t)ws_bytes) return VS_E_UNSUPPORTED;
     if (bias)
         hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
+    if (!p->tuned) autotune(*p, handle_for(dev), a, w, c, ws, (size_t)ws_bytes, stream);
     const float alpha = 1.f, beta = 0.f;
     const hipblasStatus_t st = hipblasLtMatmul(handle_for(dev), p->desc, &alpha, w, p->lw, a, p->la, &beta, c, p->lc,
                                                c, p->lc, &p->algo, ws, (size_t)ws_bytes, stream);

@@ -43,50 +43,67 @@ struct Epi {
 
 __device__ __forceinline__ int g_off(int row, int ch) { return row * 128 + 16 * (ch ^ (row & 7)); }
 
-__device__ __forceinline__ void load4(const bf16_t* p, float* v) {
-    const u32x2_t w = *reinterpret_cast<const u32x2_t*>(p);
-    v[0] = bflo(w[0]);
-    v[1] = bfhi(w[0]);
-    v[2] = bflo(w[1]);
-    v[3] = bfhi(w[1]);
+template <int W>
+__device__ __forceinline__ void loadw(const bf16_t* p, float* v) {
+    if constexpr (W == 4) {
+        const u32x2_t w = *reinterpret_cast<const u32x2_t*>(p);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) { v[2 * i] = bflo(w[i]); v[2 * i + 1] = bfhi(w[i]); }
+    } else {
+        const u32x4_t w = *reinterpret_cast<const u32x4_t*>(p);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { v[2 * i] = bflo(w[i]); v[2 * i + 1] = bfhi(w[i]); }
+    }
+}
+__device__ __forceinline__ void load4(const bf16_t* p, float* v) { loadw<4>(p, v); }
+
+// the op that follows each linear, on W consecutive columns of row m: y = bf16(acc + bias), then
+// GELU / SiLU / gate-residual [+ hint] / residual with the reference's bf16 rounding points
+template <int W>
+__device__ __forceinline__ void epilogue_store_w(const float* a, int m, int n, bf16_t* C, long long ldc,
+                                                 const Epi& ep) {
+    const int bidx = m / ep.rows_per_batch;
+    float bv[W] = {};
+    if (ep.bias) loadw<W>(ep.bias + n, bv);
+    float y[W];
+#pragma unroll
+    for (int e = 0; e < W; ++e) y[e] = rbf(a[e] + bv[e]);
+    if (ep.mode == VS_EPI_GELU) {
+#pragma unroll
+        for (int e = 0; e < W; ++e) y[e] = gelu_tanh_f(y[e]);
+    } else if (ep.mode == VS_EPI_SILU) {
+#pragma unroll
+        for (int e = 0; e < W; ++e) y[e] = silu_f(y[e]);
+    } else if (ep.mode == VS_EPI_GATE_RES) {
+        float rv[W], gv[W];
+        loadw<W>(ep.res + (long long)m * ep.ld_res + n, rv);
+        loadw<W>(ep.gate + (long long)bidx * ep.gate_bstride + n, gv);
+#pragma unroll
+        for (int e = 0; e < W; ++e) y[e] = rbf(rv[e] + rbf(gv[e] * y[e]));
+        if (ep.hint) {
+            float hv[W];
+            loadw<W>(ep.hint + (long long)m * ep.ld_hint + n, hv);
+#pragma unroll
+            for (int e = 0; e < W; ++e) y[e] = y[e] + rbf(hv[e] * ep.hint_scale);
+        }
+    } else if (ep.mode == VS_EPI_RES) {
+        float rv[W];
+        loadw<W>(ep.res + (long long)m * ep.ld_res + n, rv);
+#pragma unroll
+        for (int e = 0; e < W; ++e) y[e] = rv[e] + rbf(ep.alpha * y[e]);
+    }
+    if constexpr (W == 4) {
+        *reinterpret_cast<u32x2_t*>(C + (long long)m * ldc + n) = u32x2_t{pack2(y[0], y[1]), pack2(y[2], y[3])};
+    } else {
+        *reinterpret_cast<u32x4_t*>(C + (long long)m * ldc + n) =
+            u32x4_t{pack2(y[0], y[1]), pack2(y[2], y[3]), pack2(y[4], y[5]), pack2(y[6], y[7])};
+    }
 }
 
 __device__ __forceinline__ void epilogue_store(const f32x4_t& a, int m, int n, bf16_t* C, long long ldc,
                                                const Epi& ep) {
-    const int bidx = m / ep.rows_per_batch;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (ep.bias) load4(ep.bias + n, bv);
-    float y[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) y[e] = rbf(a[e] + bv[e]);
-    if (ep.mode == VS_EPI_GELU) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = gelu_tanh_f(y[e]);
-    } else if (ep.mode == VS_EPI_SILU) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = silu_f(y[e]);
-    } else if (ep.mode == VS_EPI_GATE_RES) {
-        float rv[4], gv[4];
-        load4(ep.res + (long long)m * ep.ld_res + n, rv);
-        load4(ep.gate + (long long)bidx * ep.gate_bstride + n, gv);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = rbf(rv[e] + rbf(gv[e] * y[e]));
-        if (ep.hint) {
-            float hv[4];
-            load4(ep.hint + (long long)m * ep.ld_hint + n, hv);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) y[e] = y[e] + rbf(hv[e] * ep.hint_scale);
-        }
-    } else if (ep.mode == VS_EPI_RES) {
-        float rv[4];
-        load4(ep.res + (long long)m * ep.ld_res + n, rv);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = rv[e] + rbf(ep.alpha * y[e]);
-    }
-    u32x2_t w;
-    w[0] = pack2(y[0], y[1]);
-    w[1] = pack2(y[2], y[3]);
-    *reinterpret_cast<u32x2_t*>(C + (long long)m * ldc + n) = w;
+    const float v[4] = {a[0], a[1], a[2], a[3]};
+    epilogue_store_w<4>(v, m, n, C, ldc, ep);
 }
 
 __global__ __launch_bounds__(NTHR, 2) void gemm_bf16_tn(
@@ -306,6 +323,18 @@ __global__ __launch_bounds__(256) void gemm_epi_apply(const bf16_t* Y, long long
     float v[4];
     load4(Y + (long long)m * ldy + n, v);
     epilogue_store(f32x4_t{v[0], v[1], v[2], v[3]}, m, n, C, ldc, ep);
+}
+
+// The same, 8 columns per thread with 16-B accesses and a (row, column-chunk) grid: no 64-bit
+// index division, one pass at the HBM rate (N % 8 == 0 and 16-B aligned rows; host-checked).
+__global__ __launch_bounds__(256) void gemm_epi_apply8(const bf16_t* Y, long long ldy, bf16_t* C, long long ldc,
+                                                       int N, Epi ep) {
+    const int m = blockIdx.x;
+    const int n = 8 * (blockIdx.y * 256 + threadIdx.x);
+    if (n >= N) return;
+    float v[8];
+    loadw<8>(Y + (long long)m * ldy + n, v);
+    epilogue_store_w<8>(v, m, n, C, ldc, ep);
 }
 
 template <bool BUF>
@@ -930,11 +959,16 @@ KSplit plan_ksplit(int ntiles, int nh, int cus) {
 // tile GEMMs (qkv 1.12x, FFN-up 1.05x) and loses the 580-tile ones (0.85-0.97x).  So: hipBLASLt
 // when the grid holds >= 1024 tiles (4 full rounds on 256 CUs), at any K (the 1.3B model's K = 1536
 // GEMMs: 1217-1300 TF/s against 707-797 on the 128^2 kernel, profiles/r1/gemm_bench_r1f.log).
-static bool lt_route(int m, int n) {
+// hipBLASLt (autotuned per shape, blaslt.hip) vs the 256^2 MFMA kernel with its split tail, measured
+// per 14B block GEMM (profiles/r1/gemm_lt_tune_r1i.log): hipBLASLt wins on every grid of >= 1024
+// 256^2 tiles, and on 512-1023-tile grids (the SP=8 row count) while K <= 8192; the K = 13824
+// FFN-down GEMM at that size stays on the MFMA kernel (0.926 vs 0.971 ms).
+static bool lt_route(int m, int n, int k) {
     const char* e = getenv("VS_GEMM_BACKEND");
     const int mode = !e ? 2 : (e[0] == 'v' ? 0 : (e[0] == 'l' ? 1 : 2));   // 0 never, 1 always, 2 auto
     if (mode != 2) return mode == 1;
-    return (long long)((m + 255) / 256) * ((n + 255) / 256) >= 1024;
+    const long long tiles = (long long)((m + 255) / 256) * ((n + 255) / 256);
+    return tiles >= 1024 || (tiles >= 512 && k <= 8192);
 }
 
 static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n) {
@@ -987,7 +1021,7 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
     }
     const bool big = force ? force == 256
                           : k >= 4096 && (long long)((m + BT - 1) / BT) * ((n + BT - 1) / BT) >= 240;
-    if (k2 == 0 && lt_route(m, n)) {
+    if (k2 == 0 && lt_route(m, n, k)) {
         // hipBLASLt for A W^T + bias, then the rest of the epilogue (see blaslt.hip).  Falls through
         // to the MFMA kernels when no workspace is bound or hipBLASLt declines the shape.
         const bool staged = epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES;
@@ -1001,9 +1035,18 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
             if (epilogue != VS_EPI_BIAS) {
                 Epi e2 = ep;
                 e2.bias = nullptr;
-                const long long threads = (long long)m * (n / 4);
-                hipLaunchKernelGGL(gemm_epi_apply, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
-                                   (hipStream_t)stream, y, ldy, (bf16_t*)c, ldc, m, n, e2);
+                const bool w8 = n % 8 == 0 && ldy % 8 == 0 && ldc % 8 == 0 && aligned16(y) && aligned16(c) &&
+                                (!e2.res || (e2.ld_res % 8 == 0 && aligned16(e2.res))) &&
+                                (!e2.gate || (e2.gate_bstride % 8 == 0 && aligned16(e2.gate))) &&
+                                (!e2.hint || (e2.ld_hint % 8 == 0 && aligned16(e2.hint)));
+                if (w8) {
+                    hipLaunchKernelGGL(gemm_epi_apply8, dim3((unsigned)m, (unsigned)((n / 8 + 255) / 256)), dim3(256),
+                                       0, (hipStream_t)stream, y, ldy, (bf16_t*)c, ldc, n, e2);
+                } else {
+                    const long long threads = (long long)m * (n / 4);
+                    hipLaunchKernelGGL(gemm_epi_apply, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                                       (hipStream_t)stream, y, ldy, (bf16_t*)c, ldc, m, n, e2);
+                }
                 VS_CHECK_LAUNCH();
             }
             return VS_OK;
