@@ -306,8 +306,9 @@ def main():
         "dtype": "fp8_e4m3 (block linears) + bf16 (attention, norms)" if args.config == "fp8" else "bf16",
         "data": "synthetic (random-init weights, seeded latents/contexts/VACE context)",
         "config": {"workload": f"Wan2.1-VACE-{args.model} {args.width}x{args.height}x{args.frames}: "
-                               f"{m['num_layers']} DiT + {len(m['vace_layers'])} VACE blocks, CFG 5.0 as one "
-                               f"batch-2 forward + Euler",
+                               f"{m['num_layers']} DiT + {len(m['vace_layers'])} VACE blocks, "
+                               + ("CFG 1.2 as one batch-2 forward + UniPC (config 5)" if args.config == "fp8"
+                                  else "CFG 5.0 as one batch-2 forward + Euler"),
                    "model": f"Wan2.1-VACE-{args.model}", "global_batch": 1, "seq_len": S,
                    "latent_shape": [1, 16, T, Hl, Wl], "parallelism": f"sp{world}" if world > 1 else "single",
                    "lora": "merged (zero runtime cost, as the reference's GeneralLoRALoader)",

@@ -25,8 +25,10 @@ struct LtKey {
     int dev, m, n, k;
     long long lda, ldw, ldc;
     bool bias;
+    bool fp8;          // e4m3fn operands with a per-row (per-token) fp32 scale on A
     bool operator<(const LtKey& o) const {
-        return std::tie(dev, m, n, k, lda, ldw, ldc, bias) < std::tie(o.dev, o.m, o.n, o.k, o.lda, o.ldw, o.ldc, o.bias);
+        return std::tie(dev, m, n, k, lda, ldw, ldc, bias, fp8) <
+               std::tie(o.dev, o.m, o.n, o.k, o.lda, o.ldw, o.ldc, o.bias, o.fp8);
     }
 };
 
@@ -71,8 +73,15 @@ LtPlan* plan_for(const LtKey& key, size_t ws_bytes) {
         hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi));
         hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
     }
-    if (hipblasLtMatrixLayoutCreate(&p.lw, HIP_R_16BF, key.k, key.n, key.ldw) != HIPBLAS_STATUS_SUCCESS ||
-        hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, key.k, key.m, key.lda) != HIPBLAS_STATUS_SUCCESS ||
+    const hipDataType in_t = key.fp8 ? HIP_R_8F_E4M3 : HIP_R_16BF;
+    if (key.fp8) {
+        // fp8_linear (layers.py:115-151): (x8 . w8^T) * scale_x[row] + bias, one bf16 rounding; the
+        // token axis is D's column axis here, hipBLASLt's "B" outer scale vector
+        const hipblasLtMatmulMatrixScale_t vec = HIPBLASLT_MATMUL_MATRIX_SCALE_OUTER_VEC_32F;
+        hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_B_SCALE_MODE, &vec, sizeof(vec));
+    }
+    if (hipblasLtMatrixLayoutCreate(&p.lw, in_t, key.k, key.n, key.ldw) != HIPBLAS_STATUS_SUCCESS ||
+        hipblasLtMatrixLayoutCreate(&p.la, in_t, key.k, key.m, key.lda) != HIPBLAS_STATUS_SUCCESS ||
         hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_16BF, key.n, key.m, key.ldc) != HIPBLAS_STATUS_SUCCESS)
         return nullptr;
     hipblasLtMatmulPreference_t pref = nullptr;
@@ -109,7 +118,7 @@ void autotune(LtPlan& p, hipblasLtHandle_t h, const void* a, const void* w, void
     if (hipEventCreate(&e0) != hipSuccess) return;
     if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return; }
     const float alpha = 1.f, beta = 0.f;
-    float best = 1e30f;
+    float best = 1e30f, first = 1e30f;
     size_t bi = 0;
     for (size_t i = 0; i < p.cand.size(); ++i) {
         if (p.cand[i].workspaceSize > ws_bytes) continue;
@@ -125,8 +134,13 @@ void autotune(LtPlan& p, hipblasLtHandle_t h, const void* a, const void* w, void
         if (!ok || hipEventSynchronize(e1) != hipSuccess) continue;
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, e0, e1);
+        if (i == 0) first = ms;
         if (ms < best) { best = ms; bi = i; }
     }
+    // keep the heuristic's (deterministic) first pick unless another candidate is clearly faster,
+    // so that timing noise between near-equal candidates does not change the algorithm -- and the
+    // fp32 summation order -- from run to run or rank to rank
+    if (best > 0.97f * first) bi = 0;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     p.algo = p.cand[bi].algo;
@@ -136,24 +150,39 @@ void autotune(LtPlan& p, hipblasLtHandle_t h, const void* a, const void* w, void
 
 }  // namespace
 
-// C[m][n] (ld ldc) = bf16(A W^T + bias) on `stream` with hipBLASLt; 0 on success, VS_E_UNSUPPORTED
-// when hipBLASLt has no algorithm for the shape or the bound workspace (kind 2) is too small.
-int vs_lt_gemm_bias(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc, int m,
-                    int n, int k, const void* bias, hipStream_t stream) {
+namespace {
+int lt_gemm(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc, int m, int n, int k,
+            const void* bias, const float* scale_a, hipStream_t stream) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return VS_E_LAUNCH;
     long long ws_bytes = 0;
     float* ws = vs_bound_workspace(2, dev, stream, &ws_bytes);
     if (!ws) return VS_E_UNSUPPORTED;
     std::lock_guard<std::mutex> lock(g_mu);
-    const LtKey key{dev, m, n, k, lda, ldw, ldc, bias != nullptr};
+    const LtKey key{dev, m, n, k, lda, ldw, ldc, bias != nullptr, scale_a != nullptr};
     LtPlan* p = plan_for(key, (size_t)ws_bytes);
     if (!p || p->ws_need > (size_t)ws_bytes) return VS_E_UNSUPPORTED;
     if (bias)
         hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
+    if (scale_a)
+        hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_B_SCALE_POINTER, &scale_a, sizeof(scale_a));
     if (!p->tuned) autotune(*p, handle_for(dev), a, w, c, ws, (size_t)ws_bytes, stream);
     const float alpha = 1.f, beta = 0.f;
     const hipblasStatus_t st = hipblasLtMatmul(handle_for(dev), p->desc, &alpha, w, p->lw, a, p->la, &beta, c, p->lc,
                                                c, p->lc, &p->algo, ws, (size_t)ws_bytes, stream);
     return st == HIPBLAS_STATUS_SUCCESS ? VS_OK : VS_E_LAUNCH;
+}
+}  // namespace
+
+// C[m][n] (ld ldc) = bf16(A W^T + bias) on `stream` with hipBLASLt; 0 on success, VS_E_UNSUPPORTED
+// when hipBLASLt has no algorithm for the shape or the bound workspace (kind 2) is too small.
+int vs_lt_gemm_bias(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc, int m,
+                    int n, int k, const void* bias, hipStream_t stream) {
+    return lt_gemm(a, lda, w, ldw, c, ldc, m, n, k, bias, nullptr, stream);
+}
+
+// C[m][n] = bf16((A8 W8^T) * scale_a[row] + bias), e4m3fn operands (fp8_linear); same contract.
+int vs_lt_gemm_fp8(const void* a8, long long lda, const float* scale_a, const void* w8, long long ldw, void* c,
+                   long long ldc, int m, int n, int k, const void* bias, hipStream_t stream) {
+    return lt_gemm(a8, lda, w8, ldw, c, ldc, m, n, k, bias, scale_a, stream);
 }

@@ -971,6 +971,40 @@ static bool lt_route(int m, int n, int k) {
     return tiles >= 1024 || (tiles >= 512 && k <= 8192);
 }
 
+// hipBLASLt for bf16(A W^T [* scale] + bias) (gemm(y, ldy)), then the rest of the epilogue with
+// the fused kernels' code (see blaslt.hip).  false: no workspace bound or hipBLASLt declined the
+// shape -- the caller falls through to the MFMA kernels.
+template <class Gemm>
+static bool lt_with_epilogue(void* c, long long ldc, int m, int n, int epilogue, const Epi& ep, hipStream_t stream,
+                             Gemm gemm) {
+    const bool staged = epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES;
+    bf16_t* y = (bf16_t*)c;
+    long long ldy = ldc;
+    if (staged) {
+        y = (bf16_t*)vs_split_workspace(3, (size_t)m * n * 2, stream);
+        ldy = n;
+    }
+    if (!y || gemm((void*)y, ldy) != VS_OK) return false;
+    if (epilogue != VS_EPI_BIAS) {
+        Epi e2 = ep;
+        e2.bias = nullptr;
+        const bool w8 = n % 8 == 0 && ldy % 8 == 0 && ldc % 8 == 0 && aligned16(y) && aligned16(c) &&
+                        (!e2.res || (e2.ld_res % 8 == 0 && aligned16(e2.res))) &&
+                        (!e2.gate || (e2.gate_bstride % 8 == 0 && aligned16(e2.gate))) &&
+                        (!e2.hint || (e2.ld_hint % 8 == 0 && aligned16(e2.hint)));
+        if (w8) {
+            hipLaunchKernelGGL(gemm_epi_apply8, dim3((unsigned)m, (unsigned)((n / 8 + 255) / 256)), dim3(256), 0,
+                               stream, y, ldy, (bf16_t*)c, ldc, n, e2);
+        } else {
+            const long long threads = (long long)m * (n / 4);
+            hipLaunchKernelGGL(gemm_epi_apply, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, y, ldy,
+                               (bf16_t*)c, ldc, m, n, e2);
+        }
+        if (hipGetLastError() != hipSuccess) return false;
+    }
+    return true;
+}
+
 static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n) {
     if (epilogue < VS_EPI_BIAS || epilogue > VS_EPI_RES) return VS_E_INVALID;
     ep = Epi{};
@@ -1021,37 +1055,11 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
     }
     const bool big = force ? force == 256
                           : k >= 4096 && (long long)((m + BT - 1) / BT) * ((n + BT - 1) / BT) >= 240;
-    if (k2 == 0 && lt_route(m, n, k)) {
-        // hipBLASLt for A W^T + bias, then the rest of the epilogue (see blaslt.hip).  Falls through
-        // to the MFMA kernels when no workspace is bound or hipBLASLt declines the shape.
-        const bool staged = epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES;
-        bf16_t* y = (bf16_t*)c;
-        long long ldy = ldc;
-        if (staged) {
-            y = (bf16_t*)vs_split_workspace(3, (size_t)m * n * 2, (hipStream_t)stream);
-            ldy = n;
-        }
-        if (y && vs_lt_gemm_bias(a, lda, w, ldw, y, ldy, m, n, k, ep.bias, (hipStream_t)stream) == VS_OK) {
-            if (epilogue != VS_EPI_BIAS) {
-                Epi e2 = ep;
-                e2.bias = nullptr;
-                const bool w8 = n % 8 == 0 && ldy % 8 == 0 && ldc % 8 == 0 && aligned16(y) && aligned16(c) &&
-                                (!e2.res || (e2.ld_res % 8 == 0 && aligned16(e2.res))) &&
-                                (!e2.gate || (e2.gate_bstride % 8 == 0 && aligned16(e2.gate))) &&
-                                (!e2.hint || (e2.ld_hint % 8 == 0 && aligned16(e2.hint)));
-                if (w8) {
-                    hipLaunchKernelGGL(gemm_epi_apply8, dim3((unsigned)m, (unsigned)((n / 8 + 255) / 256)), dim3(256),
-                                       0, (hipStream_t)stream, y, ldy, (bf16_t*)c, ldc, n, e2);
-                } else {
-                    const long long threads = (long long)m * (n / 4);
-                    hipLaunchKernelGGL(gemm_epi_apply, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
-                                       (hipStream_t)stream, y, ldy, (bf16_t*)c, ldc, m, n, e2);
-                }
-                VS_CHECK_LAUNCH();
-            }
-            return VS_OK;
-        }
-    }
+    if (k2 == 0 && lt_route(m, n, k) &&
+        lt_with_epilogue(c, ldc, m, n, epilogue, ep, (hipStream_t)stream, [&](void* y, long long ldy) {
+            return vs_lt_gemm_bias(a, lda, w, ldw, y, ldy, m, n, k, ep.bias, (hipStream_t)stream);
+        }))
+        return VS_OK;
     if (big) {
         const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
         static int impl = -1;
@@ -1137,6 +1145,16 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
     Epi ep;
     const int rc = fill_epi(ep, epilogue, epi, m, n);
     if (rc) return rc;
+    // hipBLASLt fp8 (OCP e4m3 operands, per-token fp32 scale vector as hipBLASLt's outer B scale)
+    // + the epilogue pass: 1.3-1.6x the fp8 MFMA kernel on every 14B block shape at SP=1 and SP=8
+    // and bit-identical to it, epilogues included (profiles/r1/gemm_fp8_lt_r1j.log).
+    // VS_FP8_BACKEND=vstyler forces the MFMA kernel, which also runs when no workspace is bound.
+    const char* fb = getenv("VS_FP8_BACKEND");
+    if (!(fb && fb[0] == 'v') &&
+        lt_with_epilogue(c, ldc, m, n, epilogue, ep, (hipStream_t)stream, [&](void* y, long long ldy) {
+            return vs_lt_gemm_fp8(a8, lda, scale_a, w8, ldw, y, ldy, m, n, k, ep.bias, (hipStream_t)stream);
+        }))
+        return VS_OK;
     const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
     static bool attr = false;
     if (!attr) {

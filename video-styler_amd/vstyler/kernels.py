@@ -3,6 +3,7 @@
 PyTorch is used only for device memory and streams; every computation below is a kernel of
 libvstyler.so.  Wrappers validate dtype/device/layout and raise ValueError before launching.
 """
+import os
 import ctypes
 
 import torch
@@ -105,7 +106,7 @@ def gemm(a, w, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, g
     if k2 == 0:
         _split_ws(1, a)
         _split_ws(2, a)
-        if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES) and ((M + 255) // 256) * ((N + 255) // 256) >= 1024:
+        if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES) and _lt_route(M, N, K):
             _split_ws(3, a, M * N * 2)       # staging for the hipBLASLt route (vs_gemm decides)
     _lib.check(_lib.load().vs_gemm(a.data_ptr(), lda, w.data_ptr(), ldw, out.data_ptr(), ldc, M, N, K,
                                    int(epilogue), ep, _ptr(a2), lda2, _ptr(w2), ldw2, k2, _stream(a)))
@@ -129,6 +130,18 @@ def quant_fp8_rows(x, x8, scale):
     return x8, scale
 
 
+def _lt_route(M, N, K):
+    """Mirror of vs_gemm's routing rule (gemm.hip lt_route): grids of >= 1024 256x256 tiles, or
+    >= 512 with K <= 8192, go to hipBLASLt -- the shim binds the epilogue staging buffer for them."""
+    be = os.environ.get("VS_GEMM_BACKEND", "")
+    if be.startswith("v"):
+        return False
+    if be.startswith("l"):
+        return True
+    tiles = ((M + 255) // 256) * ((N + 255) // 256)
+    return tiles >= 1024 or (tiles >= 512 and K <= 8192)
+
+
 def gemm_fp8(a8, scale_a, w8, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, gate_bstride=0,
              hint=None, hint_scale=1.0, alpha=1.0, rows_per_batch=0):
     """out = epilogue(scale_a[m] * (a8 @ w8^T)) with e4m3 operands (see vs_gemm_fp8)."""
@@ -138,6 +151,10 @@ def gemm_fp8(a8, scale_a, w8, out, epilogue=VS_EPI_BIAS, bias=None, residual=Non
     if Kw != K or Mo != M or No != N or scale_a.dtype != torch.float32:
         raise ValueError(f"gemm_fp8 shape mismatch a8={tuple(a8.shape)} w8={tuple(w8.shape)} out={tuple(out.shape)}")
     ep = _epilogue(bias, residual, gate, gate_bstride, hint, hint_scale, alpha, rows_per_batch)
+    if not os.environ.get("VS_FP8_BACKEND", "").startswith("v"):      # hipBLASLt route (vs_gemm_fp8)
+        _split_ws(2, a8)
+        if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES):
+            _split_ws(3, a8, M * N * 2)
     _lib.check(_lib.load().vs_gemm_fp8(a8.data_ptr(), lda, scale_a.data_ptr(), w8.data_ptr(), ldw, out.data_ptr(),
                                        ldc, M, N, K, int(epilogue), ep, _stream(a8)))
     return out
