@@ -55,7 +55,7 @@ typedef struct vs_epilogue {
  * (diffsynth/vram_management/layers.py:173-188) incl. the un-merged LoRA term out + x A^T B^T
  * (layers.py:180-182): pass A2 = alpha * x A^T (computed by a previous vs_gemm) and W2 = B.
  * K and K2 must be multiples of 64, lda/ldw/lda2/ldw2 multiples of 8, N a multiple of 4.
- * Execution: grids of >= 1024 256x256 tiles (or >= 512 with K <= 8192) without a LoRA phase run
+ * Execution: grids of >= 1024 256x256 tiles (or >= 256 with K <= 8192) without a LoRA phase run
  * bf16(A W^T + bias) on hipBLASLt (needs a kind-2 workspace bound on the stream; the first eager
  * call of a shape times the heuristic's candidates and keeps the fastest, VS_LT_TUNE=0 disables)
  * and finish the epilogue with the same

@@ -14,7 +14,7 @@ def timed(fn, reps=5):
     return sorted(ts)[reps // 2]
 
 
-for M in (59280, 7410):
+for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
     for name, N, Kd, epi in (("qkv", 15360, 5120, K.VS_EPI_BIAS), ("o-proj", 5120, 5120, K.VS_EPI_GATE_RES),
                              ("cross-q", 5120, 5120, K.VS_EPI_BIAS), ("cross-o", 5120, 5120, K.VS_EPI_RES),
                              ("ffn-up", 13824, 5120, K.VS_EPI_GELU), ("ffn-down", 5120, 13824, K.VS_EPI_GATE_RES)):

@@ -9,7 +9,13 @@ from vstyler.usp import UlyssesGroup, _Done
 def permute_ref(src, dst, batch, s_local, world, cpr, ld_local, jstride, mode):
     """Pure-torch statement of vs_ulysses_permute (include/vstyler.h)."""
     B, Sl, P = batch, s_local, world
-    src1, dst1 = src.reshape(-1), dst.reshape(-1)
+
+    def flat(t):      # element view of t's storage from its first element (row-strided views too)
+        if t.is_contiguous():
+            return t.reshape(-1)
+        span = (t.shape[0] - 1) * t.stride(0) + t.shape[1] if t.dim() == 2 else t.numel()
+        return t.as_strided((span,), (1,))
+    src1, dst1 = flat(src), flat(dst)
     j = torch.arange(P).view(P, 1, 1, 1)
     b = torch.arange(B).view(1, B, 1, 1)
     t = torch.arange(Sl).view(1, 1, Sl, 1)

@@ -960,15 +960,16 @@ KSplit plan_ksplit(int ntiles, int nh, int cus) {
 // when the grid holds >= 1024 tiles (4 full rounds on 256 CUs), at any K (the 1.3B model's K = 1536
 // GEMMs: 1217-1300 TF/s against 707-797 on the 128^2 kernel, profiles/r1/gemm_bench_r1f.log).
 // hipBLASLt (autotuned per shape, blaslt.hip) vs the 256^2 MFMA kernel with its split tail, measured
-// per 14B block GEMM (profiles/r1/gemm_lt_tune_r1i.log): hipBLASLt wins on every grid of >= 1024
-// 256^2 tiles, and on 512-1023-tile grids (the SP=8 row count) while K <= 8192; the K = 13824
-// FFN-down GEMM at that size stays on the MFMA kernel (0.926 vs 0.971 ms).
+// per 14B block GEMM (profiles/r1/gemm_lt_tune_r1i.log, gemm_backend_ab_r1j.log): hipBLASLt wins on
+// every grid of >= 1024 256^2 tiles, and on 256-1023-tile grids (the SP=8 row counts 7410 and, per
+// CFG micro-batch, 3705) while K <= 8192 (1.01-1.32x); the K = 13824 FFN-down GEMM at those sizes
+// stays on the MFMA kernel (0.88-0.96x on hipBLASLt).
 static bool lt_route(int m, int n, int k) {
     const char* e = getenv("VS_GEMM_BACKEND");
     const int mode = !e ? 2 : (e[0] == 'v' ? 0 : (e[0] == 'l' ? 1 : 2));   // 0 never, 1 always, 2 auto
     if (mode != 2) return mode == 1;
     const long long tiles = (long long)((m + 255) / 256) * ((n + 255) / 256);
-    return tiles >= 1024 || (tiles >= 512 && k <= 8192);
+    return tiles >= 1024 || (tiles >= 256 && k <= 8192);
 }
 
 // hipBLASLt for bf16(A W^T [* scale] + bias) (gemm(y, ldy)), then the rest of the epilogue with

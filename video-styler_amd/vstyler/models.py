@@ -61,10 +61,19 @@ def quantize_fp8_(module):
     linear(); embeddings, VACE before/after projections and the head stay bf16."""
     n = 0
     for blk in [m for m in module.modules() if isinstance(m, DiTBlock)]:
+        for att in (blk.self_attn, blk.cross_attn):
+            att._fw8 = None
+            if _fused_views(att) is not None:       # fused q|k|v / k|v: one e4m3 buffer, per-Linear views
+                att._fw8 = att._fw.to(torch.float8_e4m3fn).view(torch.uint8).contiguous()
         for lin in (blk.self_attn.q, blk.self_attn.k, blk.self_attn.v, blk.self_attn.o, blk.cross_attn.q,
                     blk.cross_attn.k, blk.cross_attn.v, blk.cross_attn.o, blk.ffn[0], blk.ffn[2]):
             lin.weight_fp8 = lin.weight.detach().to(torch.float8_e4m3fn).view(torch.uint8).contiguous()
             n += 1
+        for att in (blk.self_attn, blk.cross_attn):
+            if att._fw8 is not None:
+                d = att.dim
+                for i, name in enumerate(att.fused):
+                    getattr(att, name).weight_fp8 = att._fw8[i * d:(i + 1) * d]
     return n
 
 
@@ -101,7 +110,12 @@ class LayerNormAffine(nn.Module):
 
 
 class AttentionParams(nn.Module):
-    def __init__(self, dim, num_heads, device=None):
+    """q/k/v/o Linears + QK norms under the reference's key names.  The Linears listed in `fused`
+    (same input: q|k|v of self-attention, k|v of cross-attention) keep their weights and biases as
+    row slices of one [n*dim, dim] / [n*dim] buffer, so their projections run as ONE GEMM
+    (fused_linear); state-dict loading, LoRA merging and init all write through the slices."""
+
+    def __init__(self, dim, num_heads, device=None, fused=()):
         super().__init__()
         self.dim, self.num_heads = dim, num_heads
         self.q = Linear(dim, dim, device=device)
@@ -110,6 +124,54 @@ class AttentionParams(nn.Module):
         self.o = Linear(dim, dim, device=device)
         self.norm_q = RMSNormW(dim, device=device)
         self.norm_k = RMSNormW(dim, device=device)
+        self.fused = tuple(fused)
+        self._fw = self._fb = self._fw8 = None
+        if self.fused:
+            n = len(self.fused)
+            self._fw = torch.empty(n * dim, dim, device=device, dtype=BF16)
+            self._fb = torch.empty(n * dim, device=device, dtype=BF16)
+            for i, name in enumerate(self.fused):
+                lin = getattr(self, name)
+                lin.weight = nn.Parameter(self._fw[i * dim:(i + 1) * dim], requires_grad=False)
+                lin.bias = nn.Parameter(self._fb[i * dim:(i + 1) * dim], requires_grad=False)
+
+
+def _fused_views(mod):
+    """(W, b, W8 or None) when the fused Linears still alias the fused buffers (nothing rebound
+    their parameters, no hot-loaded LoRA, fp8 copies all present or all absent), else None."""
+    if not getattr(mod, "fused", ()) or mod._fw is None:
+        return None
+    d = mod.dim
+    fp8 = [getattr(getattr(mod, n), "weight_fp8", None) is not None for n in mod.fused]
+    if any(fp8) and (not all(fp8) or mod._fw8 is None):
+        return None
+    for i, name in enumerate(mod.fused):
+        lin = getattr(mod, name)
+        if getattr(lin, "lora_A", None) is not None:
+            return None
+        if lin.weight.data_ptr() != mod._fw[i * d].data_ptr() or lin.bias is None or \
+                lin.bias.data_ptr() != mod._fb[i * d:].data_ptr():
+            return None
+        if fp8[i] and lin.weight_fp8.data_ptr() != mod._fw8[i * d].data_ptr():
+            return None
+    return mod._fw, mod._fb, (mod._fw8 if all(fp8) else None)
+
+
+def fused_linear(mod, x, ws, tag):
+    """All of mod.fused's projections of x as one GEMM into a [M, n*dim] buffer (column block i =
+    Linear i), or None when the fusion does not apply (the caller runs them one by one)."""
+    f = _fused_views(mod)
+    if f is None:
+        return None
+    W, b, W8 = f
+    out = ws.get("fused" + tag, (x.shape[0], W.shape[0]))
+    if W8 is not None:
+        M, Kd = x.shape
+        x8 = ws.get("fp8_x", (M, Kd), torch.uint8)
+        sc = ws.get("fp8_scale", (M,), torch.float32)
+        K.quant_fp8_rows(x, x8, sc)
+        return K.gemm_fp8(x8, sc, W8, out, bias=b)
+    return K.gemm(x, W, out, bias=b)
 
 
 class Sequential3(nn.Module):
@@ -191,8 +253,8 @@ class DiTBlock(nn.Module):
     def __init__(self, dim, num_heads, ffn_dim, eps=1e-6, device=None):
         super().__init__()
         self.dim, self.num_heads, self.ffn_dim, self.eps = dim, num_heads, ffn_dim, eps
-        self.self_attn = AttentionParams(dim, num_heads, device)
-        self.cross_attn = AttentionParams(dim, num_heads, device)
+        self.self_attn = AttentionParams(dim, num_heads, device, fused=("q", "k", "v"))
+        self.cross_attn = AttentionParams(dim, num_heads, device, fused=("k", "v"))
         self.norm3 = LayerNormAffine(dim, device)
         self.ffn = Sequential3(Linear(dim, ffn_dim, device=device), Linear(ffn_dim, dim, device=device))
         self.modulation = _param(1, 6, dim, device=device)
@@ -241,9 +303,13 @@ class DiTBlock(nn.Module):
         mod, h, q, k, v = p["mod"], p["h"], p["q"], p["k"], p["v"]
         K.layernorm_modulate(p["x"], h, eps, shift=mod[:, 0], scale=mod[:, 1], mod_bstride=6 * D, rows_per_batch=S)
         sa = self.self_attn
-        linear(sa.q, h, q, ws)
-        linear(sa.k, h, k, ws)
-        linear(sa.v, h, v, ws)
+        qkv = fused_linear(sa, h, ws, "qkv" + p["tag"])
+        if qkv is not None:            # one GEMM; q/k/v are column slices of [M, 3D]
+            q, k, v = p["q"], p["k"], p["v"] = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+        else:
+            linear(sa.q, h, q, ws)
+            linear(sa.k, h, k, ws)
+            linear(sa.v, h, v, ws)
         K.rmsnorm_rope(q, sa.norm_q.weight, eps, rope=rc.rope, grid=rc.grid, rows_per_batch=S,
                        token_offset=rc.token_offset)
         K.rmsnorm_rope(k, sa.norm_k.weight, eps, rope=rc.rope, grid=rc.grid, rows_per_batch=S,
@@ -271,12 +337,16 @@ class DiTBlock(nn.Module):
         K.layernorm_modulate(x, h, eps, weight=self.norm3.weight, bias=self.norm3.bias)
         ca = self.cross_attn
         L = rc.ctx_len
-        kc, vc = ws.get("kc" + p["tag"], (nb * L, D)), ws.get("vc" + p["tag"], (nb * L, D))
         linear(ca.q, h, q, ws)
         K.rmsnorm_rope(q, ca.norm_q.weight, eps)
-        linear(ca.k, p["ctx"], kc, ws)
+        kv = fused_linear(ca, p["ctx"], ws, "kvc" + p["tag"])
+        if kv is not None:
+            kc, vc = kv[:, :D], kv[:, D:]
+        else:
+            kc, vc = ws.get("kc" + p["tag"], (nb * L, D)), ws.get("vc" + p["tag"], (nb * L, D))
+            linear(ca.k, p["ctx"], kc, ws)
+            linear(ca.v, p["ctx"], vc, ws)
         K.rmsnorm_rope(kc, ca.norm_k.weight, eps)
-        linear(ca.v, p["ctx"], vc, ws)
         K.attention(q, kc, vc, o, self.num_heads, nb)
         linear(ca.o, o, x, ws, epilogue=K.VS_EPI_RES, residual=x)
         # --- FFN (wan_video_dit.py:228-229) + VACE hint (wan_video_new.py:1450)

@@ -126,8 +126,8 @@ class UlyssesGroup:
         e.chunk = batch * e.Sl * e.cpr                # elements of one tensor per rank chunk
         send = e.ws.get("sp_send" + tag, (P * 3 * e.chunk,))
         recv = e.ws.get("sp_recv" + tag, (P * 3 * e.chunk,))
-        for i, t in enumerate((q, k, v)):
-            self._permute(t, send[i * e.chunk:], batch, e.Sl, e.cpr, D, 3 * e.chunk, 0)
+        for i, t in enumerate((q, k, v)):     # row stride: q/k/v may be column slices of a fused q|k|v
+            self._permute(t, send[i * e.chunk:], batch, e.Sl, e.cpr, t.stride(0), 3 * e.chunk, 0)
         e.work = self._all_to_all(recv, send)
         return e
 
