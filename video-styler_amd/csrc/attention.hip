@@ -41,14 +41,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
 
 // ---------------------------------------------------------------------------------------------
 // Two phases per 64-key tile, the two wave halves one barrier apart, one S tile live:
-//   B_{i-1}: [load V(i)]   S = K(i) Q^T (16 MFMA)                     ; store K(i+1) -> slot (i+1)&1
-//   A_i:     [load K(i+2)] O^T += V(i-1)^T P(i-1) (16 MFMA) || softmax(S) -> P(i) ; store V(i) -> slot i&1
-// and the softmax is a max-free fast path: p = exp2(c*s - m) against the current reference max m,
-// packed to bf16 at once, and a lane's tile partial sum rs checked once per tile.  Every p <= rs,
+//   B_{i-1}: [load V(i)]   S = K(i) Q^T (16 MFMA) || exps of S's keys 0-31    ; store K(i+1) -> slot (i+1)&1
+//   A_i:     [load K(i+2)] O^T += V(i-1)^T P(i-1) (16 MFMA) || pack keys 0-31, softmax of keys 32-63
+//            -> P(i) ; store V(i) -> slot i&1
+// (the split puts half of the exps and row sums into the QK phase's empty VALU slots: +2.3 % on
+// the 14B shape, profiles/r1/attention_ab_r1l.log), and the softmax is a max-free fast path:
+// p = exp2(c*s - m) against the current reference max m, packed to bf16, and a lane's tile
+// partial sum rs (both halves) checked once per tile.  Every p <= rs,
 // so rs <= SUM_THR (= 2^8) guarantees P <= 2^8 -- the bound of v1's lazy rescale (CDNA guide T13).
 // When any lane of the wave exceeds it (always on the first tile; later only when a row's max has
 // grown), the exact path runs after the tile's PV(i-1) MFMAs: row max, m' = max(m, max), O (which
-// already holds P(i-1)V(i-1) at the old scale) and l scaled by exp2(m - m'), P(i) recomputed.
+// already holds P(i-1)V(i-1) at the old scale) and l scaled by exp2(m - m'), P(i) recomputed (the
+// keys 0-31 half from log2 of its in-place exps, or from K in global memory if one overflowed).
 // Ring hazards (group 0 runs B_{i-1} at phase 2i and A_i at 2i+1, group 1 one phase later):
 // K(i+1) is written at 2i / 2i+1 into the slot K(i-1) was read from at 2i-2 / 2i-1 and first read
 // at 2i+2; V(i) is written at 2i+1 / 2i+2 into the slot V(i-2) was read from at 2i-1 / 2i and first
@@ -194,72 +198,72 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
 
     f32x16_t s[2];        // S^T of the current tile: keys 32t + (i&3) + 8(i>>2) + 4hh, row q0 + r
     u32x4_t pk[4];        // P as the PV B operands (bf16 pairs): keys 16ks .. 16ks+15 of this lane's row
-    // row-sum partials.  VS_ATTN_RSINIT: the tile's first chunk initialises them (no 0 + p adds);
-    // VS_ATTN_PKSUM: one packed pair summed with v_pk_add_f32 (implies RSINIT)
-#ifdef VS_ATTN_PKSUM
-#define VS_ATTN_RSINIT 1
-    f32x2_t rsv;
-#define RS_TOTAL (rsv.x + rsv.y)
-#define RS_RESET()
-#define RS_PIN() asm volatile("" : "+v"(rsv))
-#else
-    float rs0, rs1;
+    float rs0, rs1;       // row-sum partials of the s[1] half (PV phase); rsA: the s[0] half (QK phase)
+    float rsA = 0.f;
 #define RS_TOTAL (rs0 + rs1)
-#ifdef VS_ATTN_RSINIT
-#define RS_RESET()
-#else
-#define RS_RESET() (rs0 = 0.f, rs1 = 0.f)
-#endif
-#define RS_PIN() asm volatile("" : "+v"(rs0), "+v"(rs1))
-#endif
-    auto p_chunk = [&](int ss) {   // elements 4ss..4ss+3 (flat 16t + i) of the tile's 32 scores
+    auto p_chunk = [&](int ss) __attribute__((always_inline)) {   // elements 4ss..4ss+3 (flat 16t + i)
         const int t = ss >> 2, i0 = 4 * (ss & 3);
         const float p0 = __builtin_amdgcn_exp2f(s[t][i0]);
         const float p1 = __builtin_amdgcn_exp2f(s[t][i0 + 1]);
         const float p2 = __builtin_amdgcn_exp2f(s[t][i0 + 2]);
         const float p3 = __builtin_amdgcn_exp2f(s[t][i0 + 3]);
-#if defined(VS_ATTN_PKSUM)
-        const f32x2_t pa = {p0, p2}, pb = {p1, p3};
-        if (ss == 0) rsv = pa + pb;
-        else rsv += pa + pb;
-#elif defined(VS_ATTN_RSINIT)
-        if (ss == 0) { rs0 = p0 + p1; rs1 = p2 + p3; }
-        else { rs0 += p0 + p1; rs1 += p2 + p3; }
-#else
         rs0 += p0 + p1;
         rs1 += p2 + p3;
-#endif
         const int ks = 2 * t + (i0 >> 3), j = (i0 & 7) >> 1;
         const bf16x2_t w0 = {(__bf16)p0, (__bf16)p1}, w1 = {(__bf16)p2, (__bf16)p3};
         pk[ks][j] = __builtin_bit_cast(unsigned, w0);
         pk[ks][j + 1] = __builtin_bit_cast(unsigned, w1);
-        // pin the chunk here: without it LLVM sinks the whole softmax below the PV MFMAs
     };
-    // S^T = K Q^T over 8 d-steps, two chains (keys 0-31 / 32-63).  K fragments are read
-    // VS_ATTN_KDEPTH d-steps ahead (default 3): with one step of look-ahead the QK burst stalls on
+    // the s[0] half's exponentials (computed in place in the QK phase) packed into pk
+    auto p_pack = [&](int ss) __attribute__((always_inline)) {
+        const int i0 = 4 * ss, ks = i0 >> 3, j = (i0 & 7) >> 1;
+        const bf16x2_t w0 = {(__bf16)s[0][i0], (__bf16)s[0][i0 + 1]};
+        const bf16x2_t w1 = {(__bf16)s[0][i0 + 2], (__bf16)s[0][i0 + 3]};
+        pk[ks][j] = __builtin_bit_cast(unsigned, w0);
+        pk[ks][j + 1] = __builtin_bit_cast(unsigned, w1);
+    };
+    auto mask_half = [&](int t, int kv0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int key = kv0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            if (key >= Skv) s[t][i] = -INFINITY;
+        }
+    };
+    // S^T = K Q^T: the s[0] chain (keys 0-31, 8 d-steps) first, then the s[1] chain with the s[0]
+    // half's softmax exps in place, two per MFMA gap, and their sum rsA (the QK phase's VALU slots
+    // are otherwise empty; the PV phase keeps only the s[1] half).  K fragments are read
+    // VS_ATTN_KDEPTH MFMAs ahead (default 4): with one step of look-ahead the QK burst stalls on
     // LDS latency and holds the SIMD's matrix pipe for ~2x its 16 MFMAs while the partner wave's
     // PV+softmax phase starves (measured with -DVS_ATTN_STAMPS).
 #ifndef VS_ATTN_KDEPTH
-#define VS_ATTN_KDEPTH 3
+#define VS_ATTN_KDEPTH 4
 #endif
-    auto qk = [&](int slot) {
+    auto qk = [&](int slot, int kv0) __attribute__((always_inline)) {
         const char* base = smem + slot * KT + krd;
         constexpr int DEP = VS_ATTN_KDEPTH;
-        bf16x8_t ka[8], kb[8];
+        const bool last = kv0 + BKV > Skv;
+        bf16x8_t kf[16];
+        auto kaddr = [&](int j) { return base + (j >= 8 ? 32 * KROW : 0) + 32 * (j & 7); };
 #pragma unroll
-        for (int ss = 0; ss < DEP; ++ss) {
-            ka[ss] = *reinterpret_cast<const bf16x8_t*>(base + 32 * ss);
-            kb[ss] = *reinterpret_cast<const bf16x8_t*>(base + 32 * KROW + 32 * ss);
-        }
+        for (int j = 0; j < DEP; ++j) kf[j] = *reinterpret_cast<const bf16x8_t*>(kaddr(j));
 #pragma unroll
-        for (int ss = 0; ss < 8; ++ss) {
-            if (ss + DEP < 8) {
-                ka[ss + DEP] = *reinterpret_cast<const bf16x8_t*>(base + 32 * (ss + DEP));
-                kb[ss + DEP] = *reinterpret_cast<const bf16x8_t*>(base + 32 * KROW + 32 * (ss + DEP));
-            }
+        for (int j = 0; j < 16; ++j) {
+            if (j + DEP < 16) kf[j + DEP] = *reinterpret_cast<const bf16x8_t*>(kaddr(j + DEP));
+            if (j == 8 && last) mask_half(0, kv0);
             __builtin_amdgcn_sched_barrier(0);
-            s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[ss], qf[ss], ss == 0 ? negm : s[0], 0, 0, 0);
-            s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb[ss], qf[ss], ss == 0 ? negm : s[1], 0, 0, 0);
+            if (j < 8) {
+                s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[j], qf[j], j == 0 ? negm : s[0], 0, 0, 0);
+            } else {
+                s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[j], qf[j - 8], j == 8 ? negm : s[1], 0, 0, 0);
+                const int e = 2 * (j - 8);
+                s[0][e] = __builtin_amdgcn_exp2f(s[0][e]);
+                s[0][e + 1] = __builtin_amdgcn_exp2f(s[0][e + 1]);
+                const float pp = s[0][e] + s[0][e + 1];
+                rsA = j == 8 ? pp : rsA + pp;
+                // pure VALU floats freely in the IR (past the phase barrier into its uses): tie
+                // each pair to its MFMA gap
+                asm volatile("" : "+v"(rsA));
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -281,9 +285,10 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
 #ifdef VS_ATTN_STAMPS
     int stamp_it = 0;
 #endif
-    auto pv_softmax = [&](int slot, bool with_pv) {
+    auto pv_softmax = [&](int slot, bool with_pv) __attribute__((always_inline)) {
         const char* base = smem + 2 * KT + slot * VT;
-        RS_RESET();
+        rs0 = 0.f;
+        rs1 = 0.f;
         bf16x8_t va[4], vb[4];
         if (with_pv) read_vt(base, 0, va);
 #pragma unroll
@@ -298,11 +303,18 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
                     o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[dt], __builtin_bit_cast(bf16x8_t, pk[ks]),
                                                                     o[dt], 0, 0, 0);
             }
-            p_chunk(2 * ks);
-            p_chunk(2 * ks + 1);
-            // pure VALU floats freely in the DAG (a sched_barrier alone does not hold it): tie the
-            // chunk's sums to this point so its exps land in this k-step's MFMA region
-            RS_PIN();
+            if (ks < 2) {               // keys 0-31: exponentiated in the QK phase, pack only
+                p_pack(2 * ks);
+                p_pack(2 * ks + 1);
+            } else {                    // keys 32-63
+                p_chunk(2 * ks);
+                p_chunk(2 * ks + 1);
+                // tie the chunk's sums here so its exps land in this k-step's MFMA region
+                asm volatile("" : "+v"(rs0), "+v"(rs1));
+            }
+            // use P(i)'s packed k-step here: otherwise LLVM sinks every pack below the exact-path
+            // branch and keeps the fp32 p values live through the PV phase
+            asm volatile("" :: "v"(pk[ks]));
             __builtin_amdgcn_sched_barrier(0);
             if (with_pv) ATTN_STAMP(3 + ks);
         }
@@ -346,9 +358,30 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
             for (int i = 0; i < 16; ++i) s[t][i] += delta;
 #pragma unroll
         for (int i = 0; i < 16; ++i) negm[i] = -mnew;
-        RS_RESET();
+        rs0 = 0.f;
+        rs1 = 0.f;
 #pragma unroll
         for (int ss = 0; ss < 8; ++ss) p_chunk(ss);
+    };
+    // exact path of the split softmax: s[0] holds p0 = exp2(S0); restore S0 = log2(p0), or, when a
+    // p0 overflowed (a row max grown by >= 128 in the exp2 domain), recompute S0 from K in global
+    // memory (the K(i) LDS slot may already hold K(i+2) for the other wave half)
+    auto exact_split = [&](bool first, int kv0) __attribute__((always_inline)) {
+        if (__any(!(rsA < INFINITY))) {
+            const int krow = min(kv0 + r, Skv - 1);
+            const bf16_t* kp = Kb + (long long)krow * ldk + 8 * hh;
+#pragma unroll
+            for (int ss = 0; ss < 8; ++ss) {
+                const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kp + 16 * ss);
+                s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ss], ss == 0 ? negm : s[0], 0, 0, 0);
+            }
+            if (kv0 + BKV > Skv) mask_half(0, kv0);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[0][i] = __builtin_amdgcn_logf(s[0][i]);
+        }
+        exact(first);
+        rsA = 0.f;
     };
 
     auto phase_bar = [&]() {
@@ -359,40 +392,35 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     __syncthreads();
     const int grp = wave >> 2;
     if (grp == 1) phase_bar();
-    for (int it = 0; it < nkv; ++it) {
+    // one tile: B_{it-1} (QK(it) + the s[0] half's exps), A_it (PV(it-1) + the s[1] half).  Tile 0
+    // (no PV, always the exact path) is peeled out of the loop: with one loop body shape the
+    // kernel stays spill-free (a loop with the it == 0 cases inside spilled at 256 VGPRs)
+    auto tile = [&](int it, auto first_c) __attribute__((always_inline)) {
+        constexpr bool first = decltype(first_c)::value;
 #ifdef VS_ATTN_STAMPS
         stamp_it = it;
 #endif
         ATTN_STAMP(0);
-        // ---- B_{it-1}
         load_v(it * BKV);
-        qk(it & 1);
+        qk(it & 1, it * BKV);
         if (it + 1 < nkv) store_k((it + 1) & 1);
         ATTN_STAMP(1);
         phase_bar();
         ATTN_STAMP(2);
-        // ---- A_it
         if (it + 2 < nkv) load_k((it + 2) * BKV);
         if ((it + 1) * BKV > Skv) {
             asm volatile("");
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int key = it * BKV + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
-                    if (key >= Skv) s[t][i] = -INFINITY;
-                }
+            mask_half(1, it * BKV);
         }
-        if (it > 0)
-            pv_softmax((it - 1) & 1, true);
-        else
-            pv_softmax(0, false);
-        if (__any(RS_TOTAL > SUM_THR) || it == 0) exact(it == 0);
-        l += RS_TOTAL;
+        pv_softmax((it - 1) & 1, !first);
+        if (first || __any(rsA + RS_TOTAL > SUM_THR)) exact_split(first, it * BKV);
+        l += rsA + RS_TOTAL;
         store_v(it & 1);
         ATTN_STAMP(7);
         phase_bar();
-    }
+    };
+    tile(0, std::true_type{});
+    for (int it = 1; it < nkv; ++it) tile(it, std::false_type{});
 #ifdef VS_ATTN_STAMPS
     // stamps of tiles (nkv-32) .. nkv-1 (ring of 32), copied out by workgroup 0's waves 0 and 4
     if (blockIdx.x == 0 && (wave & 3) == 0) {
