@@ -1,0 +1,65 @@
+"""Fused q|k|v (self-attention) and k|v (cross-attention) projections: the Linears' parameters are
+row-slice views of one buffer, so loading / merging / init write through and the block runs one
+GEMM; anything that breaks the aliasing (rebinding a parameter, a hot-loaded LoRA, mixed fp8)
+makes fused_linear fall back to the per-Linear GEMMs.  CPU-only (no kernels run)."""
+import torch
+import torch.nn as nn
+
+from vstyler.models import DiTBlock, _fused_views
+
+BF16 = torch.bfloat16
+
+
+def _block():
+    blk = DiTBlock(256, 2, 512, device="cpu")
+    g = torch.Generator().manual_seed(3)
+    sd = {k: torch.randn(v.shape, generator=g).to(BF16) for k, v in blk.state_dict().items()}
+    blk.load_state_dict(sd)
+    return blk, sd
+
+
+def test_fused_views_alias_loaded_weights():
+    blk, sd = _block()
+    for att, names in ((blk.self_attn, ("q", "k", "v")), (blk.cross_attn, ("k", "v"))):
+        f = _fused_views(att)
+        assert f is not None
+        W, b, W8 = f
+        assert W8 is None
+        for i, n in enumerate(names):
+            pre = "self_attn." if att is blk.self_attn else "cross_attn."
+            assert torch.equal(W[i * 256:(i + 1) * 256], sd[pre + n + ".weight"])
+            assert torch.equal(b[i * 256:(i + 1) * 256], sd[pre + n + ".bias"])
+    # the reference key layout is unchanged (no extra parameters or buffers)
+    assert set(blk.state_dict()) == set(sd)
+
+
+def test_in_place_updates_write_through():
+    blk, _ = _block()
+    with torch.no_grad():
+        blk.self_attn.k.weight.add_(1.0)            # e.g. a LoRA merge writes in place
+    W = _fused_views(blk.self_attn)[0]
+    assert torch.equal(W[256:512], blk.self_attn.k.weight)
+
+
+def test_fallback_when_aliasing_breaks():
+    blk, _ = _block()
+    blk.self_attn.v.weight = nn.Parameter(blk.self_attn.v.weight.detach().clone(), requires_grad=False)
+    assert _fused_views(blk.self_attn) is None
+    assert _fused_views(blk.cross_attn) is not None
+    blk2, _ = _block()
+    blk2.cross_attn.k.lora_A = torch.zeros(32, 256, dtype=BF16)     # hot-loaded LoRA
+    assert _fused_views(blk2.cross_attn) is None
+    blk3, _ = _block()
+    blk3.self_attn.q.weight_fp8 = torch.zeros(256, 256, dtype=torch.uint8)   # fp8 on one Linear only
+    assert _fused_views(blk3.self_attn) is None
+
+
+def test_quantize_fp8_keeps_fusion():
+    from vstyler.models import quantize_fp8_
+    blk, _ = _block()
+    assert quantize_fp8_(blk) == 10
+    W, b, W8 = _fused_views(blk.self_attn)
+    assert W8 is not None and W8.dtype == torch.uint8 and W8.shape == (768, 256)
+    assert torch.equal(W8[256:512], blk.self_attn.k.weight_fp8)
+    ref = blk.self_attn.k.weight.detach().to(torch.float8_e4m3fn).view(torch.uint8)
+    assert torch.equal(blk.self_attn.k.weight_fp8, ref)

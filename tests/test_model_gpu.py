@@ -159,3 +159,32 @@ def test_denoise_graph_replay_bit_identical_to_eager(tiny):
     graph = pipe.denoise(lat, cp.cuda(), cn.cuda(), vc.cuda(), num_inference_steps=4, use_graph=True)
     assert pipe.last_graph is not None
     assert torch.equal(eager, graph)
+
+
+def test_hotloaded_lora_on_fused_projections_matches_merged():
+    """A LoRA hot-loaded on Linears that normally run fused (self-attention q|k|v, cross-attention
+    k|v of the VACE blocks) makes those blocks fall back to per-Linear GEMMs with the fused second K
+    phase; the forward must match the same LoRA merged into the weights (which keeps the fusion)."""
+    from vstyler import model_fn_wan_video
+    from vstyler.lora import hotload_lora, merge_lora
+    from vstyler.models import _fused_views
+    cfg = O.WAN_CONFIGS["tiny"]
+    W = O.random_weights(cfg, seed=5)
+    g = torch.Generator().manual_seed(91)
+    D, r = cfg["dim"], 32
+    lora = {}
+    for n in ("vace_blocks.0.self_attn.q", "vace_blocks.0.self_attn.v", "vace_blocks.1.cross_attn.k"):
+        lora[n + ".lora_A.default.weight"] = (0.05 * torch.randn(r, D, generator=g)).to(BF16)
+        lora[n + ".lora_B.default.weight"] = (0.05 * torch.randn(D, r, generator=g)).to(BF16)
+    lat, cp, cn, vc = O.synthetic_inputs(cfg, 5, 128, 128)
+    t = torch.tensor([700.0]).to(BF16).cuda()
+    outs = []
+    for mode in ("merge", "hotload"):
+        dit, vace = build(cfg, W)
+        (merge_lora if mode == "merge" else hotload_lora)(vace, lora, alpha=0.8)
+        fused = _fused_views(vace.vace_blocks[0].self_attn) is not None
+        assert fused == (mode == "merge")
+        outs.append(model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=cp.cuda(),
+                                       vace_context=vc.cuda()))
+    mx, rl = err(outs[1], outs[0].cpu())
+    assert rl < 1e-2, (mx, rl)
