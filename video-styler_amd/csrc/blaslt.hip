@@ -108,12 +108,13 @@ LtPlan* plan_for(const LtKey& key, size_t ws_bytes) {
 // being captured into a graph (no host sync possible) and with VS_LT_TUNE=0.
 void autotune(LtPlan& p, hipblasLtHandle_t h, const void* a, const void* w, void* c, float* ws, size_t ws_bytes,
               hipStream_t stream) {
-    p.tuned = true;
-    if (p.cand.size() < 2) return;
+    if (p.cand.size() < 2) { p.tuned = true; return; }
     const char* env = std::getenv("VS_LT_TUNE");
-    if (env && env[0] == '0') return;
+    if (env && env[0] == '0') { p.tuned = true; return; }
+    // inside a graph capture: keep the heuristic pick for now and tune on a later eager call
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+    p.tuned = true;
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess) return;
     if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return; }
