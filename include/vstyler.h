@@ -75,6 +75,13 @@ int vs_gemm(const void* a, long long lda, const void* w, long long ldw, void* c,
 int vs_gemm_split_plan(int m, int n, int k, int cus, int* out);
 
 /*
+ * 1 when vs_gemm would send an (m, n, k) GEMM without a LoRA phase to hipBLASLt (so a binding knows
+ * to bind the kind-3 staging buffer for its gate-residual / residual epilogues), 0 for the MFMA
+ * kernels, VS_E_INVALID for non-positive sizes.  Honours VS_GEMM_BACKEND.  Host-only.
+ */
+int vs_gemm_route(int m, int n, int k);
+
+/*
  * fp8 path (config 5; AutoWrappedLinear.fp8_linear, diffsynth/vram_management/layers.py:115-151):
  * vs_quant_fp8_rows quantises activations per row, s[m] = max(max_k |x[m][k]| / 448, 1),
  * x8 = e4m3fn(x / (s + 1e-8)) (OCP e4m3, round-to-nearest-even); vs_gemm_fp8 computes

@@ -133,3 +133,21 @@ def test_gemm_split_plan_host_only():
         if ntail:
             assert pk % 32 == 0 and (ks - 1) * pk < args[2] <= ks * pk
     assert lib.vs_gemm_split_plan(64, 64, 100, 256, out) == 1
+
+
+def test_gemm_route_rule(monkeypatch):
+    """vs_gemm_route: hipBLASLt for grids of >= 1024 256x256 tiles, or >= 256 tiles with K <= 8192
+    (gemm.hip lt_route, measured in profiles/r1/gemm_backend_ab_r1j.log); VS_GEMM_BACKEND forces."""
+    from vstyler import _lib
+    lib = _lib.load()
+    monkeypatch.delenv("VS_GEMM_BACKEND", raising=False)
+    assert lib.vs_gemm_route(59280, 5120, 13824) == 1       # 4640 tiles
+    assert lib.vs_gemm_route(7410, 5120, 5120) == 1         # 580 tiles, K 5120
+    assert lib.vs_gemm_route(3705, 5120, 5120) == 1         # 300 tiles
+    assert lib.vs_gemm_route(7410, 5120, 13824) == 0        # 580 tiles, K 13824
+    assert lib.vs_gemm_route(1024, 10240, 5120) == 0        # 160 tiles
+    assert lib.vs_gemm_route(0, 1, 1) == _lib.VS_E_INVALID if hasattr(_lib, "VS_E_INVALID") else lib.vs_gemm_route(0, 1, 1) != 0
+    monkeypatch.setenv("VS_GEMM_BACKEND", "vstyler")
+    assert lib.vs_gemm_route(59280, 5120, 5120) == 0
+    monkeypatch.setenv("VS_GEMM_BACKEND", "lt")
+    assert lib.vs_gemm_route(64, 64, 64) == 1

@@ -1189,6 +1189,11 @@ extern "C" int vs_quant_fp8_rows(const void* x, long long ldx, void* x8, long lo
     return VS_OK;
 }
 
+extern "C" int vs_gemm_route(int m, int n, int k) {
+    if (m <= 0 || n <= 0 || k <= 0) return VS_E_INVALID;
+    return lt_route(m, n, k) ? 1 : 0;
+}
+
 extern "C" int vs_gemm_split_plan(int m, int n, int k, int cus, int* out) {
     if (!out || m <= 0 || n <= 0 || k <= 0 || k % BK || cus < 0) return VS_E_INVALID;
     const KSplit p = plan_ksplit(((m + BT - 1) / BT) * ((n + BT - 1) / BT), k / HK, cus);

@@ -60,6 +60,7 @@ SIGNATURES = {
                     _F, _P],
     "vs_attn_split_plan": [_I, _I, _I, _I, _I, _P],
     "vs_gemm_split_plan": [_I, _I, _I, _I, _P],
+    "vs_gemm_route": [_I, _I, _I],
     "vs_split_workspace_bytes": [_I],
     "vs_split_workspace_bind": [_I, _P, _LL, _P],
     "vs_layernorm_modulate": [_P, _LL, _P, _LL, _I, _I, _I, _P, _P, _LL, _P, _P, _F, _P],

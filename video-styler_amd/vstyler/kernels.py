@@ -131,15 +131,9 @@ def quant_fp8_rows(x, x8, scale):
 
 
 def _lt_route(M, N, K):
-    """Mirror of vs_gemm's routing rule (gemm.hip lt_route): grids of >= 1024 256x256 tiles, or
-    >= 256 with K <= 8192, go to hipBLASLt -- the shim binds the epilogue staging buffer for them."""
-    be = os.environ.get("VS_GEMM_BACKEND", "")
-    if be.startswith("v"):
-        return False
-    if be.startswith("l"):
-        return True
-    tiles = ((M + 255) // 256) * ((N + 255) // 256)
-    return tiles >= 1024 or (tiles >= 256 and K <= 8192)
+    """vs_gemm's routing decision (vs_gemm_route): the shim binds the epilogue staging buffer for
+    GEMMs that go to hipBLASLt."""
+    return _lib.load().vs_gemm_route(int(M), int(N), int(K)) == 1
 
 
 def gemm_fp8(a8, scale_a, w8, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, gate_bstride=0,
