@@ -188,6 +188,20 @@ def test_attention(K, B, Sq, Skv, H):
     assert mx < 3e-2 and rl < 1e-2, (mx, rl)
 
 
+@pytest.mark.parametrize("Skv", [1, 31, 32, 33, 63, 64, 65, 129])
+def test_attention_key_tile_edges(K, Skv):
+    """Key counts around the 64-key tile and its two 32-key halves: the keys 0-31 half is masked
+    and exponentiated inside the QK phase (split softmax), the keys 32-63 half in the PV phase."""
+    B, Sq, H = 1, 300, 2
+    D = H * 128
+    q, k, v = rnd(B, Sq, D, seed=40), rnd(B, Skv, D, seed=41), rnd(B, Skv, D, seed=42)
+    ref = O.attention(q, k, v, H)
+    out = torch.empty(B * Sq, D, dtype=BF16, device="cuda")
+    K.attention(q.cuda().view(B * Sq, D), k.cuda().view(B * Skv, D), v.cuda().view(B * Skv, D), out, H, B)
+    mx, rl = err(out.view(B, Sq, D), ref)
+    assert mx < 3e-2 and rl < 1e-2, (mx, rl)
+
+
 def test_attention_online_rescale_spike(K):
     """Rule 26 of the CDNA guide: force the running-max rescale by a late large score."""
     B, S, H = 1, 512, 1
