@@ -41,9 +41,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
 
 // ---------------------------------------------------------------------------------------------
 // Two phases per 64-key tile, the two wave halves one barrier apart, one S tile live:
-//   B_{i-1}: [load V(i)]   S = K(i) Q^T (16 MFMA) || exps of S's keys 0-31    ; store K(i+1) -> slot (i+1)&1
-//   A_i:     [load K(i+2)] O^T += V(i-1)^T P(i-1) (16 MFMA) || pack keys 0-31, softmax of keys 32-63
-//            -> P(i) ; store V(i) -> slot i&1
+//   B_{i-1}: [store K(i+1) -> slot (i+1)&1; load V(i)]   S = K(i) Q^T (16 MFMA) || exps of S's keys 0-31
+//   A_i:     [store V(i) -> slot i&1; load K(i+2)]   O^T += V(i-1)^T P(i-1) (16 MFMA)
+//            || pack keys 0-31, softmax of keys 32-63 -> P(i)
+// (the LDS stores open the phase: +1 % over storing at its end, profiles/r1/attention_ab_r1l.log)
 // (the split puts half of the exps and row sums into the QK phase's empty VALU slots: +2.3 % on
 // the 14B shape, profiles/r1/attention_ab_r1l.log), and the softmax is a max-free fast path:
 // p = exp2(c*s - m) against the current reference max m, packed to bf16, and a lane's tile
@@ -401,12 +402,15 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
         stamp_it = it;
 #endif
         ATTN_STAMP(0);
+        // each phase opens with the LDS store of the tile staged one phase earlier (its slot's last
+        // reader finished before the barrier that opened this phase), then the next global loads
+        if (it + 1 < nkv) store_k((it + 1) & 1);     // K(it+1), loaded at the start of A_{it-1}
         load_v(it * BKV);
         qk(it & 1, it * BKV);
-        if (it + 1 < nkv) store_k((it + 1) & 1);
         ATTN_STAMP(1);
         phase_bar();
         ATTN_STAMP(2);
+        store_v(it & 1);                             // V(it), loaded at the start of B_{it-1}
         if (it + 2 < nkv) load_k((it + 2) * BKV);
         if ((it + 1) * BKV > Skv) {
             asm volatile("");
@@ -415,7 +419,6 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
         pv_softmax((it - 1) & 1, !first);
         if (first || __any(rsA + RS_TOTAL > SUM_THR)) exact_split(first, it * BKV);
         l += rsA + RS_TOTAL;
-        store_v(it & 1);
         ATTN_STAMP(7);
         phase_bar();
     };
