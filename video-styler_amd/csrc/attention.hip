@@ -233,11 +233,11 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     // S^T = K Q^T: the s[0] chain (keys 0-31, 8 d-steps) first, then the s[1] chain with the s[0]
     // half's softmax exps in place, two per MFMA gap, and their sum rsA (the QK phase's VALU slots
     // are otherwise empty; the PV phase keeps only the s[1] half).  K fragments are read
-    // VS_ATTN_KDEPTH MFMAs ahead (default 5): with one step of look-ahead the QK burst stalls on
+    // VS_ATTN_KDEPTH MFMAs ahead (default 4): with one step of look-ahead the QK burst stalls on
     // LDS latency and holds the SIMD's matrix pipe for ~2x its 16 MFMAs while the partner wave's
     // PV+softmax phase starves (measured with -DVS_ATTN_STAMPS).
 #ifndef VS_ATTN_KDEPTH
-#define VS_ATTN_KDEPTH 5
+#define VS_ATTN_KDEPTH 4
 #endif
     auto qk = [&](int slot, int kv0) __attribute__((always_inline)) {
         const char* base = smem + slot * KT + krd;
