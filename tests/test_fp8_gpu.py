@@ -109,3 +109,37 @@ def test_model_fn_fp8_tiny_vs_oracle():
     mx, rl = err(out, ref)
     print(f"fp8 tiny forward: max-abs {mx:.4g} rel-L2 {rl:.4g} (floor {fmx:.4g} / {frl:.4g})")
     assert rl <= 1.5 * frl + 2e-3 and mx <= 1.5 * fmx + 2e-2
+
+
+@pytest.mark.parametrize("epi", ["bias", "gelu", "gate_res", "res"])
+def test_gemm_fp8_hipblaslt_route_matches_mfma_kernel(epi, monkeypatch):
+    """vs_gemm_fp8's default route (hipBLASLt fp8 with the per-token scale as its outer B-scale
+    vector, then the epilogue pass) against the fp8 MFMA kernel (VS_FP8_BACKEND=vstyler), on random
+    data: bit-identical for every epilogue (profiles/r1/gemm_fp8_lt_r1j.log measures the same at
+    the 14B shapes)."""
+    K = _k()
+    M, N, Kd = 1500, 2048, 2560
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(M, Kd, device="cuda", generator=g).to(BF16)
+    w8 = (0.05 * torch.randn(N, Kd, device="cuda", generator=g)).to(torch.float8_e4m3fn).view(torch.uint8)
+    b = (0.1 * torch.randn(N, device="cuda", generator=g)).to(BF16)
+    res0 = torch.randn(M, N, device="cuda", generator=g).to(BF16)
+    gate = (0.3 * torch.randn(2, N, device="cuda", generator=g)).to(BF16)
+    x8 = torch.empty(M, Kd, dtype=torch.uint8, device="cuda")
+    sc = torch.empty(M, dtype=torch.float32, device="cuda")
+    K.quant_fp8_rows(x, x8, sc)
+    outs = []
+    for be in ("lt", "vstyler"):
+        monkeypatch.setenv("VS_FP8_BACKEND", be)
+        out = res0.clone() if epi in ("gate_res", "res") else torch.empty(M, N, dtype=BF16, device="cuda")
+        kw = dict(bias=b)
+        if epi == "gelu":
+            kw["epilogue"] = K.VS_EPI_GELU
+        elif epi == "gate_res":
+            kw.update(epilogue=K.VS_EPI_GATE_RES, residual=out, gate=gate, gate_bstride=N, rows_per_batch=M // 2)
+        elif epi == "res":
+            kw.update(epilogue=K.VS_EPI_RES, residual=out, alpha=0.5)
+        K.gemm_fp8(x8, sc, w8, out, **kw)
+        torch.cuda.synchronize()
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
