@@ -135,6 +135,19 @@ int vs_layernorm_modulate(const void* x, long long ldx, void* out, long long ldo
                           void* stream);
 
 /*
+ * x = epilogue(y, x) then out = vs_layernorm_modulate(x): the gate-residual / residual epilogue of a
+ * projection whose bf16(A W^T + bias) was staged in y (vs_gemm's hipBLASLt route), fused with the
+ * LayerNorm [+ affine] [+ modulate] that reads the updated row next (wan_video_dit.py:225-228).
+ * epilogue: VS_EPI_GATE_RES (epi->gate, gate_bstride, rows_per_batch, optional hint) or VS_EPI_RES
+ * (epi->alpha); epi->residual is ignored (x is the residual).  Same rounding points as vs_gemm's
+ * epilogue followed by vs_layernorm_modulate: bit-identical to the two calls.
+ */
+int vs_residual_layernorm(const void* y, long long ldy, void* x, long long ldx, void* out, long long ldo, int rows,
+                          int dim, int epilogue, const vs_epilogue* epi, int rows_per_batch, const void* shift,
+                          const void* scale, long long mod_bstride, const void* weight, const void* bias,
+                          float eps, void* stream);
+
+/*
  * In place: x = bf16(bf16(x * rsqrt(mean(x^2)+eps)) * weight) over the full row (all heads), then
  * (if rope != NULL) the interleaved 3-D RoPE of each head_dim slice with table rope[pos][pair]
  * (float2 cos,sin; pair axes 22 t / 21 h / 21 w).  Token index = (row % rows_per_batch) +

@@ -329,6 +329,34 @@ def test_layernorm_modulate(K):
     assert err(out, ref)[0] <= 2 ** -5 * max(1.0, ref.float().abs().max().item())
 
 
+@pytest.mark.parametrize("mode", ["gate_res", "gate_res_hint", "res"])
+def test_residual_layernorm_matches_two_passes(K, mode):
+    """vs_residual_layernorm == vs_gemm's residual epilogue on a staged y, then vs_layernorm_modulate."""
+    B, S, D = 2, 37, 1536
+    M = B * S
+    y, x0 = rnd(M, D, scale=0.5, seed=60).cuda(), rnd(M, D, scale=2.0, seed=61).cuda()
+    mod = rnd(B, 6, D, scale=0.3, seed=62).cuda()
+    hint = rnd(M, D, seed=63).cuda()
+    w, b = (rnd(D, scale=0.1, seed=64) + 1).cuda(), rnd(D, scale=0.1, seed=65).cuda()
+    eye = torch.eye(D, dtype=BF16, device="cuda")       # y = y . I^T exactly: the epilogue runs on y
+    x1, h1 = x0.clone(), torch.empty(M, D, dtype=BF16, device="cuda")
+    x2, h2 = x0.clone(), torch.empty(M, D, dtype=BF16, device="cuda")
+    if mode == "res":
+        K.gemm(y, eye, x1, epilogue=K.VS_EPI_RES, residual=x1, alpha=0.75)
+        K.layernorm_modulate(x1, h1, 1e-6, shift=mod[:, 3], scale=mod[:, 4], mod_bstride=6 * D, rows_per_batch=S)
+        K.residual_layernorm(y, x2, h2, 1e-6, epilogue=K.VS_EPI_RES, alpha=0.75, shift=mod[:, 3], scale=mod[:, 4],
+                             mod_bstride=6 * D, rows_per_batch=S)
+    else:
+        hk = dict(hint=hint, hint_scale=0.5) if mode == "gate_res_hint" else {}
+        K.gemm(y, eye, x1, epilogue=K.VS_EPI_GATE_RES, residual=x1, gate=mod[:, 2], gate_bstride=6 * D,
+               rows_per_batch=S, **hk)
+        K.layernorm_modulate(x1, h1, 1e-6, weight=w, bias=b)
+        K.residual_layernorm(y, x2, h2, 1e-6, epilogue=K.VS_EPI_GATE_RES, gate=mod[:, 2], gate_bstride=6 * D,
+                             gate_rows=S, weight=w, bias=b, **hk)
+    assert torch.equal(x1, x2)
+    assert torch.equal(h1, h2)
+
+
 def test_rmsnorm_rope(K):
     B, grid, H = 2, (3, 4, 5), 2
     S, D = 60, 256

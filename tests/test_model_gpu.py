@@ -188,3 +188,21 @@ def test_hotloaded_lora_on_fused_projections_matches_merged():
                                        vace_context=vc.cuda()))
     mx, rl = err(outs[1], outs[0].cpu())
     assert rl < 1e-2, (mx, rl)
+
+
+def test_fused_residual_layernorm_bit_identical(monkeypatch):
+    """The hipBLASLt route's residual epilogue fused with the following LayerNorm
+    (vs_residual_layernorm) gives exactly the unfused forward (same rounding points)."""
+    from vstyler import model_fn_wan_video
+    cfg = O.WAN_CONFIGS["tiny"]
+    W = O.random_weights(cfg, seed=5)
+    dit, vace = build(cfg, W)
+    lat, cp, cn, vc = O.synthetic_inputs(cfg, 5, 128, 128)
+    t = torch.tensor([600.0]).to(BF16).cuda()
+    monkeypatch.setenv("VS_GEMM_BACKEND", "lt")          # tiny shapes: force the hipBLASLt route
+    outs = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("VSTYLER_FUSE_RES_LN", fuse)
+        outs.append(model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=cp.cuda(),
+                                       vace_context=vc.cuda()))
+    assert torch.equal(outs[0], outs[1])

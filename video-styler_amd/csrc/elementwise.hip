@@ -97,6 +97,95 @@ __global__ __launch_bounds__(RT) void ln_modulate_kernel(
     }
 }
 
+// Gated / plain residual add of a staged projection y (the hipBLASLt route's bf16(A W^T + bias))
+// into x, then LayerNorm [+ affine] [+ modulate] of the updated row into out: the vs_gemm epilogue
+// (VS_EPI_GATE_RES: x = bf16(x + bf16(gate*y)) [+ bf16(hint*s)]; VS_EPI_RES: x = bf16(x + bf16(alpha*y)))
+// followed by ln_modulate_kernel's arithmetic on the stored bf16 row -- the same rounding points as
+// the two separate passes, one read of x instead of two (wan_video_dit.py:225-228).
+__global__ __launch_bounds__(RT) void residual_ln_kernel(
+    const bf16_t* __restrict__ y, long long ldy, bf16_t* __restrict__ x, long long ldx, bf16_t* __restrict__ out,
+    long long ldo, int dim, int mode, const bf16_t* __restrict__ gate, long long gate_bstride, int rpb_gate,
+    float alpha, const bf16_t* __restrict__ hint, long long ld_hint, float hint_scale, int rpb,
+    const bf16_t* __restrict__ shift, const bf16_t* __restrict__ scale, long long mbs,
+    const bf16_t* __restrict__ w, const bf16_t* __restrict__ bb, float eps) {
+    __shared__ float red[RT / 64];
+    const long long row = blockIdx.x;
+    const int nch = dim >> 3;
+    const bf16_t* yr = y + row * ldy;
+    bf16_t* xr = x + row * ldx;
+    const bf16_t* gr = gate ? gate + (row / rpb_gate) * gate_bstride : nullptr;
+    float v[MAXCH][8];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXCH; ++c) {
+        const int ch = threadIdx.x + c * RT;
+        if (ch < nch) {
+            float yv[8], xv[8];
+            unpack8(*reinterpret_cast<const u32x4_t*>(yr + ch * 8), yv);
+            unpack8(*reinterpret_cast<const u32x4_t*>(xr + ch * 8), xv);
+            if (mode == VS_EPI_GATE_RES) {
+                float gv[8];
+                unpack8(*reinterpret_cast<const u32x4_t*>(gr + ch * 8), gv);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[c][e] = rbf(xv[e] + rbf(gv[e] * yv[e]));
+                if (hint) {
+                    float hv[8];
+                    unpack8(*reinterpret_cast<const u32x4_t*>(hint + row * ld_hint + ch * 8), hv);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[c][e] = v[c][e] + rbf(hv[e] * hint_scale);
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[c][e] = xv[e] + rbf(alpha * yv[e]);
+            }
+            const u32x4_t pk = pack8(v[c]);
+            *reinterpret_cast<u32x4_t*>(xr + ch * 8) = pk;
+            unpack8(pk, v[c]);                           // LayerNorm reads the stored bf16 row
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s += v[c][e];
+        }
+    }
+    const float mean = block_sum(s, red) / dim;
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXCH; ++c) {
+        const int ch = threadIdx.x + c * RT;
+        if (ch < nch) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float d = v[c][e] - mean;
+                q += d * d;
+            }
+        }
+    }
+    const float rstd = rsqrtf(block_sum(q, red) / dim + eps);
+    const long long bidx = row / rpb;
+    bf16_t* orow = out + row * ldo;
+#pragma unroll
+    for (int c = 0; c < MAXCH; ++c) {
+        const int ch = threadIdx.x + c * RT;
+        if (ch >= nch) continue;
+        float o8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o8[e] = (v[c][e] - mean) * rstd;
+        if (w) {
+            float wv[8], bv[8];
+            unpack8(*reinterpret_cast<const u32x4_t*>(w + ch * 8), wv);
+            unpack8(*reinterpret_cast<const u32x4_t*>(bb + ch * 8), bv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o8[e] = o8[e] * wv[e] + bv[e];
+        }
+        if (shift) {
+            float sh[8], sc[8];
+            unpack8(*reinterpret_cast<const u32x4_t*>(shift + bidx * mbs + ch * 8), sh);
+            unpack8(*reinterpret_cast<const u32x4_t*>(scale + bidx * mbs + ch * 8), sc);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o8[e] = rbf(rbf(rbf(o8[e]) * rbf(1.f + sc[e])) + sh[e]);
+        }
+        *reinterpret_cast<u32x4_t*>(orow + ch * 8) = pack8(o8);
+    }
+}
+
 // RMSNorm over the full row (wan_video_dit.py:106-111) + interleaved 3-D RoPE (:92-97)
 __global__ __launch_bounds__(RT) void rmsnorm_rope_kernel(
     bf16_t* __restrict__ x, long long ldx, int dim, int hd, const bf16_t* __restrict__ w, float eps,
@@ -345,6 +434,34 @@ extern "C" int vs_layernorm_modulate(const void* x, long long ldx, void* out, lo
                        (const bf16_t*)x, ldx, (bf16_t*)out, ldo, dim, rows_per_batch,
                        (const bf16_t*)shift, (const bf16_t*)scale, mod_bstride,
                        (const bf16_t*)weight, (const bf16_t*)bias, eps);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_residual_layernorm(const void* y, long long ldy, void* x, long long ldx, void* out, long long ldo,
+                                     int rows, int dim, int epilogue, const vs_epilogue* epi, int rows_per_batch,
+                                     const void* shift, const void* scale, long long mod_bstride,
+                                     const void* weight, const void* bias, float eps, void* stream) {
+    if (!y || !x || !out || !epi || rows <= 0 || dim <= 0 || dim % 8 || dim > MAXCH * RT * 8) return VS_E_INVALID;
+    if (epilogue != VS_EPI_GATE_RES && epilogue != VS_EPI_RES) return VS_E_INVALID;
+    if (ldy < dim || ldx < dim || ldo < dim || ((ldy | ldx | ldo) & 7) || !al16(y) || !al16(x) || !al16(out))
+        return VS_E_INVALID;
+    if (epilogue == VS_EPI_GATE_RES) {
+        if (!epi->gate || !al16(epi->gate) || (epi->gate_bstride & 7)) return VS_E_INVALID;
+        if (epi->hint && (!al16(epi->hint) || (epi->ld_hint & 7) || epi->ld_hint < dim)) return VS_E_INVALID;
+    }
+    if ((shift == nullptr) != (scale == nullptr) || (weight == nullptr) != (bias == nullptr)) return VS_E_INVALID;
+    if (shift && (!al16(shift) || !al16(scale) || (mod_bstride & 7))) return VS_E_INVALID;
+    if (weight && (!al16(weight) || !al16(bias))) return VS_E_INVALID;
+    const int rpb_gate = epi->rows_per_batch > 0 ? epi->rows_per_batch : rows;
+    if (rows_per_batch <= 0) rows_per_batch = rows;
+    const bool gated = epilogue == VS_EPI_GATE_RES;
+    hipLaunchKernelGGL(residual_ln_kernel, dim3(rows), dim3(RT), 0, (hipStream_t)stream, (const bf16_t*)y, ldy,
+                       (bf16_t*)x, ldx, (bf16_t*)out, ldo, dim, epilogue,
+                       gated ? (const bf16_t*)epi->gate : nullptr, epi->gate_bstride, rpb_gate, epi->alpha,
+                       gated ? (const bf16_t*)epi->hint : nullptr, epi->ld_hint, epi->hint_scale, rows_per_batch,
+                       (const bf16_t*)shift, (const bf16_t*)scale, mod_bstride, (const bf16_t*)weight,
+                       (const bf16_t*)bias, eps);
     VS_CHECK_LAUNCH();
     return VS_OK;
 }

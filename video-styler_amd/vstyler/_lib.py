@@ -64,6 +64,8 @@ SIGNATURES = {
     "vs_split_workspace_bytes": [_I],
     "vs_split_workspace_bind": [_I, _P, _LL, _P],
     "vs_layernorm_modulate": [_P, _LL, _P, _LL, _I, _I, _I, _P, _P, _LL, _P, _P, _F, _P],
+    "vs_residual_layernorm": [_P, _LL, _P, _LL, _P, _LL, _I, _I, _I, ctypes.POINTER(VsEpilogue), _I, _P, _P, _LL,
+                              _P, _P, _F, _P],
     "vs_rmsnorm_rope": [_P, _LL, _I, _I, _I, _P, _F, _P, _I, _I, _I, _I, _I, _I, _P],
     "vs_patchify": [_P, _P, _I, _I, _I, _I, _I, _P],
     "vs_unpatchify": [_P, _P, _I, _I, _I, _I, _I, _P],

@@ -133,7 +133,7 @@ def quant_fp8_rows(x, x8, scale):
 def _lt_route(M, N, K):
     """vs_gemm's routing decision (vs_gemm_route): the shim binds the epilogue staging buffer for
     GEMMs that go to hipBLASLt."""
-    return _lib.load().vs_gemm_route(int(M), int(N), int(K)) == 1
+    return gemm_route(M, N, K)
 
 
 def gemm_fp8(a8, scale_a, w8, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, gate_bstride=0,
@@ -197,6 +197,28 @@ def layernorm_modulate(x, out, eps=1e-6, shift=None, scale=None, mod_bstride=0, 
                                                  _ptr(shift), _ptr(scale), int(mod_bstride), _ptr(weight),
                                                  _ptr(bias), float(eps), _stream(x)))
     return out
+
+
+def residual_layernorm(y, x, out, eps=1e-6, epilogue=VS_EPI_GATE_RES, gate=None, gate_bstride=0, gate_rows=0,
+                       alpha=1.0, hint=None, hint_scale=1.0, shift=None, scale=None, mod_bstride=0,
+                       rows_per_batch=0, weight=None, bias=None):
+    """x = epilogue(y, x) (gate-residual / residual of a staged projection y), then
+    out = layernorm_modulate(x) -- one pass (vs_residual_layernorm)."""
+    M, D, ldy = _rows(y, "y")
+    Mx, Dx, ldx = _rows(x, "x")
+    Mo, Do, ldo = _rows(out, "out")
+    if (Mx, Dx) != (M, D) or (Mo, Do) != (M, D):
+        raise ValueError("residual_layernorm: shape mismatch")
+    ep = _epilogue(None, None, gate, gate_bstride, hint, hint_scale, alpha, gate_rows)
+    _lib.check(_lib.load().vs_residual_layernorm(y.data_ptr(), ldy, x.data_ptr(), ldx, out.data_ptr(), ldo, M, D,
+                                                 int(epilogue), ep, int(rows_per_batch), _ptr(shift), _ptr(scale),
+                                                 int(mod_bstride), _ptr(weight), _ptr(bias), float(eps), _stream(x)))
+    return out
+
+
+def gemm_route(M, N, K):
+    """1 if vs_gemm sends an (M, N, K) GEMM without LoRA phase to hipBLASLt (vs_gemm_route)."""
+    return _lib.load().vs_gemm_route(int(M), int(N), int(K)) == 1
 
 
 def rmsnorm_rope(x, weight, eps=1e-6, rope=None, grid=(1, 1, 1), rows_per_batch=0, token_offset=0, head_dim=128):

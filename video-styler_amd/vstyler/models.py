@@ -9,6 +9,7 @@ Reference: diffsynth/models/wan_video_dit.py (DiTBlock :196-230, Head :253-269, 
 (diffsynth/pipelines/wan_video_new.py:1260-1468).
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -53,6 +54,17 @@ def linear(lin, x, out, ws, **epi):
         K.gemm(x, la, t)
         a2, w2 = t, lin.lora_B
     return K.gemm(x, lin.weight, out, bias=lin.bias, a2=a2, w2=w2, **epi)
+
+
+def _fusable_lt(lin, M):
+    """True when `lin` on M rows runs as a plain bf16 GEMM on vs_gemm's hipBLASLt route (no fp8 copy,
+    no hot-loaded LoRA): its residual epilogue can then fuse with the LayerNorm that follows
+    (vs_residual_layernorm).  VSTYLER_FUSE_RES_LN=0 disables."""
+    if getattr(lin, "weight_fp8", None) is not None or getattr(lin, "lora_A", None) is not None:
+        return False
+    if os.environ.get("VSTYLER_FUSE_RES_LN", "1") == "0":
+        return False
+    return K.gemm_route(M, lin.out_features, lin.in_features)
 
 
 def quantize_fp8_(module):
@@ -331,10 +343,17 @@ class DiTBlock(nn.Module):
         if rc.sp is not None:
             rc.sp.finish(p["xchg"], o)
         sa = self.self_attn
-        linear(sa.o, o, x, ws, epilogue=K.VS_EPI_GATE_RES, residual=x, gate=mod[:, 2],
-               gate_bstride=6 * D, rows_per_batch=S)
-        # --- cross-attention (wan_video_dit.py:227, :171-186)
-        K.layernorm_modulate(x, h, eps, weight=self.norm3.weight, bias=self.norm3.bias)
+        if _fusable_lt(sa.o, M):
+            # hipBLASLt route: bf16(o Wo^T + b) staged, then gate-residual + LN3 in one pass
+            y = ws.get("res_y" + p["tag"], (M, D))
+            K.gemm(o, sa.o.weight, y, bias=sa.o.bias)
+            K.residual_layernorm(y, x, h, eps, epilogue=K.VS_EPI_GATE_RES, gate=mod[:, 2], gate_bstride=6 * D,
+                                 gate_rows=S, weight=self.norm3.weight, bias=self.norm3.bias)
+        else:
+            linear(sa.o, o, x, ws, epilogue=K.VS_EPI_GATE_RES, residual=x, gate=mod[:, 2],
+                   gate_bstride=6 * D, rows_per_batch=S)
+            # --- cross-attention (wan_video_dit.py:227, :171-186)
+            K.layernorm_modulate(x, h, eps, weight=self.norm3.weight, bias=self.norm3.bias)
         ca = self.cross_attn
         L = rc.ctx_len
         linear(ca.q, h, q, ws)
@@ -348,9 +367,15 @@ class DiTBlock(nn.Module):
             linear(ca.v, p["ctx"], vc, ws)
         K.rmsnorm_rope(kc, ca.norm_k.weight, eps)
         K.attention(q, kc, vc, o, self.num_heads, nb)
-        linear(ca.o, o, x, ws, epilogue=K.VS_EPI_RES, residual=x)
-        # --- FFN (wan_video_dit.py:228-229) + VACE hint (wan_video_new.py:1450)
-        K.layernorm_modulate(x, h, eps, shift=mod[:, 3], scale=mod[:, 4], mod_bstride=6 * D, rows_per_batch=S)
+        if _fusable_lt(ca.o, M):
+            y = ws.get("res_y" + p["tag"], (M, D))
+            K.gemm(o, ca.o.weight, y, bias=ca.o.bias)
+            K.residual_layernorm(y, x, h, eps, epilogue=K.VS_EPI_RES, alpha=1.0, shift=mod[:, 3], scale=mod[:, 4],
+                                 mod_bstride=6 * D, rows_per_batch=S)
+        else:
+            linear(ca.o, o, x, ws, epilogue=K.VS_EPI_RES, residual=x)
+            # --- FFN (wan_video_dit.py:228-229) + VACE hint (wan_video_new.py:1450)
+            K.layernorm_modulate(x, h, eps, shift=mod[:, 3], scale=mod[:, 4], mod_bstride=6 * D, rows_per_batch=S)
         f = ws.get("f" + p["tag"], (M, self.ffn_dim))
         linear(self.ffn[0], h, f, ws, epilogue=K.VS_EPI_GELU)
         linear(self.ffn[2], f, x, ws, epilogue=K.VS_EPI_GATE_RES, residual=x,
