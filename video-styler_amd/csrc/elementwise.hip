@@ -186,59 +186,109 @@ __global__ __launch_bounds__(RT) void residual_ln_kernel(
     }
 }
 
-// RMSNorm over the full row (wan_video_dit.py:106-111) + interleaved 3-D RoPE (:92-97)
+// NR row sums at once: the same shuffle tree and slot order as block_sum, one barrier pair
+template <int NR>
+__device__ __forceinline__ void block_sum_n(float* v, float* red) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v[i] += __shfl_xor(v[i], o);
+    __syncthreads();
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < NR; ++i) red[i * (RT / 64) + w] = v[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < RT / 64; ++k) t += red[i * (RT / 64) + k];
+        v[i] = t;
+    }
+}
+
+// RMSNorm over the full row (wan_video_dit.py:106-111) + interleaved 3-D RoPE (:92-97).
+// NR rows per block (VS_RMS_ROWS, default 1): their loads all issue before the one reduction.
+// Measured at the 14B shape on q|k|v slices (tests/probes/rownorm_ab.py, profiles/r1/rownorm_ab_r1s.log):
+// NR = 1 262 us, 2 270 us, 4 331 us -- more rows per block cost occupancy, not latency.  The
+// LDS-gathered RoPE pairs took NR = 1 from 294 us (4 global 8-B gathers per 16-B chunk) to 262 us.
+template <int NR>
 __global__ __launch_bounds__(RT) void rmsnorm_rope_kernel(
-    bf16_t* __restrict__ x, long long ldx, int dim, int hd, const bf16_t* __restrict__ w, float eps,
-    const float2* __restrict__ rope, int rope_len, int gf, int gh, int gw, int rpb, int tok_off) {
-    __shared__ float red[RT / 64];
-    const long long row = blockIdx.x;
+    bf16_t* __restrict__ x, long long ldx, int rows, int dim, int hd, const bf16_t* __restrict__ w, float eps,
+    const float2* __restrict__ rope, int gf, int gh, int gw, int rpb, int tok_off) {
+    __shared__ float red[NR * (RT / 64)];
+    __shared__ __attribute__((aligned(16))) float2 rc[NR][64];   // each row's 64 RoPE pairs (hd = 128)
+    const long long row0 = (long long)blockIdx.x * NR;
+    const int nr = (int)min((long long)NR, rows - row0);
     const int nch = dim >> 3;
-    bf16_t* xr = x + row * ldx;
-    float v[MAXCH][8];
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < MAXCH; ++c) {
-        const int ch = threadIdx.x + c * RT;
-        if (ch < nch) {
-            unpack8(*reinterpret_cast<const u32x4_t*>(xr + ch * 8), v[c]);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) s += v[c][e] * v[c][e];
-        }
-    }
-    const float r = rsqrtf(block_sum(s, red) / dim + eps);
-    int pf = 0, ph = 0, pw = 0;
-    if (rope) {
-        const int t = (int)(row % rpb) + tok_off;
-        pw = t % gw;
-        ph = (t / gw) % gh;
-        pf = t / (gw * gh);
-    }
     const int half = hd >> 1;
     const int tdim = half - 2 * (hd / 3 / 2);   // 22 temporal pairs for hd=128
     const int hdim = hd / 3 / 2;                 // 21
+    if (rope && threadIdx.x < half) {
+        // the row's (f, h, w) picks one table row per pair group: gathered once per row into LDS
+        // (visible after the reduction's barriers) instead of 4 scattered 8-B loads per 16-B chunk
+        const int j = threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            if (i >= nr) break;
+            const int t = (int)((row0 + i) % rpb) + tok_off;
+            const int pos = j < tdim ? t / (gw * gh) : (j < tdim + hdim ? (t / gw) % gh : t % gw);
+            rc[i][j] = rope[(long long)pos * half + j];
+        }
+    }
+    float v[NR][MAXCH][8];
+    float s[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        s[i] = 0.f;
+        if (i >= nr) continue;
+        const bf16_t* xr = x + (row0 + i) * ldx;
+#pragma unroll
+        for (int c = 0; c < MAXCH; ++c) {
+            const int ch = threadIdx.x + c * RT;
+            if (ch < nch) unpack8(*reinterpret_cast<const u32x4_t*>(xr + ch * 8), v[i][c]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+#pragma unroll
+        for (int c = 0; c < MAXCH; ++c) {
+            const int ch = threadIdx.x + c * RT;
+            if (i < nr && ch < nch)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) s[i] += v[i][c][e] * v[i][c][e];
+        }
+    block_sum_n<NR>(s, red);
 #pragma unroll
     for (int c = 0; c < MAXCH; ++c) {
         const int ch = threadIdx.x + c * RT;
         if (ch >= nch) continue;
-        float wv[8], y[8];
+        float wv[8];
         unpack8(*reinterpret_cast<const u32x4_t*>(w + ch * 8), wv);
+        const int pair0 = ((ch * 8) % hd) >> 1;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) y[e] = rbf(rbf(v[c][e] * r) * wv[e]);
-        if (rope) {
-            const int pair0 = ((ch * 8) % hd) >> 1;
+        for (int i = 0; i < NR; ++i) {
+            if (i >= nr) break;
+            const float r = rsqrtf(s[i] / dim + eps);
+            float y[8];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int j = pair0 + e;
-                const int pos = j < tdim ? pf : (j < tdim + hdim ? ph : pw);
-                const float2 cs = rope[(long long)pos * half + j];
-                const float a = y[2 * e], b = y[2 * e + 1];
-                y[2 * e] = a * cs.x - b * cs.y;
-                y[2 * e + 1] = a * cs.y + b * cs.x;
+            for (int e = 0; e < 8; ++e) y[e] = rbf(rbf(v[i][c][e] * r) * wv[e]);
+            if (rope) {
+                const f32x4_t c01 = *reinterpret_cast<const f32x4_t*>(&rc[i][pair0]);
+                const f32x4_t c23 = *reinterpret_cast<const f32x4_t*>(&rc[i][pair0 + 2]);
+                const float2 css[4] = {{c01[0], c01[1]}, {c01[2], c01[3]}, {c23[0], c23[1]}, {c23[2], c23[3]}};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float2 cs = css[e];
+                    const float a = y[2 * e], b = y[2 * e + 1];
+                    y[2 * e] = a * cs.x - b * cs.y;
+                    y[2 * e + 1] = a * cs.y + b * cs.x;
+                }
             }
+            *reinterpret_cast<u32x4_t*>(x + (row0 + i) * ldx + ch * 8) = pack8(y);
         }
-        *reinterpret_cast<u32x4_t*>(xr + ch * 8) = pack8(y);
     }
-    (void)rope_len;
 }
 
 // Conv3d (1,2,2) im2col: one thread per (token, channel) writes 4 contiguous columns
@@ -481,9 +531,13 @@ extern "C" int vs_rmsnorm_rope(void* x, long long ldx, int rows, int dim, int he
             return VS_E_INVALID;
     }
     if (rows_per_batch <= 0) rows_per_batch = rows;
-    hipLaunchKernelGGL(rmsnorm_rope_kernel, dim3(rows), dim3(RT), 0, (hipStream_t)stream,
-                       (bf16_t*)x, ldx, dim, head_dim, (const bf16_t*)weight, eps,
-                       (const float2*)rope, rope_len, gf, gh, gw, rows_per_batch, token_offset);
+#ifndef VS_RMS_ROWS
+#define VS_RMS_ROWS 1
+#endif
+    constexpr int NR = VS_RMS_ROWS;
+    hipLaunchKernelGGL(rmsnorm_rope_kernel<NR>, dim3((unsigned)((rows + NR - 1) / NR)), dim3(RT), 0,
+                       (hipStream_t)stream, (bf16_t*)x, ldx, rows, dim, head_dim, (const bf16_t*)weight, eps,
+                       (const float2*)rope, gf, gh, gw, rows_per_batch, token_offset);
     VS_CHECK_LAUNCH();
     return VS_OK;
 }
