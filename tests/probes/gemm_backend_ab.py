@@ -14,10 +14,17 @@ def timed(fn, reps=5):
     return sorted(ts)[reps // 2]
 
 
-for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
-    for name, N, Kd, epi in (("qkv", 15360, 5120, K.VS_EPI_BIAS), ("o-proj", 5120, 5120, K.VS_EPI_GATE_RES),
-                             ("cross-q", 5120, 5120, K.VS_EPI_BIAS), ("cross-o", 5120, 5120, K.VS_EPI_RES),
-                             ("ffn-up", 13824, 5120, K.VS_EPI_GELU), ("ffn-down", 5120, 13824, K.VS_EPI_GATE_RES)):
+# "ctx": the per-step context GEMMs (fused cross k|v over the CFG batch's 2 x 512 context rows)
+CTX = sys.argv[1:2] == ["ctx"]
+SHAPES = ((("cross-kv", 10240, 5120, K.VS_EPI_BIAS), ("text-1", 5120, 4096, K.VS_EPI_GELU),
+           ("text-2", 5120, 5120, K.VS_EPI_BIAS), ("t5-attn", 4096, 4096, K.VS_EPI_BIAS),
+           ("t5-ffn", 10240, 4096, K.VS_EPI_BIAS), ("time-proj", 30720, 5120, K.VS_EPI_BIAS),
+           ("1.3B-kv", 3072, 1536, K.VS_EPI_BIAS)) if CTX else
+          (("qkv", 15360, 5120, K.VS_EPI_BIAS), ("o-proj", 5120, 5120, K.VS_EPI_GATE_RES),
+           ("cross-q", 5120, 5120, K.VS_EPI_BIAS), ("cross-o", 5120, 5120, K.VS_EPI_RES),
+           ("ffn-up", 13824, 5120, K.VS_EPI_GELU), ("ffn-down", 5120, 13824, K.VS_EPI_GATE_RES)))
+for M in (1024, 512, 2) if CTX else ([int(v) for v in sys.argv[1:]] or (59280, 7410)):
+    for name, N, Kd, epi in SHAPES:
         a = torch.randn(M, Kd, device="cuda").to(torch.bfloat16)
         w = (0.05 * torch.randn(N, Kd, device="cuda")).to(torch.bfloat16)
         b = (0.1 * torch.randn(N, device="cuda")).to(torch.bfloat16)

@@ -136,8 +136,9 @@ def test_gemm_split_plan_host_only():
 
 
 def test_gemm_route_rule(monkeypatch):
-    """vs_gemm_route: hipBLASLt for grids of >= 1024 256x256 tiles, or >= 256 tiles with K <= 8192
-    (gemm.hip lt_route, measured in profiles/r1/gemm_backend_ab_r1j.log); VS_GEMM_BACKEND forces."""
+    """vs_gemm_route: hipBLASLt for grids of >= 1024 256x256 tiles, or >= 256 tiles with K <= 8192,
+    or smaller grids with N >= 2048 and 1024 <= K <= 8192 (gemm.hip lt_route, measured in
+    profiles/r1/gemm_backend_ab_r1j.log and gemm_backend_ab_ctx_r1s.log); VS_GEMM_BACKEND forces."""
     from vstyler import _lib
     lib = _lib.load()
     monkeypatch.delenv("VS_GEMM_BACKEND", raising=False)
@@ -145,7 +146,12 @@ def test_gemm_route_rule(monkeypatch):
     assert lib.vs_gemm_route(7410, 5120, 5120) == 1         # 580 tiles, K 5120
     assert lib.vs_gemm_route(3705, 5120, 5120) == 1         # 300 tiles
     assert lib.vs_gemm_route(7410, 5120, 13824) == 0        # 580 tiles, K 13824
-    assert lib.vs_gemm_route(1024, 10240, 5120) == 0        # 160 tiles
+    assert lib.vs_gemm_route(1024, 10240, 5120) == 1        # 160 tiles: cross k|v over the context
+    assert lib.vs_gemm_route(2, 30720, 5120) == 1           # time projection
+    assert lib.vs_gemm_route(512, 4096, 10240) == 0         # 32 tiles, K 10240 (UMT5 FFN-down)
+    assert lib.vs_gemm_route(59280, 64, 5120) == 0          # head: 232 tiles, N 64
+    assert lib.vs_gemm_route(59280, 5120, 64) == 1          # patch embedding: 4640 tiles
+    assert lib.vs_gemm_route(1024, 1536, 4096) == 0         # 24 tiles, N 1536
     assert lib.vs_gemm_route(0, 1, 1) == _lib.VS_E_INVALID if hasattr(_lib, "VS_E_INVALID") else lib.vs_gemm_route(0, 1, 1) != 0
     monkeypatch.setenv("VS_GEMM_BACKEND", "vstyler")
     assert lib.vs_gemm_route(59280, 5120, 5120) == 0

@@ -963,13 +963,17 @@ KSplit plan_ksplit(int ntiles, int nh, int cus) {
 // per 14B block GEMM (profiles/r1/gemm_lt_tune_r1i.log, gemm_backend_ab_r1j.log): hipBLASLt wins on
 // every grid of >= 1024 256^2 tiles, and on 256-1023-tile grids (the SP=8 row counts 7410 and, per
 // CFG micro-batch, 3705) while K <= 8192 (1.01-1.32x); the K = 13824 FFN-down GEMM at those sizes
-// stays on the MFMA kernel (0.88-0.96x on hipBLASLt).
+// stays on the MFMA kernel (0.88-0.96x on hipBLASLt).  Grids of < 256 tiles with N >= 2048 and
+// 1024 <= K <= 8192 -- the per-step context GEMMs (fused cross k|v over 2 x 512 context rows, text
+// embedding), the time projection (M = 2) and the UMT5 layers -- also go to hipBLASLt: 1.05-2.4x
+// the 128^2 kernel (profiles/r1/gemm_backend_ab_ctx_r1s.log); the narrow head (N = 64) and the
+// patch embeddings (K = 64 / 384) are unmeasured there and stay on the MFMA kernels.
 static bool lt_route(int m, int n, int k) {
     const char* e = getenv("VS_GEMM_BACKEND");
     const int mode = !e ? 2 : (e[0] == 'v' ? 0 : (e[0] == 'l' ? 1 : 2));   // 0 never, 1 always, 2 auto
     if (mode != 2) return mode == 1;
     const long long tiles = (long long)((m + 255) / 256) * ((n + 255) / 256);
-    return tiles >= 1024 || (tiles >= 256 && k <= 8192);
+    return tiles >= 1024 || (k <= 8192 && (tiles >= 256 || (n >= 2048 && k >= 1024)));
 }
 
 // hipBLASLt for bf16(A W^T [* scale] + bias) (gemm(y, ldy)), then the rest of the epilogue with
