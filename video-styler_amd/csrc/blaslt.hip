@@ -16,6 +16,7 @@
 
 #include <hipblaslt/hipblaslt.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -88,11 +89,14 @@ LtPlan* plan_for(const LtKey& key, size_t ws_bytes) {
     if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return nullptr;
     const uint64_t wsb = ws_bytes;
     hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
-    constexpr int NCAND = 16;
-    hipblasLtMatmulHeuristicResult_t res[NCAND];
+    // candidates the autotune times: 16 (VS_LT_NCAND = 1..64 for A/B runs)
+    constexpr int MAXCAND = 64;
+    int ncand = 16;
+    if (const char* e = std::getenv("VS_LT_NCAND")) ncand = std::min(MAXCAND, std::max(1, std::atoi(e)));
+    hipblasLtMatmulHeuristicResult_t res[MAXCAND];
     int found = 0;
     const hipblasStatus_t st =
-        hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.lw, p.la, p.lc, p.lc, pref, NCAND, res, &found);
+        hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.lw, p.la, p.lc, p.lc, pref, ncand, res, &found);
     hipblasLtMatmulPreferenceDestroy(pref);
     if (st != HIPBLAS_STATUS_SUCCESS || found < 1) return nullptr;
     p.cand.assign(res, res + found);
