@@ -374,11 +374,13 @@ def denoise(W, cfg, latents, context_pos, context_neg, vace_context=None, num_in
 # fp8 linear (AutoWrappedLinear.fp8_linear, vram_management/layers.py:115-151; e4m3fn, OCP)
 # --------------------------------------------------------------------------------------
 def fp8_quant_rows(x):
-    """layers.py:124-135: scale_a = clamp(rowmax|x| / 448, min=1) (fp32), x8 = (x / (scale_a + 1e-8))
-    cast to float8_e4m3fn.  Returns (x8 as float8_e4m3fn, scale_a [M, 1] fp32)."""
+    """layers.py:124-135: scale_a = clamp(rowmax|x| / 448, min=1).float() -- the division and the
+    clamp run on the bf16 x_max, so the quotient is rounded to bf16 before the clamp (:130-134) --
+    then x8 = (x / (scale_a + 1e-8)) in fp32 (bf16 / fp32 tensors promote), cast to float8_e4m3fn.
+    Returns (x8 as float8_e4m3fn, scale_a [M, 1] fp32)."""
     x2 = x.reshape(-1, x.shape[-1])
     x_max = torch.max(torch.abs(x2), dim=-1, keepdim=True).values
-    scale_a = torch.clamp(x_max.float() / 448.0, min=1.0)
+    scale_a = torch.clamp(x_max.to(BF16) / 448.0, min=1.0).float()
     x8 = (x2.float() / (scale_a + 1e-8)).to(torch.float8_e4m3fn)
     return x8, scale_a
 

@@ -63,3 +63,17 @@ def test_quantize_fp8_keeps_fusion():
     assert torch.equal(W8[256:512], blk.self_attn.k.weight_fp8)
     ref = blk.self_attn.k.weight.detach().to(torch.float8_e4m3fn).view(torch.uint8)
     assert torch.equal(blk.self_attn.k.weight_fp8, ref)
+
+
+def test_fp8_row_scale_rounds_quotient_to_bf16():
+    """fp8_linear (layers.py:130-134) divides and clamps the bf16 row max: the scale is
+    bf16(max|x| / 448) clamped at 1, not the fp32 quotient."""
+    from oracle import wan_oracle as O
+    x = torch.zeros(3, 64, dtype=BF16)
+    x[0, 5] = 1000.0      # 1000 / 448 = 2.2321...: bf16 2.234375
+    x[1, 7] = -3000.0     # 6.6964... -> bf16 6.71875
+    x[2, 1] = 100.0       # below 448: clamp to 1
+    _, s = O.fp8_quant_rows(x)
+    assert s.dtype == torch.float32
+    assert torch.equal(s.view(-1), torch.tensor([2.234375, 6.71875, 1.0]))
+    assert s[0].item() != 1000.0 / 448.0

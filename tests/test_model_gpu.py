@@ -146,6 +146,66 @@ def test_lora_merge_and_hotload():
     assert err(out, ref)[1] < 1e-2
 
 
+def test_two_hotloaded_loras_add_up():
+    """Two hot-loads on one Linear accumulate like the reference's lora_A_weights / lora_B_weights
+    lists (layers.py:180-182, forward :183-185: out + x A1^T B1^T + x A2^T B2^T); ranks 32 and 96
+    (padded to 64 and 128, stacked into one K phase)."""
+    from vstyler.lora import hotload_lora
+    from vstyler.models import Linear, Workspace, linear
+    import torch.nn as nn
+    g = torch.Generator().manual_seed(92)
+    D = 256
+    m = nn.Module()
+    m.add_module("q", Linear(D, D, device="cuda"))
+    w = (0.05 * torch.randn(D, D, generator=g)).to(BF16)
+    b = (0.01 * torch.randn(D, generator=g)).to(BF16)
+    m.q.weight.data.copy_(w)
+    m.q.bias.data.copy_(b)
+    adapters = []
+    for r, alpha in ((32, 0.7), (96, 1.3)):
+        up = (0.05 * torch.randn(D, r, generator=g)).to(BF16)
+        down = (0.05 * torch.randn(r, D, generator=g)).to(BF16)
+        assert hotload_lora(m, {"q.lora_A.default.weight": down, "q.lora_B.default.weight": up}, alpha=alpha) == 1
+        adapters.append((O.bf(down.float() * alpha), up))
+    assert m.q.lora_A.shape == (64 + 128, D) and m.q.lora_B.shape == (D, 64 + 128)
+    x = torch.randn(100, D, generator=g).to(BF16)
+    out = torch.empty(100, D, dtype=BF16, device="cuda")
+    linear(m.q, x.cuda(), out, Workspace("cuda"))
+    ref = O.linear(x, w, b)
+    for a_s, up in adapters:                     # the reference's loop: one bf16 add per adapter
+        t = O.bf(x.float() @ a_s.float().t())
+        ref = O.bf(ref.float() + O.bf(t.float() @ up.float().t()).float())
+    one = O.lora_linear(x, w, b, *adapters[0])
+    assert err(one, ref)[1] > 1e-2               # the second adapter is not negligible
+    assert err(out, ref)[1] < 1e-2
+
+
+def test_merge_lora_after_fp8_quantisation_refreshes_e4m3_copy():
+    """merge_lora on a layer quantize_fp8_ already converted rewrites its e4m3 copy (which
+    linear() reads instead of the bf16 weight), including the fused q|k|v e4m3 buffer views."""
+    from vstyler.lora import merge_lora
+    from vstyler.models import quantize_fp8_, _fused_views
+    cfg = O.WAN_CONFIGS["tiny"]
+    W = O.random_weights(cfg, seed=5)
+    dit, vace = build(cfg, W)
+    quantize_fp8_(vace)
+    g = torch.Generator().manual_seed(93)
+    D, r = cfg["dim"], 32
+    lora = {}
+    for n in ("vace_blocks.0.self_attn.k", "vace_blocks.0.ffn.0"):
+        lin_out = cfg["ffn_dim"] if n.endswith("ffn.0") else D
+        lora[n + ".lora_A.default.weight"] = (0.05 * torch.randn(r, D, generator=g)).to(BF16)
+        lora[n + ".lora_B.default.weight"] = (0.05 * torch.randn(lin_out, r, generator=g)).to(BF16)
+    assert merge_lora(vace, lora, alpha=1.0) == 2
+    blk = vace.vace_blocks[0]
+    for lin in (blk.self_attn.k, blk.ffn[0]):
+        want = lin.weight.detach().to(torch.float8_e4m3fn).view(torch.uint8)
+        assert torch.equal(lin.weight_fp8, want)
+    assert _fused_views(blk.self_attn) is not None
+    fw8 = blk.self_attn._fw8
+    assert torch.equal(fw8[D:2 * D], blk.self_attn.k.weight.detach().to(torch.float8_e4m3fn).view(torch.uint8))
+
+
 def test_denoise_graph_replay_bit_identical_to_eager(tiny):
     """The hipGraph-captured step (captured once, replayed with per-step timestep/dsigma slots)
     gives exactly the eager loop's latents (same kernels, same order)."""

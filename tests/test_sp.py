@@ -129,9 +129,12 @@ def test_ulysses_sp2_model_bit_identical_on_one_gpu():
 
 
 def _rccl_worker(port, q):
-    """World size 1 over the 'nccl' backend (RCCL): the product UlyssesGroup's device-side
-    all_to_all_single (async, waited on the current stream) and all_gather_into_tensor run for real.
-    Multi-rank RCCL needs one GPU per rank, which the 8-GPU scaling bench covers."""
+    """World size 1 over the 'nccl' backend (RCCL): the product UlyssesGroup with
+    force_collectives, so model_fn_wan_video takes the sharded path and the device-side
+    all_to_all_single (async, waited on the current stream, under both overlap schedules) and
+    all_gather_into_tensor run for real; plus the three attention stages and the token gather
+    driven directly.  Multi-rank RCCL needs one GPU per rank (the driver's 8-GPU bench); the
+    multi-rank orchestration is covered by the gloo tests above."""
     try:
         import sys
         for p in (ROOT, os.path.join(ROOT, "video-styler_amd"), os.path.join(ROOT, "tests")):
@@ -140,11 +143,33 @@ def _rccl_worker(port, q):
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
                           LOCAL_RANK="0")
         from oracle import wan_oracle as O
+        from vstyler import kernels as K
         from vstyler import model_fn_wan_video
+        from vstyler.models import RunCtx, Workspace
         from vstyler.usp import UlyssesGroup, init_distributed
         from test_model_gpu import build
         init_distributed()
         assert torch.distributed.get_backend() == "nccl"
+        res = {}
+        # (1) the stages driven directly: exchange_start -> attend -> finish == plain attention
+        g = torch.Generator().manual_seed(7)
+        B, S, H = 2, 320, 2
+        D = H * 128
+        qkv = (torch.randn(B * S, 3 * D, generator=g)).to(torch.bfloat16).cuda()
+        qq, kk, vv = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+        ref = torch.empty(B * S, D, dtype=torch.bfloat16, device="cuda")
+        K.attention(qq, kk, vv, ref, H, B)
+        sp = UlyssesGroup(force_collectives=True)
+        o = torch.empty_like(ref)
+        sp.finish(sp.attend(sp.exchange_start(qq, kk, vv, H, B, tag="t")), o)
+        torch.cuda.synchronize()
+        res["stages"] = torch.equal(o, ref) and sp.collective_calls == 2
+        rc = RunCtx(B, S, (1, 1, S), None, None, 0, Workspace("cuda"))
+        xl, _, rc2 = sp.shard_tokens(ref, None, rc)
+        full = sp.gather_tokens(xl[:, :64].contiguous(), rc2)
+        torch.cuda.synchronize()
+        res["gather"] = torch.equal(full, ref[:, :64]) and sp.collective_calls == 3
+        # (2) the whole model through the sharded path, both schedules
         cfg = O.WAN_CONFIGS["tiny"]
         W = O.random_weights(cfg, seed=5)
         dit, vace = build(cfg, W, "cuda:0")
@@ -152,16 +177,20 @@ def _rccl_worker(port, q):
         t = torch.tensor([833.3333]).to(torch.bfloat16).cuda()
         ctx = torch.cat([cp, cn]).cuda()
         single = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx, vace_context=vc.cuda())
-        same = True
         for overlap in (True, False):
-            sp = UlyssesGroup()
+            sp = UlyssesGroup(force_collectives=True)
             sp.overlap = overlap
             par = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx,
                                      vace_context=vc.cuda(), use_unified_sequence_parallel=True, sp_group=sp)
             torch.cuda.synchronize()
-            same = same and torch.equal(single.cpu(), par.cpu())
+            # 2 all-to-alls per self-attention (x2 micro-batches with overlap) + 1 gather
+            nblk = cfg["num_layers"] + len(cfg["vace_layers"])
+            want_calls = nblk * 2 * (2 if overlap else 1) + 1
+            res[f"model_overlap{int(overlap)}"] = torch.equal(single.cpu(), par.cpu()) and \
+                sp.collective_calls == want_calls
+            res[f"calls_overlap{int(overlap)}"] = (sp.collective_calls, want_calls)
         torch.distributed.destroy_process_group()
-        q.put(same)
+        q.put(res)
     except Exception:  # pragma: no cover
         import traceback
         q.put(traceback.format_exc())
@@ -173,6 +202,9 @@ def test_ulysses_rccl_world1_bit_identical():
     q = ctx.Queue()
     p = ctx.Process(target=_rccl_worker, args=(_port(), q))
     p.start()
-    res = q.get(timeout=600)
+    res = q.get(timeout=240)
     p.join(60)
-    assert res is True, res
+    assert isinstance(res, dict), res
+    print("rccl world1:", res)
+    assert res["stages"] is True and res["gather"] is True, res
+    assert res["model_overlap1"] is True and res["model_overlap0"] is True, res

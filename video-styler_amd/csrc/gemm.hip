@@ -871,8 +871,9 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_fp8_tn_256(
     }
 }
 
-// Per-row activation quantisation of fp8_linear (layers.py:124-137): s = max(max|x| / 448, 1),
-// x8 = e4m3(x / (s + 1e-8)) (fp32 division, round-to-nearest-even), one wave per row.
+// Per-row activation quantisation of fp8_linear (layers.py:124-137): s = max(bf16(max|x| / 448), 1)
+// (the reference divides and clamps the bf16 row max, so the quotient is rounded to bf16 before the
+// clamp), x8 = e4m3(x / (s + 1e-8)) (fp32 division, round-to-nearest-even), one wave per row.
 __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __restrict__ x, long long ldx,
                                                              uint8_t* __restrict__ x8, long long ld8,
                                                              float* __restrict__ scale, int rows, int cols) {
@@ -888,7 +889,7 @@ __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __res
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    const float s = fmaxf(mx / 448.0f, 1.0f);
+    const float s = fmaxf(rbf(mx / 448.0f), 1.0f);
     const float d = s + 1e-8f;
     if (lane == 0) scale[row] = s;
     uint8_t* yr = x8 + (long long)row * ld8;

@@ -3,8 +3,11 @@
 merge_lora   : GeneralLoRALoader.load (diffsynth/lora/__init__.py:11-45): W <- W + alpha*(B@A),
                computed by the MFMA GEMM with the VS_EPI_RES epilogue (bf16 mm, *alpha, + W).
 hotload_lora : AutoWrappedLinear hot-load (vram_management/layers.py:180-182, pipeline
-               wan_video_new.py:96-103): y = W x + b + B (alpha A x), fused into the main GEMM as a
-               second K phase (the "LoRA-fused linear" of BASELINE config 3).
+               wan_video_new.py:96-103): y = W x + b + sum_i B_i (alpha_i A_i x), fused into the main
+               GEMM as a second K phase (the "LoRA-fused linear" of BASELINE config 3).  Like the
+               reference's lora_A_weights / lora_B_weights lists, hot-loads accumulate: the padded
+               A_i are stacked along the rank rows and the B_i along the rank columns, so several
+               adapters stay ONE K phase (sum_i (x A_i^T) B_i^T = (x [A_1; A_2]^T) [B_1 B_2]^T).
 """
 import torch
 
@@ -89,23 +92,35 @@ def merge_lora(model, lora, alpha=1.0):
             a_t = _padded(down.t().contiguous(), cols=rp)         # [in, rp]
             w = module.weight
             K.gemm(b_mat, a_t, w, epilogue=K.VS_EPI_RES, residual=w, alpha=float(alpha))
+            w8 = getattr(module, "weight_fp8", None)
+            if w8 is not None:
+                # quantize_fp8_ ran first (config-5 order): refresh the e4m3 copy linear() reads, in
+                # place so the fused q|k|v / k|v e4m3 buffer it may be a view of sees it too
+                w8.copy_(w.detach().to(torch.float8_e4m3fn).view(torch.uint8))
             updated += 1
     print(f"{updated} tensors are updated by LoRA.")
     return updated
 
 
 def hotload_lora(model, lora, alpha=1.0):
-    """Attach (alpha*A, B) pairs to each matching Linear; the GEMM adds them as a fused K phase."""
+    """Attach (alpha*A, B) to each matching Linear (layers.py:180-182 appends to the layer's lists);
+    an adapter already attached stays and the new one is stacked onto it.  The GEMM adds them all as
+    one fused K phase.  fp8 layers take no hot-loaded LoRA (linear() raises): merge instead."""
     updated = 0
     for name, module in model.named_modules():
         if not isinstance(module, Linear):
             continue
         ka, kb = f"{name}.lora_A.default.weight", f"{name}.lora_B.default.weight"
         if ka in lora and kb in lora:
+            if getattr(module, "weight_fp8", None) is not None:
+                raise NotImplementedError(f"hot-loaded LoRA on the fp8 layer {name}: merge the LoRA instead")
             a = (lora[ka].to(device=module.weight.device, dtype=BF16) * alpha).to(BF16)   # [r, in]
             b = lora[kb].to(device=module.weight.device, dtype=BF16)                       # [out, r]
             rp = (a.shape[0] + 63) // 64 * 64
-            module.lora_A = _padded(a, rows=rp)          # [rp, in]
-            module.lora_B = _padded(b, cols=rp)          # [out, rp]
+            a, b = _padded(a, rows=rp), _padded(b, cols=rp)   # [rp, in], [out, rp]
+            if getattr(module, "lora_A", None) is not None:
+                a = torch.cat([module.lora_A, a], dim=0)
+                b = torch.cat([module.lora_B, b], dim=1).contiguous()
+            module.lora_A, module.lora_B = a, b
             updated += 1
     return updated

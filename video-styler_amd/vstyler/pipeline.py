@@ -69,7 +69,7 @@ def model_fn_wan_video(dit: WanModel, motion_controller=None, vace: VaceWanModel
         if sp is None:
             from .usp import get_default_group
             sp = get_default_group()
-        if sp is not None and sp.world_size == 1:
+        if sp is not None and sp.world_size == 1 and not getattr(sp, "force_collectives", False):
             sp = None
     rc = RunCtx(B, S, grid, dit.rope(device), ctx, L, ws)
 

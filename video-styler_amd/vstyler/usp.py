@@ -52,13 +52,17 @@ class _Exchange:
 class UlyssesGroup:
     """overlap: split the CFG batch into per-sample micro-batches inside each block so one half's
     all-to-alls (async on RCCL's stream) run under the other half's GEMMs / attention / FFN
-    (VSTYLER_SP_OVERLAP=0 disables)."""
+    (VSTYLER_SP_OVERLAP=0 disables).  force_collectives: run the sharded path (permutes and RCCL
+    collectives) even at world size 1, where model_fn_wan_video otherwise takes the plain path
+    (tests use it to drive the real collectives on a one-GPU box)."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, force_collectives=False):
         self.group = group
         self.world_size = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.overlap = os.environ.get("VSTYLER_SP_OVERLAP", "1") != "0"
+        self.force_collectives = force_collectives
+        self.collective_calls = 0
 
     # -------------------------------------------------------------- layout helpers (kernels)
     def _permute(self, src, dst, batch, s_local, cpr, ld_local, jstride, mode):
@@ -73,9 +77,11 @@ class UlyssesGroup:
     def _all_to_all(self, recv, send):
         """Asynchronous: RCCL's stream waits for the work enqueued so far on the current stream;
         the returned handle's wait() makes the current stream wait for the exchange."""
+        self.collective_calls += 1
         return dist.all_to_all_single(recv, send, group=self.group, async_op=True)
 
     def _all_gather(self, recv, send):
+        self.collective_calls += 1
         dist.all_gather_into_tensor(recv, send, group=self.group)
 
     # -------------------------------------------------------------- token sharding
