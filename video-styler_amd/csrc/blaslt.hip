@@ -27,9 +27,10 @@ struct LtKey {
     long long lda, ldw, ldc;
     bool bias;
     bool fp8;          // e4m3fn operands with a per-row (per-token) fp32 scale on A
+    bool gelu;         // hipBLASLt's GELU epilogue on the fp32 acc + bias (one bf16 rounding)
     bool operator<(const LtKey& o) const {
-        return std::tie(dev, m, n, k, lda, ldw, ldc, bias, fp8) <
-               std::tie(o.dev, o.m, o.n, o.k, o.lda, o.ldw, o.ldc, o.bias, o.fp8);
+        return std::tie(dev, m, n, k, lda, ldw, ldc, bias, fp8, gelu) <
+               std::tie(o.dev, o.m, o.n, o.k, o.lda, o.ldw, o.ldc, o.bias, o.fp8, o.gelu);
     }
 };
 
@@ -68,10 +69,13 @@ LtPlan* plan_for(const LtKey& key, size_t ws_bytes) {
     const hipblasOperation_t opT = HIPBLAS_OP_T, opN = HIPBLAS_OP_N;
     hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opT, sizeof(opT));
     hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opN, sizeof(opN));
-    if (key.bias) {
-        const hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_BIAS;
-        const hipDataType bt = HIP_R_16BF;
+    if (key.bias || key.gelu) {
+        const hipblasLtEpilogue_t epi = key.gelu ? (key.bias ? HIPBLASLT_EPILOGUE_GELU_BIAS : HIPBLASLT_EPILOGUE_GELU)
+                                                 : HIPBLASLT_EPILOGUE_BIAS;
         hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi));
+    }
+    if (key.bias) {
+        const hipDataType bt = HIP_R_16BF;
         hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
     }
     const hipDataType in_t = key.fp8 ? HIP_R_8F_E4M3 : HIP_R_16BF;
@@ -157,14 +161,14 @@ void autotune(LtPlan& p, hipblasLtHandle_t h, const void* a, const void* w, void
 
 namespace {
 int lt_gemm(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc, int m, int n, int k,
-            const void* bias, const float* scale_a, hipStream_t stream) {
+            const void* bias, const float* scale_a, bool gelu, hipStream_t stream) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return VS_E_LAUNCH;
     long long ws_bytes = 0;
     float* ws = vs_bound_workspace(2, dev, stream, &ws_bytes);
     if (!ws) return VS_E_UNSUPPORTED;
     std::lock_guard<std::mutex> lock(g_mu);
-    const LtKey key{dev, m, n, k, lda, ldw, ldc, bias != nullptr, scale_a != nullptr};
+    const LtKey key{dev, m, n, k, lda, ldw, ldc, bias != nullptr, scale_a != nullptr, gelu};
     LtPlan* p = plan_for(key, (size_t)ws_bytes);
     if (!p || p->ws_need > (size_t)ws_bytes) return VS_E_UNSUPPORTED;
     if (bias)
@@ -183,11 +187,18 @@ int lt_gemm(const void* a, long long lda, const void* w, long long ldw, void* c,
 // when hipBLASLt has no algorithm for the shape or the bound workspace (kind 2) is too small.
 int vs_lt_gemm_bias(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc, int m,
                     int n, int k, const void* bias, hipStream_t stream) {
-    return lt_gemm(a, lda, w, ldw, c, ldc, m, n, k, bias, nullptr, stream);
+    return lt_gemm(a, lda, w, ldw, c, ldc, m, n, k, bias, nullptr, false, stream);
+}
+
+// C[m][n] = bf16(GELU_tanh(A W^T + bias)) with hipBLASLt's fused GELU epilogue (the GELU of the fp32
+// acc + bias, not of its bf16 rounding); same contract.
+int vs_lt_gemm_bias_gelu(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc, int m,
+                         int n, int k, const void* bias, hipStream_t stream) {
+    return lt_gemm(a, lda, w, ldw, c, ldc, m, n, k, bias, nullptr, true, stream);
 }
 
 // C[m][n] = bf16((A8 W8^T) * scale_a[row] + bias), e4m3fn operands (fp8_linear); same contract.
 int vs_lt_gemm_fp8(const void* a8, long long lda, const float* scale_a, const void* w8, long long ldw, void* c,
                    long long ldc, int m, int n, int k, const void* bias, hipStream_t stream) {
-    return lt_gemm(a8, lda, w8, ldw, c, ldc, m, n, k, bias, scale_a, stream);
+    return lt_gemm(a8, lda, w8, ldw, c, ldc, m, n, k, bias, scale_a, false, stream);
 }

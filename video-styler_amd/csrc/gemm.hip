@@ -1061,6 +1061,15 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
     }
     const bool big = force ? force == 256
                           : k >= 4096 && (long long)((m + BT - 1) / BT) * ((n + BT - 1) / BT) >= 240;
+    // GELU on the hipBLASLt route: the library's fused GELU_BIAS epilogue (GELU-tanh of the fp32
+    // acc + bias, one bf16 rounding) instead of bf16(acc + bias) + the gemm_epi_apply8 GELU pass: the
+    // 14B FFN-up 6.18 -> 5.79 ms (profiles/r2/lt_gelu_ab.log).  It drops the reference's bf16 rounding
+    // of the linear output before F.gelu: 35 % of outputs move by one bf16 ulp, closer to the exact
+    // GELU (0.8 % off its rounding vs 35 %).  VS_LT_GELU=0 keeps the two-pass rounding points.
+    const char* lt_gelu = getenv("VS_LT_GELU");
+    if (k2 == 0 && epilogue == VS_EPI_GELU && !(lt_gelu && lt_gelu[0] == '0') && lt_route(m, n, k) &&
+        vs_lt_gemm_bias_gelu(a, lda, w, ldw, c, ldc, m, n, k, ep.bias, (hipStream_t)stream) == VS_OK)
+        return VS_OK;
     if (k2 == 0 && lt_route(m, n, k) &&
         lt_with_epilogue(c, ldc, m, n, epilogue, ep, (hipStream_t)stream, [&](void* y, long long ldy) {
             return vs_lt_gemm_bias(a, lda, w, ldw, y, ldy, m, n, k, ep.bias, (hipStream_t)stream);
