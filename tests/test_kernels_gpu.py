@@ -261,6 +261,28 @@ def test_attention_overflow_spike(K):
     assert mx < 3e-2, mx
 
 
+@pytest.mark.parametrize("late", [False, True])
+def test_attention_first_tile_low_scores(K, late):
+    """Rows whose scores are all far below the initial reference max m = 0 (exp2 domain < -60):
+    the first tile's partial sums fall under SUM_MIN, so it takes the exact path with S recomputed
+    from K (its in-place exp2 underflowed).  late: only the first 64 keys are that low and the rest
+    are ordinary, so the row's max then jumps by ~65 in a later tile (a second exact path)."""
+    B, S, H = 1, 512, 1
+    g = torch.Generator().manual_seed(36)
+    u = torch.ones(128)
+    k = (0.1 * torch.randn(B, S, 128, generator=g) + u).to(BF16)
+    if late:
+        k[0, 64:] = torch.randn(S - 64, 128, generator=g).to(BF16)
+    q = torch.randn(B, S, 128, generator=g).to(BF16)
+    for row in (0, 7, 200, 511):
+        q[0, row] = (-4.0 * u + 0.01 * torch.randn(128, generator=g)).to(BF16)
+    ref = O.attention(q, k, v := torch.randn(B, S, 128, generator=g).to(BF16), H)
+    out = torch.empty(S, 128, dtype=BF16, device="cuda")
+    K.attention(q.cuda().view(S, 128), k.cuda().view(S, 128), v.cuda().view(S, 128), out, H, B)
+    mx, rl = err(out.view(B, S, 128), ref)
+    assert mx < 3e-2 and rl < 1e-2, (mx, rl)
+
+
 def test_attention_rescale_many(K):
     """Exact-path (rescale) decisions in the middle of the key sweep for many rows: row 7's max is
     raised three times in three different tiles, other rows once each, at keys spread over the
@@ -330,6 +352,38 @@ def test_attention_split_tail(K, monkeypatch):
     assert d.max().item() < 2e-2, d.max().item()
     assert torch.equal(out[:19456], whole[:19456])        # whole items are untouched by the split
     assert torch.equal(out[:, :256], whole[:, :256])
+
+
+@pytest.mark.parametrize("B,Sq,Skv,H", [(2, 23000, 512, 3), (1, 20000, 500, 7), (2, 9000, 1000, 8)])
+def test_attention_persistent_matches_one_item_per_block(K, monkeypatch, B, Sq, Skv, H):
+    """Persistent grid (one block per CU, several items each, the K/V pipeline running across item
+    boundaries, the next item's Q prefetched through LDS): bit-identical to the one-item-per-block
+    grid (VS_ATTN_NO_PERSIST=1) -- every item starts from m = 0 exactly as a fresh block -- and
+    against a torch fp32 reference on rows of items at both ends of the blocks' item lists.  The
+    shapes cross (batch, head) boundaries between a block's consecutive items, end in partial
+    q-blocks, and have 8 key tiles (the cross-attention's 512 keys; 500: a partial last tile)."""
+    D = H * 128
+    g = torch.Generator(device="cuda").manual_seed(71)
+    q = torch.randn(B * Sq, D, device="cuda", generator=g).to(BF16)
+    k = torch.randn(B * Skv, D, device="cuda", generator=g).to(BF16)
+    v = torch.randn(B * Skv, D, device="cuda", generator=g).to(BF16)
+    out = torch.empty_like(q)
+    K.attention(q, k, v, out, H, B)
+    monkeypatch.setenv("VS_ATTN_NO_PERSIST", "1")
+    ref1 = torch.empty_like(q)
+    K.attention(q, k, v, ref1, H, B)
+    monkeypatch.delenv("VS_ATTN_NO_PERSIST")
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref1)
+    rows = torch.cat([torch.arange(0, Sq, 331), torch.tensor([255, 256, Sq - 1])]).cuda()
+    for b in range(B):
+        for h in range(H):
+            qs = q[b * Sq + rows, h * 128:(h + 1) * 128].float()
+            ks = k[b * Skv:(b + 1) * Skv, h * 128:(h + 1) * 128].float()
+            vs = v[b * Skv:(b + 1) * Skv, h * 128:(h + 1) * 128].float()
+            ref = torch.softmax(qs @ ks.t() * 128 ** -0.5, -1) @ vs
+            mx = (out[b * Sq + rows, h * 128:(h + 1) * 128].float() - ref).abs().max().item()
+            assert mx < 3e-2, (b, h, mx)
 
 
 def test_attention_strided_views(K):

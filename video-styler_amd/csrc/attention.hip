@@ -15,7 +15,12 @@
 //    lane belongs to its own query row, so every rescale is lane-local;
 //  * two phases per tile with the two wave halves one barrier apart (kernel comment below);
 //  * workgroup ids are remapped so each XCD works through contiguous (batch, head) ranges: the
-//    K/V of one head is streamed by the 32 CUs of one XCD together and served from its L2.
+//    K/V of one head is streamed by the 32 CUs of one XCD together and served from its L2;
+//  * persistent grid (one workgroup per CU, several items each, r2): the K/V pipeline runs on
+//    across item boundaries as one flattened tile sequence, the next item's Q is prefetched into
+//    LDS (prescaled) during the current item's first 8 tiles, and the finished item's O is stored
+//    inside the phase that completes it -- no per-item prologue or drain (worth most on the
+//    cross-attention, whose 512 keys are only 8 tiles per item).
 #include "common.h"
 
 namespace {
@@ -29,7 +34,9 @@ constexpr int VROW = 320;        // LDS row pitch of the V tile (256 B + 64): tr
 constexpr int KT = BKV * KROW;   // 17408
 constexpr int VT = BKV * VROW;   // 20480
 constexpr int LDS_BYTES = 2 * (KT + VT);   // K ring 2 x 17408 + V ring 2 x 20480
+constexpr int QPRE_BYTES = 9 * NTHR * 16;  // persistent mode: next item's Q / previous item's O, lane-private
 constexpr int PROW = HD + 4;     // split-tail partial row: 128 fp32 O, m, l, 2 pad (16-B aligned)
+constexpr int PERSIST_MIN_TILES = 8;       // the Q prefetch spreads its 8 chunks over the first 8 tiles
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
@@ -50,16 +57,22 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
 // p = exp2(c*s - m) against the current reference max m, packed to bf16, and a lane's tile
 // partial sum rs (both halves) checked once per tile.  Every p <= rs,
 // so rs <= SUM_THR (= 2^8) guarantees P <= 2^8 -- the bound of v1's lazy rescale (CDNA guide T13).
-// When any lane of the wave exceeds it (always on the first tile; later only when a row's max has
-// grown), the exact path runs after the tile's PV(i-1) MFMAs: row max, m' = max(m, max), O (which
-// already holds P(i-1)V(i-1) at the old scale) and l scaled by exp2(m - m'), P(i) recomputed (the
-// keys 0-31 half from log2 of its in-place exps, or from K in global memory if one overflowed).
+// When any lane of the wave exceeds it (only when a row's max has grown), the exact path runs
+// after the tile's PV(i-1) MFMAs: row max, m' = max(m, max), O (which already holds
+// P(i-1)V(i-1) at the old scale) and l scaled by exp2(m - m'), P(i) recomputed (the keys 0-31 half
+// from log2 of its in-place exps, or from K in global memory if one overflowed or underflowed).
+// An item starts from m = 0 and keeps it through its first tile unless a lane's partial sum is
+// above SUM_THR or below SUM_MIN (r2; r1 always took the exact path there): exp2(S) of any row
+// whose max score is above -60 (exp2 domain) is a normal float, and p's relative precision does
+// not depend on the reference max, so the first tile needs no max pass on typical scores -- an
+// eighth of the tiles of a 512-key cross-attention item.
 // Ring hazards (group 0 runs B_{i-1} at phase 2i and A_i at 2i+1, group 1 one phase later):
 // K(i+1) is written at 2i / 2i+1 into the slot K(i-1) was read from at 2i-2 / 2i-1 and first read
 // at 2i+2; V(i) is written at 2i+1 / 2i+2 into the slot V(i-2) was read from at 2i-1 / 2i and first
 // read at 2i+3.  Per-tile VALU ~460 issue cycles (the previous structure, with a max pass, a
 // shuffle and a two-deep S ring: ~850).  Epilogue: permlane32_swap pairs -> 16-B stores (T21).
 constexpr float SUM_THR = 256.0f;
+constexpr float SUM_MIN = 0x1p-60f;
 
 #ifdef VS_ATTN_STAMPS
 // debug build: s_memtime at the 4 phase boundaries of tiles 2..33 for wave 0 (group 0) and wave 4
@@ -78,43 +91,93 @@ constexpr int STAMP_LDS = 8 * 4 * 32 * 8;
 #define ATTN_STAMP(slot) do {} while (0)
 #endif
 
-template <bool REBASE>
-__global__ __launch_bounds__(NTHR) void attn_fwd_d128(
-    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-    bf16_t* __restrict__ O, int Sq, int Skv_all, int H, long long ldq, long long ldk, long long ldv,
-    long long ldo, long long bsq, long long bsk, long long bsv, long long bso, float c, int nqb,
-    int nmain, int nsplit, int piece_tiles, float* __restrict__ part) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+// Kernel arguments.  The fields an item switch needs (bases, batch strides, nqb, H) are read
+// through a volatile view of the argument block at each switch, so they do not stay live in SGPRs
+// across the tile loop (they pushed it past the SGPR file).
+struct AttnArgs {
+    const bf16_t *Q, *K, *V;
+    bf16_t* O;
+    long long bsq, bsk, bsv, bso;
+    long long ldq, ldk, ldv, ldo;
+    float* part;
+    float c;
+    int Sq, Skv, H, nqb, nmain, npers, nsplit, piece_tiles;
+};
 
-    // blocks [0, nmain) each run one whole (q-block, batch, head) item, XCD-remapped; the blocks
-    // after them run the last items of the grid as nsplit key ranges of piece_tiles tiles each
-    // (split tail, see vs_attn_fwd) and leave unnormalised partials for attn_combine
-    int g, piece = -1, kv_begin = 0, Skv = Skv_all;
-    if ((int)blockIdx.x < nmain) {
-        g = xcd_remap(blockIdx.x, nmain);
+template <bool REBASE>
+__global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // the argument block itself (the kernel's only argument, at the start of the kernarg segment):
+    // volatile scalar loads of it are not hoisted out of the tile loop
+    typedef const volatile AttnArgs __attribute__((address_space(4))) ColdArgs;
+    ColdArgs* cold = (ColdArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    const int Sq = args.Sq, Skv_all = args.Skv, nmain = args.nmain, npers = args.npers;
+    const int nsplit = args.nsplit, piece_tiles = args.piece_tiles;
+    const long long ldq = args.ldq, ldk = args.ldk, ldv = args.ldv, ldo = args.ldo;
+    const float c = args.c;
+    float* const part = args.part;
+
+    int piece = -1, kv_begin = 0, Skv = Skv_all;
+    int g0, gstride, n_items;
+    if ((int)blockIdx.x < npers) {
+        const int x = blockIdx.x & 7, lb = blockIdx.x >> 3;
+        const int qx = nmain >> 3, rx = nmain & 7, qbk = npers >> 3, rbk = npers & 7;
+        const int cs = x < rx ? x * (qx + 1) : rx * (qx + 1) + (x - rx) * qx;
+        const int csz = qx + (x < rx ? 1 : 0);
+        gstride = qbk + (x < rbk ? 1 : 0);
+        g0 = cs + lb;
+        n_items = lb < csz ? (csz - lb + gstride - 1) / gstride : 0;
     } else {
-        const int t = blockIdx.x - nmain;
-        g = nmain + t / nsplit;
+        const int t = blockIdx.x - npers;
+        g0 = nmain + t / nsplit;
+        gstride = 0;
+        n_items = 1;
         piece = t % nsplit;
         kv_begin = piece * piece_tiles * BKV;
         Skv = min(Skv_all - kv_begin, piece_tiles * BKV);
     }
-    const int qb = g % nqb;
-    const int bh = g / nqb;
-    const int h = bh % H, b = bh / H;
+    if (n_items == 0) return;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, hh = lane >> 5;
-    const int q0 = qb * BQ + wave * 32;
 
-    const bf16_t* Qb = Q + (long long)b * bsq + h * HD;
-    const bf16_t* Kb = K + (long long)b * bsk + (long long)kv_begin * ldk + h * HD;
-    const bf16_t* Vb = V + (long long)b * bsv + (long long)kv_begin * ldv + h * HD;
+    // per-item offsets (b, h from the item id): element offsets of the item's Q / K / V / O head
+    // column block, and the item's first query row (the wave's rows start 32 * wave further)
+    auto item_bh = [&](int j, int& qrow0) {
+        const int nqb = cold->nqb;
+        const int g = g0 + j * gstride;
+        const int qb = g % nqb, bh = g / nqb;
+        qrow0 = qb * BQ;
+        return bh;
+    };
+    auto q_base = [&](int bh) {
+        const int H = cold->H;
+        return cold->Q + (long long)(bh / H) * cold->bsq + (bh % H) * HD;
+    };
+    auto k_base = [&](int bh) {
+        const int H = cold->H;
+        return cold->K + (long long)(bh / H) * cold->bsk + (long long)kv_begin * ldk + (bh % H) * HD;
+    };
+    auto v_base = [&](int bh) {
+        const int H = cold->H;
+        return cold->V + (long long)(bh / H) * cold->bsv + (long long)kv_begin * ldv + (bh % H) * HD;
+    };
+    auto o_base = [&](int bh) {
+        const int H = cold->H;
+        return cold->O + (long long)(bh / H) * cold->bso + (bh % H) * HD;
+    };
+    const int g = g0;               // the first item (the split-tail piece's only one)
+    int q0;
+    int bh_cur = item_bh(0, q0);
+    q0 += wave * 32;
+    const bf16_t* Kb = k_base(bh_cur);   // K of the item whose tiles QK reads (exact-path recompute)
 
     // buffer descriptors over this (batch, head)'s K/V rows: per-lane byte offset constant, the
     // tile's row offset in soffset.  REBASE (a slab beyond 2^31 bytes, e.g. 1280x720x121 with the
     // fused q|k|v row layout: 111600 rows x 30 KB): the descriptor is rebuilt per tile on a 64-bit
-    // base (1.6 % slower, so only when needed).  Rows past Skv read as 0 (masked anyway).
+    // base (1.6 % slower, so only when needed).  Rows past Skv read as 0 (masked anyway).  K loads
+    // run two tiles ahead of QK, V loads one: across an item boundary each loader keeps the
+    // descriptor of the item it loads from.
     const int srow = tid >> 4, sch = tid & 15;
     const unsigned kvo0 = (unsigned)(srow * ldk * 2 + sch * 16), kvo1 = kvo0 + (unsigned)(32 * ldk * 2);
     const unsigned vvo0 = (unsigned)(srow * ldv * 2 + sch * 16), vvo1 = vvo0 + (unsigned)(32 * ldv * 2);
@@ -122,15 +185,20 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
 
     i32x4_t kst[2], vst[2];
     const int ldk32 = (int)ldk, ldv32 = (int)ldv;   // host: 64 * ld * 2 < 2^31
-    const __amdgpu_buffer_rsrc_t krs = make_rsrc(Kb, REBASE ? 0u : (unsigned)((Skv - 1) * ldk32 * 2 + HD * 2));
-    const __amdgpu_buffer_rsrc_t vrs = make_rsrc(Vb, REBASE ? 0u : (unsigned)((Skv - 1) * ldv32 * 2 + HD * 2));
+    auto slab_rsrc = [&](const bf16_t* base, int ld) {
+        return make_rsrc(base, REBASE ? 0u : (unsigned)((Skv - 1) * ld * 2 + HD * 2));
+    };
+    const bf16_t* Kload = Kb;       // base of the K loader's item, and its descriptor
+    const bf16_t* Vload = v_base(bh_cur);
+    __amdgpu_buffer_rsrc_t krs = slab_rsrc(Kload, ldk32);
+    __amdgpu_buffer_rsrc_t vrs = slab_rsrc(Vload, ldv32);
     auto tile_rsrc = [&](const bf16_t* base, int ld, int kv0) {
         const int rows = min(BKV, Skv - kv0);
         return make_rsrc(base + (long long)kv0 * ld, (unsigned)((rows - 1) * ld * 2 + HD * 2));
     };
     auto load_k = [&](int kv0) {
         if constexpr (REBASE) {
-            const __amdgpu_buffer_rsrc_t rs = tile_rsrc(Kb, ldk32, kv0);
+            const __amdgpu_buffer_rsrc_t rs = tile_rsrc(Kload, ldk32, kv0);
             kst[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, kvo0, 0, 0);
             kst[1] = __builtin_amdgcn_raw_buffer_load_b128(rs, kvo1, 0, 0);
         } else {
@@ -141,7 +209,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     };
     auto load_v = [&](int kv0) {
         if constexpr (REBASE) {
-            const __amdgpu_buffer_rsrc_t rs = tile_rsrc(Vb, ldv32, kv0);
+            const __amdgpu_buffer_rsrc_t rs = tile_rsrc(Vload, ldv32, kv0);
             vst[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, vvo0, 0, 0);
             vst[1] = __builtin_amdgcn_raw_buffer_load_b128(rs, vvo1, 0, 0);
         } else {
@@ -162,12 +230,26 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     };
 
     const int nkv = (Skv + BKV - 1) / BKV;
+    const int Ttot = n_items * nkv;           // the flattened tile sequence of all this block's items
+    // K loader cursor: item kj, tile ki of the next K tile to load (two tiles ahead of QK)
+    int kj = 0, ki = 0;
+    auto k_next = [&]() {
+        if (++ki == nkv) {
+            ki = 0;
+            if (++kj < n_items) {
+                int unused;
+                Kload = k_base(item_bh(kj, unused));
+                krs = slab_rsrc(Kload, ldk32);
+            }
+        }
+    };
     // prologue: K(0) staged and in LDS, K(1) in flight, Q fragments (B operand of S^T = K Q^T)
     load_k(0);
+    k_next();
     bf16x8_t qf[8];
     {
         const int qrow = min(q0 + r, Sq - 1);
-        const bf16_t* qp = Qb + (long long)qrow * ldq + 8 * hh;
+        const bf16_t* qp = q_base(bh_cur) + (long long)qrow * ldq + 8 * hh;
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
             // Q pre-scaled by c = log2(e)/sqrt(d) (one bf16 rounding): S^T then lands in the exp2
@@ -178,7 +260,22 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
         }
     }
     store_k(0);
-    if (nkv > 1) load_k(BKV);
+    if (Ttot > 1) {
+        load_k(ki * BKV);
+        k_next();
+    }
+    // persistent mode: the next item's Q (prescaled) and the previous item's O pass through here,
+    // 8 chunks of 16 B per lane at c * 8 KB + tid * 16 (each lane reads back only what it wrote:
+    // no barrier needed)
+    __shared__ __attribute__((aligned(16))) char qbuf_lds[QPRE_BYTES];
+    char* const qbuf = qbuf_lds;
+    int q0_nxt = 0;                 // the next item: Q rows (for the prefetch), its (b, h)
+    int bh_nxt = n_items > 1 ? item_bh(1, q0_nxt) : 0;
+    const bf16_t* qb_nxt = q_base(bh_nxt);
+    q0_nxt += wave * 32;
+    bf16_t* ob_cur = o_base(bh_cur);
+    bf16_t* ob_prev = ob_cur;
+    int q0_prev = q0;
 
     f32x16_t o[4];
 #pragma unroll
@@ -187,7 +284,8 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
         for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
     // m: the row's reference max (exp2 domain).  The QK accumulators start at -m (negm, 16 copies
     // of one per-lane value, rewritten only by the exact path), so S^T = c*QK^T - m and p = exp2(S).
-    // The first tile always takes the exact path, which sets m to that tile's row max.
+    // m starts at 0; the exact path (on the first tile only when its sums leave [SUM_MIN, SUM_THR])
+    // moves it to a row max.
     float m = 0.f, l = 0.f;
     f32x16_t negm;
 #pragma unroll
@@ -367,8 +465,10 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
     // exact path of the split softmax: s[0] holds p0 = exp2(S0); restore S0 = log2(p0), or, when a
     // p0 overflowed (a row max grown by >= 128 in the exp2 domain), recompute S0 from K in global
     // memory (the K(i) LDS slot may already hold K(i+2) for the other wave half)
-    auto exact_split = [&](bool first, int kv0) __attribute__((always_inline)) {
-        if (__any(!(rsA < INFINITY))) {
+    auto exact_split = [&](bool first, int kv0, bool low) __attribute__((always_inline)) {
+        // recompute S0 when an exp2 overflowed, or (first tile, a lane's sum below SUM_MIN) when
+        // an in-place exp2 may have underflowed with the row's max also far below m = 0
+        if (__any(!(rsA < INFINITY) || low)) {
             const int krow = min(kv0 + r, Skv - 1);
             const bf16_t* kp = Kb + (long long)krow * ldk + 8 * hh;
 #pragma unroll
@@ -385,61 +485,174 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
         rsA = 0.f;
     };
 
+    // phase barrier: this wave's LDS stores done (lgkmcnt), then s_barrier.  Written out rather than
+    // __syncthreads(), whose workgroup fence also waits for every LDS-DMA in flight (vmcnt(0)) --
+    // that would drain the next item's Q prefetch and this phase's K/V loads at every barrier
     auto phase_bar = [&]() {
         __builtin_amdgcn_sched_barrier(0);
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
     };
     __syncthreads();
     const int grp = wave >> 2;
     if (grp == 1) phase_bar();
-    // one tile: B_{it-1} (QK(it) + the s[0] half's exps), A_it (PV(it-1) + the s[1] half).  Tile 0
-    // (no PV, always the exact path) is peeled out of the loop: with one loop body shape the
-    // kernel stays spill-free (a loop with the it == 0 cases inside spilled at 256 VGPRs)
-    auto tile = [&](int it, auto first_c) __attribute__((always_inline)) {
-        constexpr bool first = decltype(first_c)::value;
+    // the normalised bf16 output of a finished item: lane (r, hh) holds columns 32dt + 8gi + 4hh .. +3
+    // of row qrow0 + r; pair groups (gi, gi+1) through one permlane32_swap per dword so each lane
+    // holds 16 contiguous bytes (T21) per chunk c = 2 dt + gp: columns 16c + 8hh .. +7.  emit(c, w)
+    // stores or stages chunk c; one column block dt at a time (8 live registers).
+    auto out_chunks = [&](auto emit) __attribute__((always_inline)) {
+        const float inv = 1.f / (l + __shfl_xor(l, 32));
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int gp = 0; gp < 2; ++gp) {
+                const int gi = 2 * gp;
+                const unsigned ax = pack2(o[dt][4 * gi] * inv, o[dt][4 * gi + 1] * inv);
+                const unsigned ay = pack2(o[dt][4 * gi + 2] * inv, o[dt][4 * gi + 3] * inv);
+                const unsigned bx = pack2(o[dt][4 * gi + 4] * inv, o[dt][4 * gi + 5] * inv);
+                const unsigned by = pack2(o[dt][4 * gi + 6] * inv, o[dt][4 * gi + 7] * inv);
+                const auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+                const auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+                emit(2 * dt + gp, u32x4_t{sx[0], sy[0], sx[1], sy[1]});
+            }
+    };
+    auto out_row = [&](bf16_t* ob, int qrow0) { return ob + (long long)(qrow0 + r) * ldo + 8 * hh; };
+    auto qslot = [&](int cidx) { return qbuf + cidx * (NTHR * 16) + tid * 16; };
+    // byte offsets of this lane's 16-B chunk c within the wave's 32-row block (Q / O rows)
+    const unsigned qvo = (unsigned)(r * ldq * 2 + 16 * hh), ovo = (unsigned)(r * ldo * 2 + 16 * hh);
+
+    // One tile T of the flattened sequence (tile ti of item tj): B_{T-1} (QK(T) + the s[0] half's
+    // exps), A_T (PV(T-1) + the s[1] half).  Tile 0 (no PV) is peeled out of the loop: with one
+    // loop body shape the kernel stays spill-free (a loop with the T == 0 cases inside spilled at
+    // 256 VGPRs).  A later item's first tile starts from m = 0, O = 0, l = 0 exactly as tile 0
+    // does, so every item's arithmetic is that of a one-item block (bit-identical results).
+    // Persistent-mode traffic: chunk ti (0..7) of the NEXT item's Q rows is loaded in tile ti's B
+    // phase and written prescaled to LDS slot ti in its A phase; the previous item's O, finished by
+    // PV(T-1) in A_T of the new item's tile 0, is staged in LDS slots 8, 1..7 there and drained one
+    // 16-B chunk per lane in the A phase of tiles 0..7 (each slot before that tile's Q chunk
+    // overwrites it).  The Q load and the O store are issued in EVERY tile, through buffer
+    // descriptors whose range is 0 when the tile has nothing to move (the load returns 0, the store
+    // is dropped): with them conditional, the compiler's vmcnt waits -- merged over both paths --
+    // waited for them at the next V-tile wait (measured: +20 % on the cross-attention).  Needs
+    // nkv >= PERSIST_MIN_TILES (host).
+    int ti = 0, tj = 0;
+    auto tile = [&](int T, auto first_c) __attribute__((always_inline)) {
+        constexpr bool first0 = decltype(first_c)::value;
+        const bool first = first0 || ti == 0;
+        const int kv0 = ti * BKV;
+#ifdef VS_ATTN_DIAG_NOQPREF
+        const bool qpref = false;         // timing diagnostic only: the next item reuses this Q
+#else
+        const bool qpref = tj + 1 < n_items && ti < PERSIST_MIN_TILES;
+#endif
+        const bool odrain = tj > 0 && ti < PERSIST_MIN_TILES;
 #ifdef VS_ATTN_STAMPS
-        stamp_it = it;
+        stamp_it = T;
 #endif
         ATTN_STAMP(0);
         // each phase opens with the LDS store of the tile staged one phase earlier (its slot's last
         // reader finished before the barrier that opened this phase), then the next global loads
-        if (it + 1 < nkv) store_k((it + 1) & 1);     // K(it+1), loaded at the start of A_{it-1}
-        load_v(it * BKV);
-        qk(it & 1, it * BKV);
+        if (T + 1 < Ttot) store_k((T + 1) & 1);      // K(T+1), loaded at the start of A_{T-1}
+        load_v(kv0);
+        const bf16x8_t qraw = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
+            make_rsrc(qb_nxt + (long long)q0_nxt * ldq, qpref ? (unsigned)(max(Sq - q0_nxt, 0) * ldq * 2) : 0u),
+            qvo + 32u * (unsigned)(ti & 7), 0, 0));
+        qk(T & 1, kv0);
         ATTN_STAMP(1);
         phase_bar();
         ATTN_STAMP(2);
-        store_v(it & 1);                             // V(it), loaded at the start of B_{it-1}
-        if (it + 2 < nkv) load_k((it + 2) * BKV);
-        if ((it + 1) * BKV > Skv) {
+        store_v(T & 1);                              // V(T), loaded at the start of B_{T-1}
+        // K(T+2); issued unconditionally (past the end it re-reads an in-range tile that is never
+        // stored) so the vmcnt waits of the phase do not depend on a branch
+        load_k(ki * BKV);
+        if (T + 2 < Ttot) k_next();
+        if (kv0 + BKV > Skv) {
             asm volatile("");
-            mask_half(1, it * BKV);
+            mask_half(1, kv0);
         }
-        pv_softmax((it - 1) & 1, !first);
-        if (first || __any(rsA + RS_TOTAL > SUM_THR)) exact_split(first, it * BKV);
+        pv_softmax((T - 1) & 1, !first0);
+        if (!first0 && ti == 0) {
+            out_chunks([&](int cidx, u32x4_t w) __attribute__((always_inline)) {
+                *reinterpret_cast<u32x4_t*>(qslot(cidx == 0 ? 8 : cidx)) = w;
+            });
+            // the new item starts from O = 0, l = 0
+            l = 0.f;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+        }
+        {
+            // chunk ti of the previous item's O (range 0 unless draining: the store is dropped)
+            const u32x4_t w = *reinterpret_cast<const u32x4_t*>(qslot(ti == 0 ? 8 : (ti & 7)));
+#ifndef VS_ATTN_DIAG_NOSTORE
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(i32x4_t, w),
+                make_rsrc(ob_prev + (long long)q0_prev * ldo, odrain ? (unsigned)(max(Sq - q0_prev, 0) * ldo * 2) : 0u),
+                ovo + 32u * (unsigned)(ti & 7), 0, 0);
+#else
+            asm volatile("" :: "v"(w));
+#endif
+        }
+        if (qpref) {
+            bf16x8_t qs;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qs[j] = (__bf16)((float)qraw[j] * c);
+            *reinterpret_cast<bf16x8_t*>(qslot(ti)) = qs;
+        }
+        {
+            const float rst = rsA + RS_TOTAL;
+            const bool low = first && !(rst >= SUM_MIN);
+            if (__any(rst > SUM_THR || low)) exact_split(first, kv0, low);
+        }
         l += rsA + RS_TOTAL;
+        if (++ti == nkv && ++tj < n_items) {
+            // switch to the next item: its prescaled Q from the LDS slots, m = 0 (as in a fresh
+            // block); the V loader and the exact-path recompute follow the QK item, the K loader
+            // is already on it
+            ti = 0;
+#ifndef VS_ATTN_DIAG_NOQPREF
+#pragma unroll
+            for (int s2 = 0; s2 < 8; ++s2) qf[s2] = *reinterpret_cast<const bf16x8_t*>(qslot(s2));
+#endif
+#pragma unroll
+            for (int i = 0; i < 16; ++i) negm[i] = 0.f;
+            m = 0.f;
+            ob_prev = ob_cur;
+            q0_prev = q0;
+            bh_cur = bh_nxt;
+            q0 = q0_nxt;
+            ob_cur = o_base(bh_cur);
+            Kb = k_base(bh_cur);
+            Vload = v_base(bh_cur);
+            vrs = slab_rsrc(Vload, ldv32);
+            if (tj + 1 < n_items) {
+                bh_nxt = item_bh(tj + 1, q0_nxt);
+                q0_nxt += wave * 32;
+                qb_nxt = q_base(bh_nxt);
+            }
+        }
         ATTN_STAMP(7);
         phase_bar();
     };
     tile(0, std::true_type{});
-    for (int it = 1; it < nkv; ++it) tile(it, std::false_type{});
+    for (int T = 1; T < Ttot; ++T) tile(T, std::false_type{});
 #ifdef VS_ATTN_STAMPS
-    // stamps of tiles (nkv-32) .. nkv-1 (ring of 32), copied out by workgroup 0's waves 0 and 4
+    // stamps of tiles (Ttot-32) .. Ttot-1 (ring of 32), copied out by workgroup 0's waves 0 and 4
     if (blockIdx.x == 0 && (wave & 3) == 0) {
         for (int i = lane; i < 128; i += 64)
             g_attn_stamps[wave >> 2][i] =
                 *reinterpret_cast<volatile unsigned long long*>(smem + LDS_BYTES + 8 * (wave * 128 + i));
     }
 #endif
-    // ---- B_{nkv-1}: the last tile's PV.  Group 0 first waits for group 1's half of V(nkv-1)
-    // (stored in group 1's A_{nkv-1}, one phase later): the extra barrier that balances the count
+    // ---- B_{Ttot-1}: the last tile's PV.  Group 0 first waits for group 1's half of V(Ttot-1)
+    // (stored in group 1's A_{Ttot-1}, one phase later): the extra barrier that balances the count
     if (grp == 0) phase_bar();
-    pv_last((nkv - 1) & 1);
+    pv_last((Ttot - 1) & 1);
 
-    const float lt = l + __shfl_xor(l, 32);
     if (piece >= 0) {
         // split-tail piece: O unnormalised (fp32, natural column order) + the row's (m, l)
+        const float lt = l + __shfl_xor(l, 32);
         float* pp = part + ((long long)(g - nmain) * nsplit + piece) * BQ * PROW + (wave * 32 + r) * PROW;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
@@ -450,30 +663,12 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(
         if (hh == 0) *reinterpret_cast<f32x2_t*>(pp + HD) = f32x2_t{m, lt};
         return;
     }
-    const float inv = 1.f / lt;
-    // lane (r, hh) holds columns 32dt + 8gi + 4hh .. +3 of row q0+r; pair groups (gi, gi+1) through
-    // one permlane32_swap per dword so each lane stores 16 contiguous bytes
-    u32x4_t w[8];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int gp = 0; gp < 2; ++gp) {
-            const int gi = 2 * gp;
-            const unsigned ax = pack2(o[dt][4 * gi] * inv, o[dt][4 * gi + 1] * inv);
-            const unsigned ay = pack2(o[dt][4 * gi + 2] * inv, o[dt][4 * gi + 3] * inv);
-            const unsigned bx = pack2(o[dt][4 * gi + 4] * inv, o[dt][4 * gi + 5] * inv);
-            const unsigned by = pack2(o[dt][4 * gi + 6] * inv, o[dt][4 * gi + 7] * inv);
-            const auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
-            const auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
-            w[2 * dt + gp][0] = sx[0];
-            w[2 * dt + gp][1] = sy[0];
-            w[2 * dt + gp][2] = sx[1];
-            w[2 * dt + gp][3] = sy[1];
-        }
-    if (q0 + r < Sq) {
-        bf16_t* op = O + (long long)b * bso + (long long)(q0 + r) * ldo + h * HD + 8 * hh;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) *reinterpret_cast<u32x4_t*>(op + 16 * k) = w[k];
+    {
+        bf16_t* op = out_row(ob_cur, q0);
+        const bool ok = q0 + r < Sq;
+        out_chunks([&](int cidx, u32x4_t w) __attribute__((always_inline)) {
+            if (ok) *reinterpret_cast<u32x4_t*>(op + 16 * cidx) = w;
+        });
     }
 }
 
@@ -575,24 +770,36 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
     }
     const float c = scale * 1.4426950408889634f;
     const bool rebase = (long long)skv * ldk * 2 >= (1LL << 31) || (long long)skv * ldv * 2 >= (1LL << 31);
-#ifdef VS_ATTN_STAMPS
-    const int lds = LDS_BYTES + STAMP_LDS;
-    (void)hipFuncSetAttribute((const void*)attn_fwd_d128<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_d128<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-#else
-    const int lds = LDS_BYTES;
-#endif
-    SplitPlan sp = plan_split(nwg, (skv + BKV - 1) / BKV, vs_cus_for_split("VS_ATTN_NO_SPLIT"));
+    const int nkv = (skv + BKV - 1) / BKV;
+    const int cus = vs_cus_for_split("VS_ATTN_NO_SPLIT");
+    SplitPlan sp = plan_split(nwg, nkv, cus);
     float* part = nullptr;
     if (sp.ntail) {
         part = vs_split_workspace(0, (size_t)sp.ntail * sp.nsplit * BQ * PROW * sizeof(float), (hipStream_t)stream);
         if (!part) sp = SplitPlan{(int)nwg, 0, 1, 0};
     }
-    const long long grid = (long long)sp.nmain + (long long)sp.ntail * sp.nsplit;
+    // persistent grid: one block per CU runs the whole items when there is more than one round of
+    // them and an item has at least PERSIST_MIN_TILES key tiles (VS_ATTN_NO_PERSIST=1: one block per
+    // item, the r1 grid)
+    const int ncu = vs_cus_for_split(nullptr);
+    const bool no_persist = getenv("VS_ATTN_NO_PERSIST") != nullptr;
+    // (the Q prefetch and the O drain address a wave's rows through 32-bit buffer ranges)
+    const bool span_ok = (long long)sq * ldq * 2 < (1LL << 32) && (long long)sq * ldo * 2 < (1LL << 32);
+    const int npers =
+        (!no_persist && span_ok && ncu > 0 && nkv >= PERSIST_MIN_TILES && sp.nmain > ncu) ? ncu : sp.nmain;
+#ifdef VS_ATTN_STAMPS
+    const int lds = LDS_BYTES + STAMP_LDS;
+    (void)hipFuncSetAttribute((const void*)attn_fwd_d128<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)attn_fwd_d128<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+#else
+    const int lds = LDS_BYTES;      // + the kernel's static QPRE_BYTES Q buffer
+#endif
+    const long long grid = (long long)npers + (long long)sp.ntail * sp.nsplit;
+    const AttnArgs args{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, bsq, bsk, bsv, bso,
+                        ldq, ldk, ldv, ldo, part, c, sq, skv, heads, nqb, sp.nmain, npers, sp.nsplit,
+                        sp.piece_tiles};
     hipLaunchKernelGGL(rebase ? attn_fwd_d128<true> : attn_fwd_d128<false>, dim3((unsigned)grid), dim3(NTHR),
-                       lds, (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                       (bf16_t*)o, sq, skv, heads, ldq, ldk, ldv, ldo, bsq, bsk, bsv, bso, c, nqb,
-                       sp.nmain, sp.nsplit, sp.piece_tiles, part);
+                       lds, (hipStream_t)stream, args);
     VS_CHECK_LAUNCH();
     if (sp.ntail) {
         const long long threads = (long long)sp.ntail * BQ * 32;
