@@ -250,19 +250,25 @@ def test_hotloaded_lora_on_fused_projections_matches_merged():
     assert rl < 1e-2, (mx, rl)
 
 
-def test_fused_residual_layernorm_bit_identical(monkeypatch):
-    """The hipBLASLt route's residual epilogue fused with the following LayerNorm
-    (vs_residual_layernorm) gives exactly the unfused forward (same rounding points)."""
+@pytest.mark.parametrize("case", ["b1", "cfg2", "cfg2_slg"])
+def test_fused_residual_layernorm_bit_identical(monkeypatch, case):
+    """The hipBLASLt route's residual epilogues fused with the LayerNorm that reads the same rows
+    next (vs_residual_layernorm: o-proj -> LN3, cross-o -> LN2, FFN-down (+ VACE hint) -> the next
+    block's LN1 or the head's norm) give exactly the unfused forward (same rounding points); with
+    the batched CFG pair, and with a skip-layer-guidance block (which runs on one sample's rows, so
+    neither it nor the block before it fuses across it)."""
     from vstyler import model_fn_wan_video
     cfg = O.WAN_CONFIGS["tiny"]
     W = O.random_weights(cfg, seed=5)
     dit, vace = build(cfg, W)
     lat, cp, cn, vc = O.synthetic_inputs(cfg, 5, 128, 128)
+    ctx = cp if case == "b1" else torch.cat([cp, cn])
+    slg = (1,) if case == "cfg2_slg" else ()
     t = torch.tensor([600.0]).to(BF16).cuda()
     monkeypatch.setenv("VS_GEMM_BACKEND", "lt")          # tiny shapes: force the hipBLASLt route
     outs = []
     for fuse in ("1", "0"):
         monkeypatch.setenv("VSTYLER_FUSE_RES_LN", fuse)
-        outs.append(model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=cp.cuda(),
-                                       vace_context=vc.cuda()))
+        outs.append(model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx.cuda(),
+                                       vace_context=vc.cuda(), slg_blocks=slg))
     assert torch.equal(outs[0], outs[1])

@@ -257,6 +257,12 @@ class RunCtx:
         self.ctx, self.ctx_len, self.ws = ctx, ctx_len, ws
         self.sp = sp                    # vstyler.usp.UlyssesGroup or None
         self.token_offset = token_offset
+        # set by a block whose FFN-down residual was fused with the next consumer's LayerNorm
+        # (DiTBlock.forward nxt=): the ws buffer holding the next block's modulation, whose h
+        # buffers then already hold its modulated LN1
+        self.pre_mod = None
+        self.mod_slot = 0
+        self.t_emb = None               # the time embedding t [B, D] (the head's modulation input)
 
 
 class DiTBlock(nn.Module):
@@ -271,10 +277,12 @@ class DiTBlock(nn.Module):
         self.ffn = Sequential3(Linear(dim, ffn_dim, device=device), Linear(ffn_dim, dim, device=device))
         self.modulation = _param(1, 6, dim, device=device)
 
-    def forward(self, x, t_mod, rc, hint=None, hint_scale=1.0, only_batch=None):
+    def forward(self, x, t_mod, rc, hint=None, hint_scale=1.0, only_batch=None, nxt=None):
         """x: [B*S, D] updated in place.  t_mod: [B, 6, D].  hint: [B*S, D] added after the block.
         only_batch: run the block for that CFG sample only (skip-layer guidance leaves the others'
-        rows untouched).
+        rows untouched).  nxt: the module that consumes x next (a DiTBlock or the Head) when it runs
+        on all rows: the FFN-down gate-residual (+ VACE hint) is then fused with its modulated
+        LayerNorm (vs_residual_layernorm, one pass over the rows instead of two).
 
         Three phases per micro-batch: (1) LN1 + q/k/v + QK-RMSNorm/RoPE, (2) self-attention,
         (3) o-proj (gated residual), cross-attention, FFN (gated residual + VACE hint).  Without SP
@@ -283,27 +291,53 @@ class DiTBlock(nn.Module):
         all-to-all runs under sample 1's projections, sample 1's under sample 0's attention, and
         the return exchanges under the other sample's attention / o-proj / cross-attn / FFN."""
         B, S, D, ws = rc.batch, rc.seq, self.dim, rc.ws
-        mod = ws.get("mod", (B, 6, D))
-        K.mod_add(self.modulation.view(6, D), t_mod, mod, 6 * D, D)   # :218-219
+        if rc.pre_mod is not None:          # the previous block already ran this one's LN1
+            mod, ln1_done = rc.pre_mod, True
+            rc.pre_mod = None
+        else:
+            rc.mod_slot ^= 1
+            mod, ln1_done = ws.get(f"mod{rc.mod_slot}", (B, 6, D)), False
+            K.mod_add(self.modulation.view(6, D), t_mod, mod, 6 * D, D)   # :218-219
         sp = rc.sp
         if only_batch is not None:
+            assert not ln1_done, "a skip-layer-guidance block cannot start from a fused LN1"
             parts = [self._part(x, mod, rc, only_batch, 1, hint, f".{only_batch}")]
         elif sp is not None and B > 1 and getattr(sp, "overlap", False):
             parts = [self._part(x, mod, rc, b, 1, hint, f".{b}") for b in range(B)]
         else:
             parts = [self._part(x, mod, rc, 0, B, hint, "")]
         for p in parts:
+            p["ln1_done"] = ln1_done
+        # the fused FFN-down epilogue needs the consumer's modulation first (its own mod buffer)
+        fuse = None
+        if nxt is not None and only_batch is None and _fusable_lt(self.ffn[2], parts[0]["M"]) and \
+                os.environ.get("VSTYLER_FUSE_FFN_LN", "1") != "0":
+            if isinstance(nxt, DiTBlock):
+                nslot = rc.mod_slot ^ 1
+                nmod = ws.get(f"mod{nslot}", (B, 6, D))
+                K.mod_add(nxt.modulation.view(6, D), t_mod, nmod, 6 * D, D)
+                fuse = dict(shift=nmod[:, 0], scale=nmod[:, 1], bstride=6 * D, mod=nmod, slot=nslot)
+            elif isinstance(nxt, Head) and len(parts) == 1:
+                hm = nxt.modulation_for(rc.t_emb, rc)
+                fuse = dict(shift=hm[:, 0], scale=hm[:, 1], bstride=2 * D, mod=None)
+        for p in parts:
             self._phase_qkv(p, rc)
         for p in parts:
             self._phase_attn(p, rc)
         for p in parts:
-            self._phase_out(p, rc, hint_scale)
+            self._phase_out(p, rc, hint_scale, fuse)
+        if fuse is not None:
+            if fuse["mod"] is not None:
+                rc.pre_mod = fuse["mod"]
+                rc.mod_slot = fuse["slot"]
+            else:
+                rc.head_ln_done = True
         return x
 
     def _part(self, x, mod, rc, b0, nb, hint, tag):
         S, D, L, ws = rc.seq, self.dim, rc.ctx_len, rc.ws
         r0, M = b0 * S, nb * S
-        p = dict(nb=nb, M=M, x=x[r0:r0 + M], mod=mod[b0:b0 + nb], ctx=rc.ctx[b0 * L:(b0 + nb) * L],
+        p = dict(nb=nb, M=M, b0=b0, x=x[r0:r0 + M], mod=mod[b0:b0 + nb], ctx=rc.ctx[b0 * L:(b0 + nb) * L],
                  hint=None if hint is None else hint[r0:r0 + M], tag=tag)
         for n in ("h", "q", "k", "v", "o"):
             p[n] = ws.get(n + tag, (M, D))
@@ -313,7 +347,9 @@ class DiTBlock(nn.Module):
         # --- self-attention inputs (wan_video_dit.py:225-226, :140-145)
         S, D, eps, ws = rc.seq, self.dim, self.eps, rc.ws
         mod, h, q, k, v = p["mod"], p["h"], p["q"], p["k"], p["v"]
-        K.layernorm_modulate(p["x"], h, eps, shift=mod[:, 0], scale=mod[:, 1], mod_bstride=6 * D, rows_per_batch=S)
+        if not p["ln1_done"]:
+            K.layernorm_modulate(p["x"], h, eps, shift=mod[:, 0], scale=mod[:, 1], mod_bstride=6 * D,
+                                 rows_per_batch=S)
         sa = self.self_attn
         qkv = fused_linear(sa, h, ws, "qkv" + p["tag"])
         if qkv is not None:            # one GEMM; q/k/v are column slices of [M, 3D]
@@ -337,7 +373,7 @@ class DiTBlock(nn.Module):
             K.attention(p["q"], p["k"], p["v"], p["o"], self.num_heads, p["nb"])
             TIMER.stop(ev)
 
-    def _phase_out(self, p, rc, hint_scale):
+    def _phase_out(self, p, rc, hint_scale, fuse=None):
         S, D, eps, ws = rc.seq, self.dim, self.eps, rc.ws
         x, mod, h, q, o, nb, M = p["x"], p["mod"], p["h"], p["q"], p["o"], p["nb"], p["M"]
         if rc.sp is not None:
@@ -378,8 +414,19 @@ class DiTBlock(nn.Module):
             K.layernorm_modulate(x, h, eps, shift=mod[:, 3], scale=mod[:, 4], mod_bstride=6 * D, rows_per_batch=S)
         f = ws.get("f" + p["tag"], (M, self.ffn_dim))
         linear(self.ffn[0], h, f, ws, epilogue=K.VS_EPI_GELU)
-        linear(self.ffn[2], f, x, ws, epilogue=K.VS_EPI_GATE_RES, residual=x,
-               gate=mod[:, 5], gate_bstride=6 * D, rows_per_batch=S, hint=p["hint"], hint_scale=hint_scale)
+        if fuse is not None:
+            # bf16(f W2^T + b) staged, then x += gate * y (+ hint) and the next consumer's modulated
+            # LayerNorm of the new x into h (its LN1 / the head's norm) in one pass
+            y = ws.get("res_y" + p["tag"], (M, D))
+            K.gemm(f, self.ffn[2].weight, y, bias=self.ffn[2].bias)
+            b0, nb = p["b0"], p["nb"]
+            K.residual_layernorm(y, x, h, eps, epilogue=K.VS_EPI_GATE_RES, gate=mod[:, 5], gate_bstride=6 * D,
+                                 gate_rows=S, hint=p["hint"], hint_scale=hint_scale,
+                                 shift=fuse["shift"][b0:b0 + nb], scale=fuse["scale"][b0:b0 + nb],
+                                 mod_bstride=fuse["bstride"], rows_per_batch=S)
+        else:
+            linear(self.ffn[2], f, x, ws, epilogue=K.VS_EPI_GATE_RES, residual=x,
+                   gate=mod[:, 5], gate_bstride=6 * D, rows_per_batch=S, hint=p["hint"], hint_scale=hint_scale)
 
 
 class Head(nn.Module):
@@ -391,13 +438,22 @@ class Head(nn.Module):
         self.head = Linear(dim, out_dim * math.prod(patch_size), device=device)
         self.modulation = _param(1, 2, dim, device=device)
 
+    def modulation_for(self, t, rc):
+        """(modulation + t) [B, 2, D] (:267, per-batch t row) in its workspace buffer."""
+        B, D = rc.batch, self.dim
+        hm = rc.ws.get("head_mod", (B, 2, D))
+        K.mod_add(self.modulation.view(2, D), t, hm, D, 0)
+        return hm
+
     def forward(self, x, t, rc):
         B, S, D, ws = rc.batch, rc.seq, self.dim, rc.ws
-        hm = ws.get("head_mod", (B, 2, D))
-        K.mod_add(self.modulation.view(2, D), t, hm, D, 0)           # :267 (per-batch t row)
         h = ws.get("h", (B * S, D))
-        K.layernorm_modulate(x, h, self.eps, shift=hm[:, 0], scale=hm[:, 1], mod_bstride=2 * D,
-                             rows_per_batch=S)
+        if getattr(rc, "head_ln_done", False):     # fused into the last block's FFN-down epilogue
+            rc.head_ln_done = False
+        else:
+            hm = self.modulation_for(t, rc)
+            K.layernorm_modulate(x, h, self.eps, shift=hm[:, 0], scale=hm[:, 1], mod_bstride=2 * D,
+                                 rows_per_batch=S)
         out = ws.get("head_out", (B * S, self.head.out_features))
         K.gemm(h, self.head.weight, out, bias=self.head.bias)
         return out
@@ -504,12 +560,13 @@ class VaceWanModel(nn.Module):
         M = rc.batch * rc.seq
         c = vace_cols_out
         hints = []
+        nb = len(self.vace_blocks)
         for n, blk in enumerate(self.vace_blocks):
             if n == 0:
                 c0 = ws.get("vace_c", (M, D))
                 linear(blk.before_proj, c, c0, ws, epilogue=K.VS_EPI_RES, residual=x)
                 c = c0
-            blk(c, t_mod, rc)
+            blk(c, t_mod, rc, nxt=self.vace_blocks[n + 1] if n + 1 < nb else None)
             hint = ws.get(f"vace_hint{n}", (M, D))
             linear(blk.after_proj, c, hint, ws)
             hints.append(hint)

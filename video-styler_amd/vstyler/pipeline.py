@@ -90,12 +90,20 @@ def model_fn_wan_video(dit: WanModel, motion_controller=None, vace: VaceWanModel
     else:
         if tea_cache is not None:
             tea_cache.begin(x)
+        rc.t_emb = t
         hints = vace(x, vace_x, t_mod, rc) if vace_x is not None else None
         vmap = vace.vace_layers_mapping if hints is not None else {}
+        nblk = len(dit.blocks)
         for i, blk in enumerate(dit.blocks):
             hint = hints[vmap[i]] if i in vmap else None
             skip = B > 1 and i in slg_blocks
-            blk(x, t_mod, rc, hint=hint, hint_scale=float(vace_scale), only_batch=0 if skip else None)
+            # the next consumer of x, whose LayerNorm this block's FFN-down epilogue can take over
+            # (not a skip-layer-guidance block, which runs on one sample's rows only)
+            if i + 1 < nblk:
+                nxt = None if (B > 1 and i + 1 in slg_blocks) else dit.blocks[i + 1]
+            else:
+                nxt = None if tea_cache is not None else dit.head
+            blk(x, t_mod, rc, hint=hint, hint_scale=float(vace_scale), only_batch=0 if skip else None, nxt=nxt)
         if tea_cache is not None:
             tea_cache.store(x)                                  # :1455-1456
     out = dit.head(x, t, rc)
