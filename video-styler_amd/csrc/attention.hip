@@ -74,6 +74,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
 constexpr float SUM_THR = 256.0f;
 constexpr float SUM_MIN = 0x1p-60f;
 
+// v_mfma_f32_32x32x16_bf16.  VS_ATTN_DIAG_MFMA16 (timing diagnostic only, wrong results): the same
+// FLOPs as two v_mfma_f32_16x16x32_bf16 on the same operands, to measure the clock / issue effect
+// of the smaller MFMA shape on this loop (MI355X_MICROARCH 'DVFS give-back' item 7)
+__device__ __forceinline__ f32x16_t mfma32(bf16x8_t a, bf16x8_t b, f32x16_t c, int half = 0) {
+#ifdef VS_ATTN_DIAG_MFMA16
+    // alternate calls update the two halves of the accumulator, so all of it stays live
+    const int o = half ? 8 : 0;
+    f32x4_t c0 = {c[o], c[o + 1], c[o + 2], c[o + 3]}, c1 = {c[o + 4], c[o + 5], c[o + 6], c[o + 7]};
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, c1, 0, 0, 0);
+    c[o] = c0[0]; c[o + 1] = c0[1]; c[o + 2] = c0[2]; c[o + 3] = c0[3];
+    c[o + 4] = c1[0]; c[o + 5] = c1[1]; c[o + 6] = c1[2]; c[o + 7] = c1[3];
+    return c;
+#else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+
 #ifdef VS_ATTN_STAMPS
 // debug build: s_memtime at the 4 phase boundaries of tiles 2..33 for wave 0 (group 0) and wave 4
 // (group 1) of workgroup 0, kept in an LDS tail during the loop (no loop-carried registers) and
@@ -351,9 +369,9 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             if (j == 8 && last) mask_half(0, kv0);
             __builtin_amdgcn_sched_barrier(0);
             if (j < 8) {
-                s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[j], qf[j], j == 0 ? negm : s[0], 0, 0, 0);
+                s[0] = mfma32(kf[j], qf[j], j == 0 ? negm : s[0], j & 1);
             } else {
-                s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[j], qf[j - 8], j == 8 ? negm : s[1], 0, 0, 0);
+                s[1] = mfma32(kf[j], qf[j - 8], j == 8 ? negm : s[1], j & 1);
                 const int e = 2 * (j - 8);
                 s[0][e] = __builtin_amdgcn_exp2f(s[0][e]);
                 s[0][e + 1] = __builtin_amdgcn_exp2f(s[0][e + 1]);
@@ -399,8 +417,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int dt = 0; dt < 4; ++dt)
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[dt], __builtin_bit_cast(bf16x8_t, pk[ks]),
-                                                                    o[dt], 0, 0, 0);
+                    o[dt] = mfma32(cur[dt], __builtin_bit_cast(bf16x8_t, pk[ks]), o[dt], ks & 1);
             }
             if (ks < 2) {               // keys 0-31: exponentiated in the QK phase, pack only
                 p_pack(2 * ks);
@@ -430,7 +447,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
                 const bf16x8_t vf = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, v0),
                                                             __builtin_bit_cast(bf16x4_t, v1), 0, 1, 2, 3,
                                                             4, 5, 6, 7);
-                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, __builtin_bit_cast(bf16x8_t, pk[ks]), o[dt], 0, 0, 0);
+                o[dt] = mfma32(vf, __builtin_bit_cast(bf16x8_t, pk[ks]), o[dt], ks & 1);
             }
     };
     auto exact = [&](bool first) {
@@ -474,7 +491,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
 #pragma unroll
             for (int ss = 0; ss < 8; ++ss) {
                 const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kp + 16 * ss);
-                s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ss], ss == 0 ? negm : s[0], 0, 0, 0);
+                s[0] = mfma32(kf, qf[ss], ss == 0 ? negm : s[0], ss & 1);
             }
             if (kv0 + BKV > Skv) mask_half(0, kv0);
         } else {
@@ -603,7 +620,11 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
         {
             const float rst = rsA + RS_TOTAL;
             const bool low = first && !(rst >= SUM_MIN);
+#ifdef VS_ATTN_DIAG_MFMA16
+            if (__any(rst > 1e30f && low)) exact_split(first, kv0, low);   // (never: garbage scores)
+#else
             if (__any(rst > SUM_THR || low)) exact_split(first, kv0, low);
+#endif
         }
         l += rsA + RS_TOTAL;
         if (++ti == nkv && ++tj < n_items) {
