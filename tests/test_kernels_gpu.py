@@ -19,6 +19,13 @@ def rnd(*shape, scale=1.0, seed=0):
     return (scale * torch.randn(*shape, generator=g)).to(BF16)
 
 
+@pytest.fixture(params=["32", "16"])
+def attn_mfma(request, monkeypatch):
+    """Every attention test runs both MFMA shapes of attn_fwd_d128 (VS_ATTN_MFMA)."""
+    monkeypatch.setenv("VS_ATTN_MFMA", request.param)
+    return request.param
+
+
 @pytest.fixture(scope="module")
 def K():
     from vstyler import kernels
@@ -209,7 +216,7 @@ def test_gemm_lora_second_phase(K):
 
 
 @pytest.mark.parametrize("B,Sq,Skv,H", [(1, 256, 256, 1), (2, 300, 300, 2), (2, 300, 77, 2), (1, 1000, 512, 3)])
-def test_attention(K, B, Sq, Skv, H):
+def test_attention(attn_mfma, K, B, Sq, Skv, H):
     D = H * 128
     q, k, v = rnd(B, Sq, D, seed=20), rnd(B, Skv, D, seed=21), rnd(B, Skv, D, seed=22)
     ref = O.attention(q, k, v, H)
@@ -220,7 +227,7 @@ def test_attention(K, B, Sq, Skv, H):
 
 
 @pytest.mark.parametrize("Skv", [1, 31, 32, 33, 63, 64, 65, 129])
-def test_attention_key_tile_edges(K, Skv):
+def test_attention_key_tile_edges(attn_mfma, K, Skv):
     """Key counts around the 64-key tile and its two 32-key halves: the keys 0-31 half is masked
     and exponentiated inside the QK phase (split softmax), the keys 32-63 half in the PV phase."""
     B, Sq, H = 1, 300, 2
@@ -233,7 +240,7 @@ def test_attention_key_tile_edges(K, Skv):
     assert mx < 3e-2 and rl < 1e-2, (mx, rl)
 
 
-def test_attention_online_rescale_spike(K):
+def test_attention_online_rescale_spike(attn_mfma, K):
     """Rule 26 of the CDNA guide: force the running-max rescale by a late large score."""
     B, S, H = 1, 512, 1
     q, k, v = rnd(B, S, 128, seed=30), rnd(B, S, 128, seed=31), rnd(B, S, 128, seed=32)
@@ -246,7 +253,7 @@ def test_attention_online_rescale_spike(K):
     assert mx < 3e-2, mx
 
 
-def test_attention_overflow_spike(K):
+def test_attention_overflow_spike(attn_mfma, K):
     """Scores that jump by far more than 128 in the exp2 domain (exp2 overflows to inf before the
     exact path runs): in the first tile, in a later tile's first and second 32-key halves."""
     B, S, H = 1, 512, 1
@@ -262,7 +269,7 @@ def test_attention_overflow_spike(K):
 
 
 @pytest.mark.parametrize("late", [False, True])
-def test_attention_first_tile_low_scores(K, late):
+def test_attention_first_tile_low_scores(attn_mfma, K, late):
     """Rows whose scores are all far below the initial reference max m = 0 (exp2 domain < -60):
     the first tile's partial sums fall under SUM_MIN, so it takes the exact path with S recomputed
     from K (its in-place exp2 underflowed).  late: only the first 64 keys are that low and the rest
@@ -283,7 +290,7 @@ def test_attention_first_tile_low_scores(K, late):
     assert mx < 3e-2 and rl < 1e-2, (mx, rl)
 
 
-def test_attention_rescale_many(K):
+def test_attention_rescale_many(attn_mfma, K):
     """Exact-path (rescale) decisions in the middle of the key sweep for many rows: row 7's max is
     raised three times in three different tiles, other rows once each, at keys spread over the
     sweep (rule 26: bounded random data alone never takes the branch after the first tile)."""
@@ -299,7 +306,7 @@ def test_attention_rescale_many(K):
     assert mx < 3e-2 and rl < 1e-2, (mx, rl)
 
 
-def test_attention_kv_slab_beyond_4gb(K):
+def test_attention_kv_slab_beyond_4gb(attn_mfma, K):
     """K/V rows of stride 32768 so one (batch, head) slab spans 4.6 GB: the buffer descriptors are
     rebased per 64-key tile (the 1280x720x121 config's fused q|k|v rows span 3.4 GB).  Checked
     against a torch fp32 softmax(QK^T/sqrt(d))V on the GPU (test-side reference)."""
@@ -320,7 +327,7 @@ def test_attention_kv_slab_beyond_4gb(K):
     assert mx < 3e-2, mx
 
 
-def test_attention_split_tail(K, monkeypatch):
+def test_attention_split_tail(attn_mfma, K, monkeypatch):
     """Split tail: 270 items on 256 CUs leave 14 items that run as 3 key ranges of 21 tiles each
     (the last ending in a partial tile) and are merged by the combine kernel.  Rows of whole and
     split items against a torch fp32 reference, and the split result against the unsplit grid."""
@@ -355,7 +362,7 @@ def test_attention_split_tail(K, monkeypatch):
 
 
 @pytest.mark.parametrize("B,Sq,Skv,H", [(2, 23000, 512, 3), (1, 20000, 500, 7), (2, 9000, 1000, 8)])
-def test_attention_persistent_matches_one_item_per_block(K, monkeypatch, B, Sq, Skv, H):
+def test_attention_persistent_matches_one_item_per_block(attn_mfma, K, monkeypatch, B, Sq, Skv, H):
     """Persistent grid (one block per CU, several items each, the K/V pipeline running across item
     boundaries, the next item's Q prefetched through LDS): bit-identical to the one-item-per-block
     grid (VS_ATTN_NO_PERSIST=1) -- every item starts from m = 0 exactly as a fresh block -- and
@@ -386,7 +393,7 @@ def test_attention_persistent_matches_one_item_per_block(K, monkeypatch, B, Sq, 
             assert mx < 3e-2, (b, h, mx)
 
 
-def test_attention_strided_views(K):
+def test_attention_strided_views(attn_mfma, K):
     # q/k/v as column slices of a fused [M, 3D] buffer (row stride 3D)
     B, S, H = 1, 200, 2
     D = H * 128
