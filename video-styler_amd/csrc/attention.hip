@@ -556,33 +556,12 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
                 pv_step(ks, cur);
             }
             if constexpr (M16) {
-#ifdef VS_ATTN_PV16_INPLACE
-                if (st < 2) {           // the s[1] half's exps in place beside chunk 1's MFMAs
-#pragma unroll
-                    for (int e = 8 * st; e < 8 * st + 8; ++e) s[1][e] = __builtin_amdgcn_exp2f(s[1][e]);
-#pragma unroll
-                    for (int gq = 2 * st; gq < 2 * st + 2; ++gq)
-                        ((gq & 1) ? rs1 : rs0) += (s[1][4 * gq] + s[1][4 * gq + 1]) + (s[1][4 * gq + 2] + s[1][4 * gq + 3]);
-                    asm volatile("" : "+v"(rs0), "+v"(rs1));
-                } else {                // chunk 1's operands are free: pack the s[1] half
-#pragma unroll
-                    for (int gq = 2 * (st - 2); gq < 2 * (st - 2) + 2; ++gq) {
-                        const int kbl = gq >> 1, qb = gq & 1;
-                        const bf16x2_t w0 = {(__bf16)s[1][4 * gq], (__bf16)s[1][4 * gq + 1]};
-                        const bf16x2_t w1 = {(__bf16)s[1][4 * gq + 2], (__bf16)s[1][4 * gq + 3]};
-                        pk[2 * qb + 1][2 * kbl] = __builtin_bit_cast(unsigned, w0);
-                        pk[2 * qb + 1][2 * kbl + 1] = __builtin_bit_cast(unsigned, w1);
-                    }
-                    asm volatile("" :: "v"(pk[1]), "v"(pk[3]));
-                }
-#else
                 if (st >= 2) {          // chunk 1's operands are free: the s[1] half, 2 groups a step
                     p_chunk(4 + 2 * (st - 2));
                     p_chunk(5 + 2 * (st - 2));
                     asm volatile("" : "+v"(rs0), "+v"(rs1));
                     asm volatile("" :: "v"(pk[1]), "v"(pk[3]));
                 }
-#endif
                 if (st == 3) {          // chunk 0's operands are free once the last MFMAs issue
 #pragma unroll
                     for (int ss = 0; ss < 4; ++ss) p_pack(ss);
@@ -664,31 +643,6 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
     auto exact_split = [&](bool first, int kv0, bool low) __attribute__((always_inline)) {
         // recompute S0 when an exp2 overflowed, or (first tile, a lane's sum below SUM_MIN) when
         // an in-place exp2 may have underflowed with the row's max also far below m = 0
-#ifdef VS_ATTN_PV16_INPLACE
-        if constexpr (M16) {
-            // the s[1] half was exponentiated in place too (PV phase)
-            if (__any(!(rs0 + rs1 < INFINITY) || low)) {
-#pragma unroll
-                for (int kbl = 0; kbl < 2; ++kbl) {
-                    const int krow = min(kv0 + 32 + 16 * kbl + lr, Skv - 1);
-                    const bf16_t* kp = Kb + (long long)krow * ldk + 8 * lg;
-#pragma unroll
-                    for (int ks = 0; ks < 4; ++ks) {
-                        const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kp + 32 * ks);
-#pragma unroll
-                        for (int qb = 0; qb < 2; ++qb) {
-                            const int g = 2 * kbl + qb;
-                            s[1] = mfma16g(kf, qf[4 * qb + ks], s[1], g, grp4(ks == 0 ? negm : s[1], g));
-                        }
-                    }
-                }
-                if (kv0 + BKV > Skv) mask_half(1, kv0);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) s[1][i] = __builtin_amdgcn_logf(s[1][i]);
-            }
-        }
-#endif
         if (__any(!(rsA + rsB < INFINITY) || low)) {
             if constexpr (M16) {
 #pragma unroll
