@@ -52,8 +52,9 @@ def test_gemm_fp8_integer_exact(M, N, Kd):
 
 
 @pytest.mark.parametrize("epi", ["bias", "gelu", "gate_res"])
-def test_gemm_fp8_random_epilogues(epi):
+def test_gemm_fp8_random_epilogues(epi, monkeypatch):
     K = _k()
+    monkeypatch.setenv("VS_LT_GELU", "0")       # the reference's rounding points (fused GELU: below)
     M, N, Kd = 700, 1024, 1536
     g = torch.Generator().manual_seed(3)
     x = torch.randn(M, Kd, generator=g).to(BF16)
@@ -128,6 +129,7 @@ def test_gemm_fp8_hipblaslt_route_matches_mfma_kernel(epi, monkeypatch):
     x8 = torch.empty(M, Kd, dtype=torch.uint8, device="cuda")
     sc = torch.empty(M, dtype=torch.float32, device="cuda")
     K.quant_fp8_rows(x, x8, sc)
+    monkeypatch.setenv("VS_LT_GELU", "0")       # the two-pass GELU route on both backends
     outs = []
     for be in ("lt", "vstyler"):
         monkeypatch.setenv("VS_FP8_BACKEND", be)
@@ -143,3 +145,40 @@ def test_gemm_fp8_hipblaslt_route_matches_mfma_kernel(epi, monkeypatch):
         torch.cuda.synchronize()
         outs.append(out)
     assert torch.equal(outs[0], outs[1])
+
+
+def test_gemm_fp8_hipblaslt_fused_gelu(monkeypatch):
+    """The default fp8 GELU route: hipBLASLt fp8 with its fused GELU_BIAS epilogue, the GELU-tanh of
+    the fp32 (x8 . w8^T) * scale + bias rounded once.  Against the fp64 GELU of that exact
+    pre-activation it is as close as one rounding allows; from fp8_linear's rounding points
+    (bf16(GELU(bf16(linear))), VS_LT_GELU=0) it differs by at most twice their own error."""
+    K = _k()
+    monkeypatch.delenv("VS_FP8_BACKEND", raising=False)
+    M, N, Kd = 700, 1024, 1536
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(M, Kd, generator=g).to(BF16)
+    w8 = (0.03 * torch.randn(N, Kd, generator=g)).to(torch.float8_e4m3fn)
+    b = (0.1 * torch.randn(N, generator=g)).to(BF16)
+    x8 = torch.empty(M, Kd, dtype=torch.uint8, device="cuda")
+    sc = torch.empty(M, dtype=torch.float32, device="cuda")
+    K.quant_fp8_rows(x.cuda(), x8, sc)
+    xd = x8.cpu().view(torch.float8_e4m3fn).double() * sc.cpu().double()[:, None]
+    pre = xd @ w8.double().t() + b.double()
+
+    def gelu64(v):
+        return 0.5 * v * (1 + torch.tanh(0.7978845608028654 * (v + 0.044715 * v ** 3)))
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("VS_LT_GELU", mode)
+        out = torch.empty(M, N, dtype=BF16, device="cuda")
+        K.gemm_fp8(x8, sc, w8.view(torch.uint8).cuda(), out, epilogue=K.VS_EPI_GELU, bias=b.cuda())
+        outs[mode] = out.cpu()
+    fused, two = outs["1"], outs["0"]
+    ex = gelu64(pre)
+    frac = (fused != ex.to(BF16)).float().mean().item()
+    assert frac < 0.03, frac
+    rel = lambda v: ((v.double() - ex).norm() / ex.norm()).item()   # noqa: E731
+    assert rel(fused) <= rel(two), (rel(fused), rel(two))
+    # the two-pass route's own error against the exact GELU bounds the difference
+    assert (fused.double() - two.double()).abs().max().item() <= \
+        2 * (two.double() - ex).abs().max().item() + 2.0 ** -14

@@ -250,7 +250,7 @@ def test_hotloaded_lora_on_fused_projections_matches_merged():
     assert rl < 1e-2, (mx, rl)
 
 
-@pytest.mark.parametrize("case", ["b1", "cfg2", "cfg2_slg"])
+@pytest.mark.parametrize("case", ["b1", "cfg2", "cfg2_slg", "cfg2_fp8"])
 def test_fused_residual_layernorm_bit_identical(monkeypatch, case):
     """The hipBLASLt route's residual epilogues fused with the LayerNorm that reads the same rows
     next (vs_residual_layernorm: o-proj -> LN3, cross-o -> LN2, FFN-down (+ VACE hint) -> the next
@@ -261,6 +261,10 @@ def test_fused_residual_layernorm_bit_identical(monkeypatch, case):
     cfg = O.WAN_CONFIGS["tiny"]
     W = O.random_weights(cfg, seed=5)
     dit, vace = build(cfg, W)
+    if case.endswith("fp8"):          # fp8 block linears (config 5): always on hipBLASLt fp8
+        from vstyler.models import quantize_fp8_
+        quantize_fp8_(dit)
+        quantize_fp8_(vace)
     lat, cp, cn, vc = O.synthetic_inputs(cfg, 5, 128, 128)
     ctx = cp if case == "b1" else torch.cat([cp, cn])
     slg = (1,) if case == "cfg2_slg" else ()

@@ -197,8 +197,9 @@ int vs_lt_gemm_bias_gelu(const void* a, long long lda, const void* w, long long 
     return lt_gemm(a, lda, w, ldw, c, ldc, m, n, k, bias, nullptr, true, stream);
 }
 
-// C[m][n] = bf16((A8 W8^T) * scale_a[row] + bias), e4m3fn operands (fp8_linear); same contract.
+// C[m][n] = bf16((A8 W8^T) * scale_a[row] + bias), e4m3fn operands (fp8_linear), with `gelu` the
+// GELU-tanh of that fp32 value before the rounding; same contract.
 int vs_lt_gemm_fp8(const void* a8, long long lda, const float* scale_a, const void* w8, long long ldw, void* c,
-                   long long ldc, int m, int n, int k, const void* bias, hipStream_t stream) {
-    return lt_gemm(a8, lda, w8, ldw, c, ldc, m, n, k, bias, scale_a, false, stream);
+                   long long ldc, int m, int n, int k, const void* bias, bool gelu, hipStream_t stream) {
+    return lt_gemm(a8, lda, w8, ldw, c, ldc, m, n, k, bias, scale_a, gelu, stream);
 }

@@ -112,4 +112,4 @@ int vs_lt_gemm_bias(const void* a, long long lda, const void* w, long long ldw, 
 int vs_lt_gemm_bias_gelu(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc, int m,
                          int n, int k, const void* bias, hipStream_t stream);
 int vs_lt_gemm_fp8(const void* a8, long long lda, const float* scale_a, const void* w8, long long ldw, void* c,
-                   long long ldc, int m, int n, int k, const void* bias, hipStream_t stream);   // blaslt.hip
+                   long long ldc, int m, int n, int k, const void* bias, bool gelu, hipStream_t stream);   // blaslt.hip

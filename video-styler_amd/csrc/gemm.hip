@@ -1164,10 +1164,16 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
     // + the epilogue pass: 1.3-1.6x the fp8 MFMA kernel on every 14B block shape at SP=1 and SP=8
     // and bit-identical to it, epilogues included (profiles/r1/gemm_fp8_lt_r1j.log).
     // VS_FP8_BACKEND=vstyler forces the MFMA kernel, which also runs when no workspace is bound.
+    // GELU as in vs_gemm: hipBLASLt's fused GELU_BIAS epilogue unless VS_LT_GELU=0.
     const char* fb = getenv("VS_FP8_BACKEND");
-    if (!(fb && fb[0] == 'v') &&
+    const char* lt_gelu = getenv("VS_LT_GELU");
+    const bool use_lt = !(fb && fb[0] == 'v');
+    if (use_lt && epilogue == VS_EPI_GELU && !(lt_gelu && lt_gelu[0] == '0') &&
+        vs_lt_gemm_fp8(a8, lda, scale_a, w8, ldw, c, ldc, m, n, k, ep.bias, true, (hipStream_t)stream) == VS_OK)
+        return VS_OK;
+    if (use_lt &&
         lt_with_epilogue(c, ldc, m, n, epilogue, ep, (hipStream_t)stream, [&](void* y, long long ldy) {
-            return vs_lt_gemm_fp8(a8, lda, scale_a, w8, ldw, y, ldy, m, n, k, ep.bias, (hipStream_t)stream);
+            return vs_lt_gemm_fp8(a8, lda, scale_a, w8, ldw, y, ldy, m, n, k, ep.bias, false, (hipStream_t)stream);
         }))
         return VS_OK;
     const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;

@@ -57,13 +57,15 @@ def linear(lin, x, out, ws, **epi):
 
 
 def _fusable_lt(lin, M):
-    """True when `lin` on M rows runs as a plain bf16 GEMM on vs_gemm's hipBLASLt route (no fp8 copy,
-    no hot-loaded LoRA): its residual epilogue can then fuse with the LayerNorm that follows
-    (vs_residual_layernorm).  VSTYLER_FUSE_RES_LN=0 disables."""
-    if getattr(lin, "weight_fp8", None) is not None or getattr(lin, "lora_A", None) is not None:
+    """True when `lin` on M rows runs on hipBLASLt (a plain bf16 GEMM on vs_gemm's hipBLASLt route, or
+    the fp8 path, which is always hipBLASLt unless VS_FP8_BACKEND=vstyler), i.e. when its residual
+    epilogue is a separate pass over a staged bf16(acc + bias) anyway: that pass can then fuse with
+    the LayerNorm that follows (vs_residual_layernorm) with the same rounding points.  A hot-loaded
+    LoRA keeps the MFMA kernel's fused epilogue.  VSTYLER_FUSE_RES_LN=0 disables."""
+    if getattr(lin, "lora_A", None) is not None or os.environ.get("VSTYLER_FUSE_RES_LN", "1") == "0":
         return False
-    if os.environ.get("VSTYLER_FUSE_RES_LN", "1") == "0":
-        return False
+    if getattr(lin, "weight_fp8", None) is not None:
+        return not os.environ.get("VS_FP8_BACKEND", "").startswith("v")
     return K.gemm_route(M, lin.out_features, lin.in_features)
 
 
@@ -382,7 +384,7 @@ class DiTBlock(nn.Module):
         if _fusable_lt(sa.o, M):
             # hipBLASLt route: bf16(o Wo^T + b) staged, then gate-residual + LN3 in one pass
             y = ws.get("res_y" + p["tag"], (M, D))
-            K.gemm(o, sa.o.weight, y, bias=sa.o.bias)
+            linear(sa.o, o, y, ws)
             K.residual_layernorm(y, x, h, eps, epilogue=K.VS_EPI_GATE_RES, gate=mod[:, 2], gate_bstride=6 * D,
                                  gate_rows=S, weight=self.norm3.weight, bias=self.norm3.bias)
         else:
@@ -405,7 +407,7 @@ class DiTBlock(nn.Module):
         K.attention(q, kc, vc, o, self.num_heads, nb)
         if _fusable_lt(ca.o, M):
             y = ws.get("res_y" + p["tag"], (M, D))
-            K.gemm(o, ca.o.weight, y, bias=ca.o.bias)
+            linear(ca.o, o, y, ws)
             K.residual_layernorm(y, x, h, eps, epilogue=K.VS_EPI_RES, alpha=1.0, shift=mod[:, 3], scale=mod[:, 4],
                                  mod_bstride=6 * D, rows_per_batch=S)
         else:
@@ -418,7 +420,7 @@ class DiTBlock(nn.Module):
             # bf16(f W2^T + b) staged, then x += gate * y (+ hint) and the next consumer's modulated
             # LayerNorm of the new x into h (its LN1 / the head's norm) in one pass
             y = ws.get("res_y" + p["tag"], (M, D))
-            K.gemm(f, self.ffn[2].weight, y, bias=self.ffn[2].bias)
+            linear(self.ffn[2], f, y, ws)
             b0, nb = p["b0"], p["nb"]
             K.residual_layernorm(y, x, h, eps, epilogue=K.VS_EPI_GATE_RES, gate=mod[:, 5], gate_bstride=6 * D,
                                  gate_rows=S, hint=p["hint"], hint_scale=hint_scale,
