@@ -285,6 +285,7 @@ def main():
             torch.cuda.synchronize()
     TIMER.enabled = False
     attn_ms, attn_n = TIMER.mean_ms("self_attn")
+    attn_tf = TIMER.tflops("self_attn")       # summed launch FLOPs / summed launch time
     if world > 1:
         tt = torch.tensor([elapsed], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -294,9 +295,11 @@ def main():
     ms_per_step = 1000 * elapsed / args.steps
     value = args.steps / elapsed
     fl_step = step_flops(m, S)
-    # self-attention launch: 4*S_q*S_kv*d per head, B=2 (CFG); under SP a rank runs H/p heads
-    attn_flops = 4.0 * S * S * m["dim"] * 2 / world
-    achieved = attn_flops / (attn_ms / 1000) / 1e12
+    # self-attention: 4*S_q*S_kv*d per head and sample, recorded per launch (vstyler.models.attn_flops):
+    # one launch per block holds both CFG samples and all heads at SP=1; under Ulysses SP a rank's
+    # launch holds H/p heads, one sample per launch with the micro-batch overlap
+    achieved = attn_tf
+    attn_flops = achieved * 1e12 * attn_ms / 1000
     out = {
         "metric": f"denoising steps/sec, Wan2.1-VACE-{args.model} {args.width}x{args.height}x{args.frames}"
                   + (" [config 5: fp8 e4m3 block linears, UniPC, CFG 1.2, SLG]" if args.config == "fp8" else ""),
@@ -327,7 +330,7 @@ def main():
                      "avg_launch_ms": round(attn_ms, 3), "launches": attn_n,
                      "timing": "HIP events on the launch stream, " + ("one instrumented eager step after the "
                                "timed hipGraph replays" if use_graph else "every launch of the timed steps"),
-                     "flops_per_launch": attn_flops},
+                     "flops_per_launch": round(attn_flops, -6)},
     }
     if world == 1 and not args.no_e2e and args.config == "bf16":
         out["e2e"] = e2e_components(dev, args.frames, args.height, args.width, elapsed / args.steps)

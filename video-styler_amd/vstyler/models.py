@@ -225,12 +225,13 @@ class KernelTimer:
         self.enabled = False
         self.events = {}
 
-    def start(self, name):
+    def start(self, name, flops=0.0):
+        """flops: the launch's algorithmic FLOPs (tflops() divides their sum by the summed time)."""
         if not self.enabled or torch.cuda.is_current_stream_capturing():
             return None
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        self.events.setdefault(name, []).append((e0, e1))
+        self.events.setdefault(name, []).append((e0, e1, float(flops)))
         return e1
 
     def stop(self, e1):
@@ -242,13 +243,27 @@ class KernelTimer:
         if not ev:
             return None, 0
         torch.cuda.synchronize()
-        return sum(a.elapsed_time(b) for a, b in ev) / len(ev), len(ev)
+        return sum(a.elapsed_time(b) for a, b, _ in ev) / len(ev), len(ev)
+
+    def tflops(self, name):
+        """Summed FLOPs / summed launch time of the bracketed launches (TFLOP/s), or None."""
+        ev = self.events.get(name, [])
+        if not ev:
+            return None
+        torch.cuda.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b, _ in ev)
+        return sum(f for _, _, f in ev) / (ms / 1000.0) / 1e12 if ms > 0 else None
 
     def reset(self):
         self.events = {}
 
 
 TIMER = KernelTimer()
+
+
+def attn_flops(q, k, batch):
+    """4 Sq Skv (heads x d) per sample: QK^T and PV of one attention launch (q: [batch Sq, heads d])."""
+    return 4.0 * (q.shape[0] // batch) * (k.shape[0] // batch) * q.shape[1] * batch
 
 
 class RunCtx:
@@ -371,7 +386,7 @@ class DiTBlock(nn.Module):
         if rc.sp is not None:
             rc.sp.attend(p["xchg"])
         else:
-            ev = TIMER.start("self_attn")
+            ev = TIMER.start("self_attn", attn_flops(p["q"], p["k"], p["nb"]))
             K.attention(p["q"], p["k"], p["v"], p["o"], self.num_heads, p["nb"])
             TIMER.stop(ev)
 

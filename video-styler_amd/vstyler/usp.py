@@ -69,8 +69,8 @@ class UlyssesGroup:
         K.ulysses_permute(src, dst, batch, s_local, self.world_size, cpr, ld_local, jstride, mode)
 
     def _attention(self, q, k, v, o, heads, batch):
-        from .models import TIMER
-        ev = TIMER.start("self_attn")
+        from .models import TIMER, attn_flops
+        ev = TIMER.start("self_attn", attn_flops(q, k, batch))
         K.attention(q, k, v, o, heads, batch)
         TIMER.stop(ev)
 
