@@ -42,6 +42,25 @@ ctx = (0.1 * torch.randn(2, 512, 4096, generator=g)).to(torch.bfloat16).to(dev)
 vc = torch.ones(1, 96, T, Hl, Wl).to(torch.bfloat16).to(dev)
 t = torch.tensor([999.0], device=dev).to(torch.bfloat16)
 OVL = os.environ.get("VSTYLER_SP_OVERLAP", "1") != "0"
+AB = os.environ.get("SPC_AB")        # "VAR=a,b": interleaved rounds of the env settings, one process
+if AB:
+    var, vals = AB.split("=")
+    P = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    sp = LocalUlysses(P, overlap=OVL)
+    fn = lambda: model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=ctx, vace_context=vc,
+                                    use_unified_sequence_parallel=True, sp_group=sp)
+    res = {v: [] for v in vals.split(",")}
+    for rnd in range(4):
+        for v in res:
+            os.environ[var] = v
+            fn(); torch.cuda.synchronize()
+            ts = []
+            for _ in range(2):
+                t0 = time.perf_counter(); fn(); torch.cuda.synchronize(); ts.append(time.perf_counter() - t0)
+            res[v].append(1000 * min(ts))
+    for v, ms in res.items():
+        print(f"SP={P} {var}={v}: per-rank CFG step " + " ".join(f"{x:.1f}" for x in ms) + " ms", flush=True)
+    sys.exit(0)
 for P in [int(a) for a in sys.argv[1:]] or [1, 8]:
     sp = LocalUlysses(P, overlap=OVL) if P > 1 else None
     fn = lambda: model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=ctx, vace_context=vc,

@@ -177,7 +177,10 @@ def _rccl_worker(port, q):
         t = torch.tensor([833.3333]).to(torch.bfloat16).cuda()
         ctx = torch.cat([cp, cn]).cuda()
         single = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx, vace_context=vc.cuda())
-        for overlap in (True, False):
+        # overlap on with phase 4 merged over both samples (default) and per sample, then off
+        for overlap, merge, key in ((True, "1", "model_overlap1"), (True, "0", "model_overlap1_permicro"),
+                                    (False, "1", "model_overlap0")):
+            os.environ["VSTYLER_SP_MERGE_FFN"] = merge
             sp = UlyssesGroup(force_collectives=True)
             sp.overlap = overlap
             par = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx,
@@ -186,9 +189,9 @@ def _rccl_worker(port, q):
             # 2 all-to-alls per self-attention (x2 micro-batches with overlap) + 1 gather
             nblk = cfg["num_layers"] + len(cfg["vace_layers"])
             want_calls = nblk * 2 * (2 if overlap else 1) + 1
-            res[f"model_overlap{int(overlap)}"] = torch.equal(single.cpu(), par.cpu()) and \
-                sp.collective_calls == want_calls
-            res[f"calls_overlap{int(overlap)}"] = (sp.collective_calls, want_calls)
+            res[key] = torch.equal(single.cpu(), par.cpu()) and sp.collective_calls == want_calls
+            res["calls_" + key] = (sp.collective_calls, want_calls)
+        os.environ.pop("VSTYLER_SP_MERGE_FFN")
         torch.distributed.destroy_process_group()
         q.put(res)
     except Exception:  # pragma: no cover
@@ -208,3 +211,4 @@ def test_ulysses_rccl_world1_bit_identical():
     print("rccl world1:", res)
     assert res["stages"] is True and res["gather"] is True, res
     assert res["model_overlap1"] is True and res["model_overlap0"] is True, res
+    assert res["model_overlap1_permicro"] is True, res

@@ -301,12 +301,14 @@ class DiTBlock(nn.Module):
         on all rows: the FFN-down gate-residual (+ VACE hint) is then fused with its modulated
         LayerNorm (vs_residual_layernorm, one pass over the rows instead of two).
 
-        Three phases per micro-batch: (1) LN1 + q/k/v + QK-RMSNorm/RoPE, (2) self-attention,
-        (3) o-proj (gated residual), cross-attention, FFN (gated residual + VACE hint).  Without SP
-        the whole CFG batch is one micro-batch.  Under Ulysses SP with overlap on, each CFG sample
-        is its own micro-batch and phases are issued 1(0) 1(1) 2(0) 2(1) 3(0) 3(1): sample 0's q|k|v
-        all-to-all runs under sample 1's projections, sample 1's under sample 0's attention, and
-        the return exchanges under the other sample's attention / o-proj / cross-attn / FFN."""
+        Four phases per micro-batch: (1) LN1 + q/k/v + QK-RMSNorm/RoPE, (2) self-attention,
+        (3) o-proj (gated residual) + LN3, (4) cross-attention, FFN (gated residual + VACE hint).
+        Without SP the whole CFG batch is one micro-batch.  Under Ulysses SP with overlap on, each
+        CFG sample is its own micro-batch for phases 1-3, issued 1(0) 1(1) 2(0) 2(1) 3(0) 3(1): sample
+        0's q|k|v all-to-all runs under sample 1's projections, sample 1's under sample 0's
+        attention, sample 0's return exchange under sample 1's attention and sample 1's under sample
+        0's o-proj; phase 4 then runs once on both samples' rows (GEMMs of 2S/p rows instead of two
+        of S/p: VSTYLER_SP_MERGE_FFN=0 keeps it per sample)."""
         B, S, D, ws = rc.batch, rc.seq, self.dim, rc.ws
         if rc.pre_mod is not None:          # the previous block already ran this one's LN1
             mod, ln1_done = rc.pre_mod, True
@@ -325,16 +327,20 @@ class DiTBlock(nn.Module):
             parts = [self._part(x, mod, rc, 0, B, hint, "")]
         for p in parts:
             p["ln1_done"] = ln1_done
+        # phase 4 on all rows at once (the overlapped SP micro-batches)
+        tail = self._part(x, mod, rc, 0, B, hint, "") if len(parts) > 1 and \
+            os.environ.get("VSTYLER_SP_MERGE_FFN", "1") != "0" else None
         # the fused FFN-down epilogue needs the consumer's modulation first (its own mod buffer)
         fuse = None
-        if nxt is not None and only_batch is None and _fusable_lt(self.ffn[2], parts[0]["M"]) and \
+        if nxt is not None and only_batch is None and \
+                _fusable_lt(self.ffn[2], (tail or parts[0])["M"]) and \
                 os.environ.get("VSTYLER_FUSE_FFN_LN", "1") != "0":
             if isinstance(nxt, DiTBlock):
                 nslot = rc.mod_slot ^ 1
                 nmod = ws.get(f"mod{nslot}", (B, 6, D))
                 K.mod_add(nxt.modulation.view(6, D), t_mod, nmod, 6 * D, D)
                 fuse = dict(shift=nmod[:, 0], scale=nmod[:, 1], bstride=6 * D, mod=nmod, slot=nslot)
-            elif isinstance(nxt, Head) and len(parts) == 1:
+            elif isinstance(nxt, Head) and (len(parts) == 1 or tail is not None):
                 hm = nxt.modulation_for(rc.t_emb, rc)
                 fuse = dict(shift=hm[:, 0], scale=hm[:, 1], bstride=2 * D, mod=None)
         for p in parts:
@@ -342,7 +348,11 @@ class DiTBlock(nn.Module):
         for p in parts:
             self._phase_attn(p, rc)
         for p in parts:
-            self._phase_out(p, rc, hint_scale, fuse)
+            self._phase_o(p, rc)
+            if tail is None:
+                self._phase_cross_ffn(p, rc, hint_scale, fuse)
+        if tail is not None:
+            self._phase_cross_ffn(tail, rc, hint_scale, fuse)
         if fuse is not None:
             if fuse["mod"] is not None:
                 rc.pre_mod = fuse["mod"]
@@ -356,8 +366,8 @@ class DiTBlock(nn.Module):
         r0, M = b0 * S, nb * S
         p = dict(nb=nb, M=M, b0=b0, x=x[r0:r0 + M], mod=mod[b0:b0 + nb], ctx=rc.ctx[b0 * L:(b0 + nb) * L],
                  hint=None if hint is None else hint[r0:r0 + M], tag=tag)
-        for n in ("h", "q", "k", "v", "o"):
-            p[n] = ws.get(n + tag, (M, D))
+        for n in ("h", "q", "k", "v", "o"):     # row slices of the all-samples buffers
+            p[n] = ws.get(n, (rc.batch * S, D))[r0:r0 + M]
         return p
 
     def _phase_qkv(self, p, rc):
@@ -390,9 +400,9 @@ class DiTBlock(nn.Module):
             K.attention(p["q"], p["k"], p["v"], p["o"], self.num_heads, p["nb"])
             TIMER.stop(ev)
 
-    def _phase_out(self, p, rc, hint_scale, fuse=None):
+    def _phase_o(self, p, rc):
         S, D, eps, ws = rc.seq, self.dim, self.eps, rc.ws
-        x, mod, h, q, o, nb, M = p["x"], p["mod"], p["h"], p["q"], p["o"], p["nb"], p["M"]
+        x, mod, h, o, M = p["x"], p["mod"], p["h"], p["o"], p["M"]
         if rc.sp is not None:
             rc.sp.finish(p["xchg"], o)
         sa = self.self_attn
@@ -407,6 +417,10 @@ class DiTBlock(nn.Module):
                    gate_bstride=6 * D, rows_per_batch=S)
             # --- cross-attention (wan_video_dit.py:227, :171-186)
             K.layernorm_modulate(x, h, eps, weight=self.norm3.weight, bias=self.norm3.bias)
+
+    def _phase_cross_ffn(self, p, rc, hint_scale, fuse=None):
+        S, D, eps, ws = rc.seq, self.dim, self.eps, rc.ws
+        x, mod, h, q, o, nb, M = p["x"], p["mod"], p["h"], p["q"], p["o"], p["nb"], p["M"]
         ca = self.cross_attn
         L = rc.ctx_len
         linear(ca.q, h, q, ws)
