@@ -1031,7 +1031,8 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
     // them and an item has at least PERSIST_MIN_TILES key tiles (VS_ATTN_NO_PERSIST=1: one block per
     // item, the r1 grid)
     const int ncu = vs_cus_for_split(nullptr);
-    const bool no_persist = getenv("VS_ATTN_NO_PERSIST") != nullptr;
+    const char* np_env = getenv("VS_ATTN_NO_PERSIST");
+    const bool no_persist = np_env && np_env[0] == '1';
     // (the Q prefetch and the O drain address a wave's rows through 32-bit buffer ranges)
     const bool span_ok = (long long)sq * ldq * 2 < (1LL << 32) && (long long)sq * ldo * 2 < (1LL << 32);
     const int npers =
