@@ -200,6 +200,13 @@ int vs_axpy(void* x, const void* y, float scale, long long n, void* stream);
  * reassembly (diffsynth/pipelines/wan_video_new.py:1459-1462). */
 int vs_ulysses_permute(const void* src, void* dst, int batch, int s_local, int world,
                        int cols_per_rank, long long ld_local, long long jstride, int mode, void* stream);
+/* The same with the packed rows `packed_ld` elements apart (>= cols_per_rank):
+ *   packed = j*jstride + (b*s_local + t)*packed_ld + c.
+ * With packed_ld = 3*cols_per_rank and q / k / v at column offsets 0 / cpr / 2cpr of each row, the
+ * all-to-all of one CFG sample delivers q|k|v rows of the whole sequence in token order, which the
+ * attention reads in place (no packed->full pass). */
+int vs_ulysses_permute_rows(const void* src, void* dst, int batch, int s_local, int world, int cols_per_rank,
+                            long long ld_local, long long jstride, long long packed_ld, int mode, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * UMT5-XXL text encoder (diffsynth/models/wan_video_text_encoder.py; GEMMs / norms / per-head

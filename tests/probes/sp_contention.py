@@ -66,11 +66,16 @@ t = torch.tensor([999.0], device=dev).to(torch.bfloat16)
 P = 8
 Gs = [int(x) for x in os.environ.get("SPC_G", "0,16,64").split(",")]
 pers = os.environ.get("SPC_PERSIST", "1,0").split(",")
-cases = [(G, pz, ov) for G in Gs for pz in pers for ov in (True, False)]
+ovs = [o == "1" for o in os.environ.get("SPC_OVERLAP", "1,0").split(",")]
+ev = os.environ.get("SPC_ENV", "")          # "VAR=a,b": one more interleaved dimension
+evar, evals = ev.split("=") if ev else ("", "-")
+cases = [(G, pz, ov, e) for G in Gs for pz in pers for ov in ovs for e in evals.split(",")]
 res = {c: [] for c in cases}
 for rnd in range(3):
     for c in cases:
-        G, pz, ov = c
+        G, pz, ov, e = c
+        if evar:
+            os.environ[evar] = e
         os.environ["VS_ATTN_NO_PERSIST"] = "0" if pz == "1" else "1"
         sp = FakeCommUlysses(P, overlap=ov, nblocks=G)
         fn = lambda: model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=ctx, vace_context=vc,
@@ -81,6 +86,6 @@ for rnd in range(3):
             t0 = time.perf_counter(); fn(); torch.cuda.synchronize(); ts.append(time.perf_counter() - t0)
         res[c].append(1000 * min(ts))
     print(f"round {rnd} done", flush=True)
-for (G, pz, ov), ms in res.items():
-    print(f"SP=8 comm-G={G:3d} persist={pz} overlap={int(ov)}: " + " ".join(f"{x:.1f}" for x in ms) + " ms",
-          flush=True)
+for (G, pz, ov, e), ms in res.items():
+    print(f"SP=8 comm-G={G:3d} persist={pz} overlap={int(ov)}" + (f" {evar}={e}" if evar else "") + ": "
+          + " ".join(f"{x:.1f}" for x in ms) + " ms", flush=True)

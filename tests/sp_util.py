@@ -6,8 +6,8 @@ import torch.distributed as dist
 from vstyler.usp import UlyssesGroup, _Done
 
 
-def permute_ref(src, dst, batch, s_local, world, cpr, ld_local, jstride, mode):
-    """Pure-torch statement of vs_ulysses_permute (include/vstyler.h)."""
+def permute_ref(src, dst, batch, s_local, world, cpr, ld_local, jstride, mode, packed_ld=None):
+    """Pure-torch statement of vs_ulysses_permute_rows (include/vstyler.h)."""
     B, Sl, P = batch, s_local, world
 
     def flat(t):      # element view of t's storage from its first element (row-strided views too)
@@ -20,7 +20,7 @@ def permute_ref(src, dst, batch, s_local, world, cpr, ld_local, jstride, mode):
     b = torch.arange(B).view(1, B, 1, 1)
     t = torch.arange(Sl).view(1, 1, Sl, 1)
     c = torch.arange(cpr).view(1, 1, 1, cpr)
-    packed = j * jstride + (b * Sl + t) * cpr + c
+    packed = j * jstride + (b * Sl + t) * (cpr if packed_ld is None else packed_ld) + c
     local = (b * Sl + t) * ld_local + j * cpr + c
     full = (b * P * Sl + j * Sl + t) * cpr + c
     so, d = {0: (local, packed), 1: (packed, local), 2: (packed, full), 3: (full, packed)}[mode]
@@ -35,8 +35,8 @@ class CpuUlysses(UlyssesGroup):
         super().__init__(group)
         self.attn_fn = attn_fn
 
-    def _permute(self, src, dst, batch, s_local, cpr, ld_local, jstride, mode):
-        permute_ref(src, dst, batch, s_local, self.world_size, cpr, ld_local, jstride, mode)
+    def _permute(self, src, dst, batch, s_local, cpr, ld_local, jstride, mode, packed_ld=None):
+        permute_ref(src, dst, batch, s_local, self.world_size, cpr, ld_local, jstride, mode, packed_ld)
 
     def _attention(self, q, k, v, o, heads, batch):
         o.copy_(self.attn_fn(q, k, v, heads, batch))

@@ -517,3 +517,18 @@ def test_ulysses_permute_roundtrip(K):
     packed2 = torch.empty_like(packed)
     K.ulysses_permute(full, packed2, B, Sl, P, cpr, D, B * Sl * cpr, 3)
     assert torch.equal(packed2, packed)
+
+
+def test_ulysses_permute_interleaved_rows(K):
+    """One sample's q|k|v packed as [rank j][token t][q | k | v] (packed_ld = 3 cpr): chunk j, read
+    as rows, is rank j's heads of q|k|v for every local token, so the concatenated chunks are the
+    whole sequence's q|k|v rows in token order (the layout usp.attend reads in place)."""
+    Sl, P, cpr = 40, 4, 128
+    D = P * cpr
+    src = [rnd(Sl, 3 * D, seed=81 + i).cuda()[:, i * D:(i + 1) * D] for i in range(3)]   # fused q|k|v slices
+    send = torch.empty(P * 3 * Sl * cpr, dtype=BF16, device="cuda")
+    for i, t in enumerate(src):
+        K.ulysses_permute(t, send[i * cpr:], 1, Sl, P, cpr, t.stride(0), 3 * Sl * cpr, 0, packed_ld=3 * cpr)
+    rows = send.view(P, Sl, 3, cpr)
+    for i, t in enumerate(src):
+        assert torch.equal(rows[:, :, i], t.reshape(Sl, P, cpr).permute(1, 0, 2))

@@ -33,22 +33,22 @@ def _init(rank, world, port):
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
 
 
-def _cpu_worker(rank, world, port, q):
+def _cpu_worker(rank, world, port, q, B=2):
     try:
         _init(rank, world, port)
         from oracle import wan_oracle as O
         from sp_util import CpuUlysses
         from vstyler.models import RunCtx, Workspace
         torch.manual_seed(0)
-        B, S, H = 2, 48, 4
+        S, H = 48, 4
         D = H * 128
         qf, kf, vf = (torch.randn(B, S, D).to(torch.bfloat16) for _ in range(3))
         ref = O.attention(qf, kf, vf, H)
 
         def attn(qq, kk, vv, heads, batch):
             s = qq.shape[0] // batch
-            return O.attention(qq.view(batch, s, -1), kk.view(batch, s, -1), vv.view(batch, s, -1), heads).view(
-                batch * s, -1)
+            return O.attention(qq.reshape(batch, s, -1), kk.reshape(batch, s, -1), vv.reshape(batch, s, -1),
+                               heads).reshape(batch * s, -1)
         sp = CpuUlysses(attn)
         ws = Workspace("cpu")
         rc = RunCtx(B, S, (1, 1, S), None, None, 0, ws)
@@ -68,11 +68,12 @@ def _cpu_worker(rank, world, port, q):
         q.put((rank, repr(e), None, None))
 
 
-def test_ulysses_exchange_cpu_gloo_world2():
+@pytest.mark.parametrize("B", [2, 1])     # B=1: q|k|v rows delivered in token order, no re-layout
+def test_ulysses_exchange_cpu_gloo_world2(B):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_cpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_cpu_worker, args=(r, 2, port, q, B)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=300) for _ in procs)

@@ -435,13 +435,13 @@ __global__ void axpy_kernel(bf16_t* __restrict__ x, const bf16_t* __restrict__ y
 
 // Ulysses sequence-parallel row permutations (8 bf16 = 16 B per thread).  Canonical index
 // (j, b, t, c): rank-chunk j, batch b, local token t, column c within a rank's head group.
-//   packed: j*jstride + (b*Sl + t)*cpr + c         (all_to_all_single chunk j)
+//   packed: j*jstride + (b*Sl + t)*pld + c         (all_to_all_single chunk j; pld >= cpr)
 //   local : (b*Sl + t)*ld + j*cpr + c             (token-sharded activations, all heads)
 //   full  : (b*P*Sl + j*Sl + t)*cpr + c            (head-sharded, full sequence)
 // mode 0 local->packed, 1 packed->local, 2 packed->full, 3 full->packed.
 __global__ void ulysses_permute_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst, int B,
-                                       int Sl, int P, int cpr, long long ld, long long jstride, int mode,
-                                       long long total8) {
+                                       int Sl, int P, int cpr, long long ld, long long jstride, long long pld,
+                                       int mode, long long total8) {
     const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (i >= total8) return;
     const int c8 = cpr >> 3;
@@ -451,7 +451,7 @@ __global__ void ulysses_permute_kernel(const bf16_t* __restrict__ src, bf16_t* _
     r /= Sl;
     const int b = (int)(r % B);
     const int j = (int)(r / B);
-    const long long packed = j * jstride + ((long long)b * Sl + t) * cpr + c;
+    const long long packed = j * jstride + ((long long)b * Sl + t) * pld + c;
     const long long local = ((long long)b * Sl + t) * ld + (long long)j * cpr + c;
     const long long full = ((long long)b * P * Sl + (long long)j * Sl + t) * cpr + c;
     long long so, d;
@@ -620,20 +620,29 @@ extern "C" int vs_axpy(void* x, const void* y, float scale, long long n, void* s
 }
 
 
-extern "C" int vs_ulysses_permute(const void* src, void* dst, int batch, int s_local, int world,
-                                  int cols_per_rank, long long ld_local, long long jstride, int mode,
-                                  void* stream) {
+extern "C" int vs_ulysses_permute_rows(const void* src, void* dst, int batch, int s_local, int world,
+                                       int cols_per_rank, long long ld_local, long long jstride,
+                                       long long packed_ld, int mode, void* stream) {
     if (!src || !dst || batch <= 0 || s_local <= 0 || world <= 0 || cols_per_rank <= 0) return VS_E_INVALID;
-    if (cols_per_rank % 8 || (ld_local & 7) || (jstride & 7) || mode < 0 || mode > 3) return VS_E_INVALID;
+    if (cols_per_rank % 8 || (ld_local & 7) || (jstride & 7) || (packed_ld & 7) || mode < 0 || mode > 3)
+        return VS_E_INVALID;
     if ((mode <= 1) && ld_local < (long long)world * cols_per_rank) return VS_E_INVALID;
-    if (jstride < (long long)batch * s_local * cols_per_rank) return VS_E_INVALID;
+    if (packed_ld < cols_per_rank) return VS_E_INVALID;
+    if (jstride < ((long long)batch * s_local - 1) * packed_ld + cols_per_rank) return VS_E_INVALID;
     if (!al16(src) || !al16(dst)) return VS_E_INVALID;
     const long long total8 = (long long)world * batch * s_local * (cols_per_rank / 8);
     hipLaunchKernelGGL(ulysses_permute_kernel, dim3(nblk(total8, 256)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)src, (bf16_t*)dst, batch, s_local, world, cols_per_rank, ld_local,
-                       jstride, mode, total8);
+                       jstride, packed_ld, mode, total8);
     VS_CHECK_LAUNCH();
     return VS_OK;
+}
+
+extern "C" int vs_ulysses_permute(const void* src, void* dst, int batch, int s_local, int world,
+                                  int cols_per_rank, long long ld_local, long long jstride, int mode,
+                                  void* stream) {
+    return vs_ulysses_permute_rows(src, dst, batch, s_local, world, cols_per_rank, ld_local, jstride,
+                                   cols_per_rank, mode, stream);
 }
 
 extern "C" const char* vs_strerror(int code) {

@@ -75,6 +75,7 @@ SIGNATURES = {
     "vs_mod_add": [_P, _P, _P, _I, _I, _I, _LL, _LL, _P],
     "vs_axpy": [_P, _P, _F, _LL, _P],
     "vs_ulysses_permute": [_P, _P, _I, _I, _I, _I, _LL, _LL, _I, _P],
+    "vs_ulysses_permute_rows": [_P, _P, _I, _I, _I, _I, _LL, _LL, _LL, _I, _P],
     "vs_embed_rows": [_P, _P, _LL, _LL, _P, _LL, _LL, _I, _P],
     "vs_t5_bias_softmax": [_P, _LL, _LL, _P, _LL, _LL, _P, _P, _I, _I, _P, _I, _I, _P],
     "vs_t5_gelu_mul": [_P, _P, _P, _LL, _P],

@@ -293,11 +293,13 @@ def axpy(x, y, scale):
     return x
 
 
-def ulysses_permute(src, dst, batch, s_local, world, cols_per_rank, ld_local, jstride, mode):
-    """Row permutation between token-sharded / all_to_all-packed / head-sharded layouts."""
-    _lib.check(_lib.load().vs_ulysses_permute(src.data_ptr(), dst.data_ptr(), int(batch), int(s_local), int(world),
-                                              int(cols_per_rank), int(ld_local), int(jstride), int(mode),
-                                              _stream(src)))
+def ulysses_permute(src, dst, batch, s_local, world, cols_per_rank, ld_local, jstride, mode, packed_ld=None):
+    """Row permutation between token-sharded / all_to_all-packed / head-sharded layouts (packed rows
+    packed_ld elements apart, default cols_per_rank)."""
+    pld = cols_per_rank if packed_ld is None else packed_ld
+    _lib.check(_lib.load().vs_ulysses_permute_rows(src.data_ptr(), dst.data_ptr(), int(batch), int(s_local),
+                                                   int(world), int(cols_per_rank), int(ld_local), int(jstride),
+                                                   int(pld), int(mode), _stream(src)))
     return dst
 
 

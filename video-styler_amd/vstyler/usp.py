@@ -46,7 +46,7 @@ class _Done:
 
 class _Exchange:
     """In-flight state of one Ulysses attention (one micro-batch of one block)."""
-    __slots__ = ("q", "B", "Sl", "Hp", "cpr", "D", "chunk", "tag", "ws", "work", "work2", "recv2")
+    __slots__ = ("q", "B", "Sl", "Hp", "cpr", "D", "chunk", "tag", "ws", "work", "work2", "recv2", "rows")
 
 
 class UlyssesGroup:
@@ -65,8 +65,8 @@ class UlyssesGroup:
         self.collective_calls = 0
 
     # -------------------------------------------------------------- layout helpers (kernels)
-    def _permute(self, src, dst, batch, s_local, cpr, ld_local, jstride, mode):
-        K.ulysses_permute(src, dst, batch, s_local, self.world_size, cpr, ld_local, jstride, mode)
+    def _permute(self, src, dst, batch, s_local, cpr, ld_local, jstride, mode, packed_ld=None):
+        K.ulysses_permute(src, dst, batch, s_local, self.world_size, cpr, ld_local, jstride, mode, packed_ld)
 
     def _attention(self, q, k, v, o, heads, batch):
         from .models import TIMER, attn_flops
@@ -132,8 +132,15 @@ class UlyssesGroup:
         e.chunk = batch * e.Sl * e.cpr                # elements of one tensor per rank chunk
         send = e.ws.get("sp_send" + tag, (P * 3 * e.chunk,))
         recv = e.ws.get("sp_recv" + tag, (P * 3 * e.chunk,))
+        # one sample: chunk j holds its tokens' q|k|v rows for rank j's heads ([Sl, 3 cpr]), so the
+        # received buffer is the whole sequence's q|k|v rows in token order -- attention reads it in
+        # place.  Several samples: chunk j is [q | k | v] of [B, Sl, cpr] each, re-laid out on arrival.
+        e.rows = batch == 1 and os.environ.get("VSTYLER_SP_ROWS", "1") != "0"
         for i, t in enumerate((q, k, v)):     # row stride: q/k/v may be column slices of a fused q|k|v
-            self._permute(t, send[i * e.chunk:], batch, e.Sl, e.cpr, t.stride(0), 3 * e.chunk, 0)
+            if e.rows:
+                self._permute(t, send[i * e.cpr:], 1, e.Sl, e.cpr, t.stride(0), 3 * e.chunk, 0, 3 * e.cpr)
+            else:
+                self._permute(t, send[i * e.chunk:], batch, e.Sl, e.cpr, t.stride(0), 3 * e.chunk, 0)
         e.work = self._all_to_all(recv, send)
         return e
 
@@ -142,13 +149,19 @@ class UlyssesGroup:
         P, B, Sl, cpr, D, chunk, ws = self.world_size, e.B, e.Sl, e.cpr, e.D, e.chunk, e.ws
         e.work.wait()
         recv = ws.get("sp_recv" + e.tag, (P * 3 * chunk,))
+        of = ws.get("sp_out_full" + e.tag, (B * P * Sl, cpr))
+        e.recv2 = ws.get("sp_recv2" + e.tag, (P * chunk,))
+        if e.rows:
+            # [P Sl, 3 cpr] in token order; O [P Sl, cpr] is already the return exchange's packing
+            rows = recv.view(P * Sl, 3 * cpr)
+            self._attention(rows[:, :cpr], rows[:, cpr:2 * cpr], rows[:, 2 * cpr:], of, e.Hp, 1)
+            e.work2 = self._all_to_all(e.recv2, of.view(-1))
+            return e
         full = ws.get("sp_full" + e.tag, (3, B * P * Sl, cpr))
         for i in range(3):
             self._permute(recv[i * chunk:], full[i], B, Sl, cpr, D, 3 * chunk, 2)
-        of = ws.get("sp_out_full" + e.tag, (B * P * Sl, cpr))
         self._attention(full[0], full[1], full[2], of, e.Hp, B)
         send2 = ws.get("sp_send2" + e.tag, (P * chunk,))
-        e.recv2 = ws.get("sp_recv2" + e.tag, (P * chunk,))
         self._permute(of, send2, B, Sl, cpr, D, chunk, 3)
         e.work2 = self._all_to_all(e.recv2, send2)
         return e
