@@ -22,12 +22,19 @@ _DEFAULT = None
 
 
 def init_distributed():
-    """wan_video_new.py:313-323: env:// rendezvous, one process per GPU; returns the local rank."""
+    """wan_video_new.py:313-323: env:// rendezvous, one process per GPU; returns the local rank.
+    The device is bound BEFORE the process group exists and handed to it as device_id, so RCCL's
+    communicator is created on this rank's GPU (not on the guess cuda:rank % count) at the first
+    collective -- barriers included."""
+    local_rank = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
     if not dist.is_initialized():
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        dist.init_process_group(backend=backend, init_method="env://")
-    local_rank = int(os.environ.get("LOCAL_RANK", dist.get_rank()))
-    if torch.cuda.is_available():
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group(backend="nccl", init_method="env://",
+                                    device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend="gloo", init_method="env://")
+    elif torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
     return local_rank
 
