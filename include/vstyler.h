@@ -24,6 +24,7 @@ extern "C" {
 #define VS_E_INVALID 1     /* bad shape / stride / alignment / null pointer            */
 #define VS_E_LAUNCH 2      /* hipGetLastError() after the launch was not hipSuccess   */
 #define VS_E_UNSUPPORTED 3 /* valid request this build does not implement (e.g. d!=128) */
+#define VS_E_COMM 4        /* RCCL missing or returned an error (vs_sp_last_error)     */
 
 const char* vs_strerror(int code);
 int vs_abi_version(void);
@@ -207,6 +208,30 @@ int vs_ulysses_permute(const void* src, void* dst, int batch, int s_local, int w
  * attention reads in place (no packed->full pass). */
 int vs_ulysses_permute_rows(const void* src, void* dst, int batch, int s_local, int world, int cols_per_rank,
                             long long ld_local, long long jstride, long long packed_ld, int mode, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Ulysses SP collectives over RCCL (xGMI), for hosts without torch.distributed.  Replace the
+ * reference's initialize_usp (diffsynth/pipelines/wan_video_new.py:313-323: init_process_group
+ * "nccl") and the xfuser/yunchang all-to-all + all_gather of the Ulysses attention and head
+ * output (diffsynth/distributed/xdit_context_parallel.py:110-131, wan_video_new.py:1459-1462).
+ * One communicator per process and GPU.  RCCL is opened at vs_sp_init (dlopen "librccl.so.1":
+ * inside a PyTorch process the copy torch loaded), so the rest of the library does not depend on it.
+ * Byte counts are per peer; buffers hold world * bytes_per_rank bytes, chunk j at j*bytes_per_rank
+ * (the vs_ulysses_permute packing).  Calls are stream-ordered and enqueue only (no host sync).
+ * ------------------------------------------------------------------------------------------- */
+#define VS_SP_UNIQUE_ID_BYTES 128
+typedef struct vs_sp_comm vs_sp_comm;
+/* rank 0 creates the id and hands it to every rank out of band (the torch store, MPI, a file) */
+int vs_sp_unique_id(void* out_id);
+/* collective over all `world` ranks; binds the communicator to HIP device `device` */
+int vs_sp_init(int rank, int world, const void* unique_id, int device, vs_sp_comm** out);
+/* recv chunk j <- chunk `rank` of rank j's send (grouped send/recv, all_to_all_single semantics) */
+int vs_sp_all_to_all(vs_sp_comm* comm, const void* send, void* recv, long long bytes_per_rank, void* stream);
+/* recv chunk j <- rank j's send (all_gather_into_tensor semantics) */
+int vs_sp_all_gather(vs_sp_comm* comm, const void* send, void* recv, long long bytes_per_rank, void* stream);
+int vs_sp_comm_destroy(vs_sp_comm* comm);
+/* the text of the last RCCL / loader failure of this thread ("" if none) */
+const char* vs_sp_last_error(void);
 
 /* ---------------------------------------------------------------------------------------------
  * UMT5-XXL text encoder (diffsynth/models/wan_video_text_encoder.py; GEMMs / norms / per-head

@@ -59,6 +59,17 @@ def test_invalid_arguments_rejected_before_launch():
     assert lib.vs_rmsnorm_rope(fake, 256, 4, 256, 128, fake, 1e-6, fake, 1024, 1, 1, 2, 4, 0, None) == 1
     # Ulysses permute: columns not a multiple of 8
     assert lib.vs_ulysses_permute(fake, fake, 1, 4, 2, 12, 24, 48, 0, None) == 1
+    # SP collectives: argument checks come before RCCL is opened or a device is touched
+    out = ctypes.c_void_p()
+    assert lib.vs_sp_unique_id(None) == 1
+    assert lib.vs_sp_init(0, 0, fake, 0, ctypes.byref(out)) == 1          # world < 1
+    assert lib.vs_sp_init(2, 2, fake, 0, ctypes.byref(out)) == 1          # rank >= world
+    assert lib.vs_sp_init(0, 1, None, 0, ctypes.byref(out)) == 1          # no unique id
+    assert lib.vs_sp_all_to_all(None, fake, fake, 16, None) == 1
+    assert lib.vs_sp_all_gather(None, fake, fake, 16, None) == 1
+    assert lib.vs_sp_comm_destroy(None) == 1
+    assert lib.vs_strerror(4).startswith(b"VS_E_COMM")
+    assert lib.vs_sp_last_error() == b""
 
 
 def test_wrappers_raise_on_bad_dtype():

@@ -207,6 +207,23 @@ def _rccl_worker(port, q):
         res["fused_lt_sp"] = torch.equal(outs[0], outs[1])
         os.environ.pop("VS_GEMM_BACKEND")
         os.environ.pop("VSTYLER_FUSE_RES_LN")
+        # (4) the C-ABI collectives (vs_sp_*: RCCL opened by libvstyler itself, its own communicator
+        # and comm stream) under the overlap schedule: bit-identical too, and the raw exchanges
+        # move exactly the bytes asked for
+        sp = UlyssesGroup(force_collectives=True, comm="native")
+        src = torch.arange(4096, dtype=torch.int32, device="cuda")
+        dst = torch.zeros_like(src)
+        sp._all_to_all(dst, src).wait()
+        gat = torch.zeros_like(src)
+        sp._all_gather(gat, src)
+        torch.cuda.synchronize()
+        res["native_raw"] = torch.equal(dst, src) and torch.equal(gat, src)
+        par = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx,
+                                 vace_context=vc.cuda(), use_unified_sequence_parallel=True, sp_group=sp)
+        torch.cuda.synchronize()
+        nblk = cfg["num_layers"] + len(cfg["vace_layers"])
+        res["native_model"] = torch.equal(single.cpu(), par.cpu()) and sp.collective_calls == 2 + nblk * 4 + 1
+        sp.native.close()
         torch.distributed.destroy_process_group()
         q.put(res)
     except Exception:  # pragma: no cover
@@ -228,3 +245,4 @@ def test_ulysses_rccl_world1_bit_identical():
     assert res["model_overlap1"] is True and res["model_overlap0"] is True, res
     assert res["model_overlap1_permicro"] is True, res
     assert res["fused_lt_sp"] is True, res
+    assert res["native_raw"] is True and res["native_model"] is True, res

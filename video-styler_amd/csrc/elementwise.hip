@@ -651,6 +651,7 @@ extern "C" const char* vs_strerror(int code) {
         case VS_E_INVALID: return "VS_E_INVALID: invalid shape, stride, alignment or pointer";
         case VS_E_LAUNCH: return "VS_E_LAUNCH: kernel launch failed";
         case VS_E_UNSUPPORTED: return "VS_E_UNSUPPORTED: configuration not implemented";
+        case VS_E_COMM: return "VS_E_COMM: RCCL unavailable or failed (vs_sp_last_error)";
         default: return "unknown vstyler error";
     }
 }

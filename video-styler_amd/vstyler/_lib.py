@@ -92,8 +92,15 @@ SIGNATURES = {
     "vs_vae_tile_blend": [_P, _LL, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
     "vs_vae_blend_finish": [_P, _P, _P, _I, _LL, _I, _P],
     "vs_vae_copy_frames": [_P, _LL, _P, _LL, _I, _LL, _P],
+    "vs_sp_unique_id": [_P],
+    "vs_sp_init": [_I, _I, _P, _I, ctypes.POINTER(_P)],
+    "vs_sp_all_to_all": [_P, _P, _P, _LL, _P],
+    "vs_sp_all_gather": [_P, _P, _P, _LL, _P],
+    "vs_sp_comm_destroy": [_P],
+    "vs_sp_last_error": [],
 }
-_RESTYPES = {"vs_strerror": ctypes.c_char_p, "vs_split_workspace_bytes": ctypes.c_longlong}
+_RESTYPES = {"vs_strerror": ctypes.c_char_p, "vs_split_workspace_bytes": ctypes.c_longlong,
+             "vs_sp_last_error": ctypes.c_char_p}
 
 _lib = None
 

@@ -10,6 +10,7 @@ VACE unsharded); per self-attention ONE all_to_all_single carries q|k|v packed t
 carries the output back; layout transforms are the vs_ulysses_permute kernel.  Requires
 S % p == 0 and heads % p == 0 (asserted instead of the reference's silent zero padding).
 """
+import ctypes
 import os
 
 import torch
@@ -51,6 +52,73 @@ class _Done:
         pass
 
 
+class _EventWork:
+    """Handle of an exchange enqueued on the native comm stream: wait() makes the current stream
+    wait for it (no host sync), as torch's async NCCL work does."""
+    __slots__ = ("ev",)
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
+class NativeComm:
+    """RCCL through libvstyler's own C ABI (vs_sp_* in include/vstyler.h) instead of
+    torch.distributed's process group -- the path a non-Python host binds.  torch.distributed is
+    used once, to hand rank 0's RCCL unique id to the other ranks.  All-to-alls run on a dedicated
+    stream ordered after the work enqueued so far (RCCL's async pattern); all-gathers run in place on
+    the current stream.  Selected with VSTYLER_SP_COMM=native."""
+
+    def __init__(self, group=None):
+        from . import _lib
+        self._lib = _lib
+        lib = _lib.load()
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        uid = ctypes.create_string_buffer(128)
+        if self.rank == 0:
+            self._check(lib.vs_sp_unique_id(uid))
+        box = [uid.raw if self.rank == 0 else None]
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast_object_list(box, src=src, group=group)
+        uid = ctypes.create_string_buffer(box[0], 128)
+        self.handle = ctypes.c_void_p()
+        self._check(lib.vs_sp_init(self.rank, self.world, uid, torch.cuda.current_device(),
+                                   ctypes.byref(self.handle)))
+        self.stream = torch.cuda.Stream()
+
+    def _check(self, code):
+        if code != 0:
+            lib = self._lib.load()
+            raise RuntimeError(f"vstyler SP comm error {code}: {lib.vs_strerror(code).decode()} "
+                               f"({lib.vs_sp_last_error().decode()})")
+
+    def _bytes_per_rank(self, t):
+        nbytes = t.numel() * t.element_size()
+        if nbytes % self.world:
+            raise ValueError(f"exchange of {nbytes} bytes does not split over {self.world} ranks")
+        return nbytes // self.world
+
+    def all_to_all(self, recv, send):
+        self.stream.wait_stream(torch.cuda.current_stream())
+        self._check(self._lib.load().vs_sp_all_to_all(self.handle, send.data_ptr(), recv.data_ptr(),
+                                                      self._bytes_per_rank(send), self.stream.cuda_stream))
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return _EventWork(ev)
+
+    def all_gather(self, recv, send):
+        self._check(self._lib.load().vs_sp_all_gather(self.handle, send.data_ptr(), recv.data_ptr(),
+                                                      send.numel() * send.element_size(),
+                                                      torch.cuda.current_stream().cuda_stream))
+
+    def close(self):
+        if self.handle:
+            self._check(self._lib.load().vs_sp_comm_destroy(self.handle))
+            self.handle = ctypes.c_void_p()
+
+
 class _Exchange:
     """In-flight state of one Ulysses attention (one micro-batch of one block)."""
     __slots__ = ("q", "B", "Sl", "Hp", "cpr", "D", "chunk", "tag", "ws", "work", "work2", "recv2", "rows")
@@ -61,15 +129,21 @@ class UlyssesGroup:
     all-to-alls (async on RCCL's stream) run under the other half's GEMMs / attention / FFN
     (VSTYLER_SP_OVERLAP=0 disables).  force_collectives: run the sharded path (permutes and RCCL
     collectives) even at world size 1, where model_fn_wan_video otherwise takes the plain path
-    (tests use it to drive the real collectives on a one-GPU box)."""
+    (tests use it to drive the real collectives on a one-GPU box).  comm: "torch" (torch.distributed
+    on the process group, default) or "native" (NativeComm: RCCL through libvstyler's vs_sp_* ABI);
+    default from VSTYLER_SP_COMM."""
 
-    def __init__(self, group=None, force_collectives=False):
+    def __init__(self, group=None, force_collectives=False, comm=None):
         self.group = group
         self.world_size = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.overlap = os.environ.get("VSTYLER_SP_OVERLAP", "1") != "0"
         self.force_collectives = force_collectives
         self.collective_calls = 0
+        comm = comm or os.environ.get("VSTYLER_SP_COMM", "torch")
+        if comm not in ("torch", "native"):
+            raise ValueError(f"VSTYLER_SP_COMM must be 'torch' or 'native', not {comm!r}")
+        self.native = NativeComm(group) if comm == "native" else None
 
     # -------------------------------------------------------------- layout helpers (kernels)
     def _permute(self, src, dst, batch, s_local, cpr, ld_local, jstride, mode, packed_ld=None):
@@ -85,10 +159,15 @@ class UlyssesGroup:
         """Asynchronous: RCCL's stream waits for the work enqueued so far on the current stream;
         the returned handle's wait() makes the current stream wait for the exchange."""
         self.collective_calls += 1
+        if self.native is not None:
+            return self.native.all_to_all(recv, send)
         return dist.all_to_all_single(recv, send, group=self.group, async_op=True)
 
     def _all_gather(self, recv, send):
         self.collective_calls += 1
+        if self.native is not None:
+            self.native.all_gather(recv, send)
+            return
         dist.all_gather_into_tensor(recv, send, group=self.group)
 
     # -------------------------------------------------------------- token sharding
