@@ -5,7 +5,8 @@ One step = the reference's CFG denoising step (wan_video_new.py:518-542): DiT(40
 and the Euler update.  Synthetic data: random-init weights (N(0,0.02), seed 5), seeded latents /
 contexts / VACE context of the real shapes (no checkpoints or datasets are reachable offline).
 
-  python bench.py [--gpus N --steps K --warmup W]        (N>1: torchrun, Ulysses SP over RCCL)
+  python bench.py [--gpus N --steps K --warmup W]        (N>1: torchrun over RCCL; N=2 CFG-parallel,
+                                                         N=4/8 Ulysses SP; VSTYLER_CFG_PARALLEL overrides)
 
 Prints one JSON line with `roofline` (self-attention kernel, HIP-event timed inside the timed
 region) and, on rank 0 at N=1, `cpu_baseline` (the CPU oracle on a bounded token sample).
@@ -155,6 +156,17 @@ def e2e_components(dev, frames, height, width, step_s, steps=50):
             "vae_decode_u8_s": round(dec_s, 3),
             "note": "2 prompts x UMT5-XXL (512 tokens) + VACE unit (2 tiled encodes) + 50 x measured step + "
                     "tiled decode + uint8; random-init weights, synthetic frames"}
+
+
+def _parallelism(sp, world):
+    """'single', 'sp<N>' (Ulysses over N ranks) or 'cfg2' / 'cfg2_sp<u>' (CFG parallelism: one CFG
+    sample per half of the ranks, Ulysses over the u ranks of a half)."""
+    if world == 1 or sp is None:
+        return "single"
+    from vstyler.usp import CfgParallel
+    if isinstance(sp, CfgParallel):
+        return "cfg2" if sp.ulysses is None else f"cfg2_sp{sp.ulysses.world_size}"
+    return f"sp{world}"
 
 
 def main():
@@ -313,7 +325,7 @@ def main():
                                + ("CFG 1.2 as one batch-2 forward + UniPC (config 5)" if args.config == "fp8"
                                   else "CFG 5.0 as one batch-2 forward + Euler"),
                    "model": f"Wan2.1-VACE-{args.model}", "global_batch": 1, "seq_len": S,
-                   "latent_shape": [1, 16, T, Hl, Wl], "parallelism": f"sp{world}" if world > 1 else "single",
+                   "latent_shape": [1, 16, T, Hl, Wl], "parallelism": _parallelism(sp, world),
                    "lora": "merged (zero runtime cost, as the reference's GeneralLoRALoader)",
                    "step_exec": "hipGraph replay" if use_graph else "eager launches",
                    "sampler": ("UniPC bh2 order 2, cfg 1.2, shift 2.0, SLG block 2 @ 0.2-0.7, VACE 0.975"

@@ -61,12 +61,19 @@ if AB:
     for v, ms in res.items():
         print(f"SP={P} {var}={v}: per-rank CFG step " + " ".join(f"{x:.1f}" for x in ms) + " ms", flush=True)
     sys.exit(0)
-for P in [int(a) for a in sys.argv[1:]] or [1, 8]:
+# args: P = Ulysses over P ranks (both CFG samples per rank); cU = CFG parallelism x Ulysses over u
+# ranks (world 2u): a rank's work is its CFG sample's batch-1 forward sharded over u (+ one velocity
+# exchange per step, not modelled)
+for a in sys.argv[1:] or ["1", "8"]:
+    cfgp = a.startswith("c")
+    P = int(a[1:] if cfgp else a)
     sp = LocalUlysses(P, overlap=OVL) if P > 1 else None
-    fn = lambda: model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=ctx, vace_context=vc,
+    c = ctx[0:1] if cfgp else ctx
+    fn = lambda: model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=c, vace_context=vc,
                                     use_unified_sequence_parallel=sp is not None, sp_group=sp)
     fn(); torch.cuda.synchronize()
     ts = []
     for _ in range(3):
         t0 = time.perf_counter(); fn(); torch.cuda.synchronize(); ts.append(time.perf_counter() - t0)
-    print(f"SP={P} overlap={OVL}: per-rank CFG step (eager) {1000 * min(ts):.1f} ms", flush=True)
+    label = f"CFG2 x SP={P} (world {2 * P})" if cfgp else f"SP={P} overlap={OVL}"
+    print(f"{label}: per-rank CFG step (eager) {1000 * min(ts):.1f} ms", flush=True)

@@ -3,7 +3,7 @@ gloo collectives (several ranks sharing one GPU).  Never used by the product pat
 import torch
 import torch.distributed as dist
 
-from vstyler.usp import UlyssesGroup, _Done
+from vstyler.usp import CfgParallel, UlyssesGroup, _Done
 
 
 def permute_ref(src, dst, batch, s_local, world, cpr, ld_local, jstride, mode, packed_ld=None):
@@ -62,3 +62,18 @@ class HostStagedUlysses(UlyssesGroup):
         parts = [torch.empty(send.shape, dtype=send.dtype) for _ in range(self.world_size)]
         dist.all_gather(parts, send.cpu().contiguous(), group=self.group)
         recv.copy_(torch.cat(parts))
+
+
+class HostStagedCfgParallel(CfgParallel):
+    """The product CfgParallel with host-staged gloo collectives (Ulysses halves: HostStagedUlysses),
+    so its ranks can share one GPU in a test."""
+
+    def __init__(self, group=None):
+        super().__init__(group, ulysses_cls=HostStagedUlysses)
+
+    def gather_cfg(self, out_pair, out_local):
+        torch.cuda.synchronize()
+        self.collective_calls += 1
+        parts = [torch.empty(out_local.shape, dtype=out_local.dtype) for _ in range(2)]
+        dist.all_gather(parts, out_local.cpu().contiguous(), group=self.pair_group)
+        out_pair.copy_(torch.cat(parts))

@@ -246,3 +246,99 @@ def test_ulysses_rccl_world1_bit_identical():
     assert res["model_overlap1_permicro"] is True, res
     assert res["fused_lt_sp"] is True, res
     assert res["native_raw"] is True and res["native_model"] is True, res
+
+
+# ------------------------------------------------------------------ CFG parallelism x Ulysses
+def _cfg_cpu_worker(rank, world, port, q):
+    """gloo, world 4: the CfgParallel plan's rank mapping and subgroups (halves = Ulysses groups,
+    pairs = the velocity exchange), and gather_cfg's sample order."""
+    try:
+        _init(rank, world, port)
+        import torch.distributed as dist
+        from vstyler.usp import CfgParallel
+        from sp_util import CpuUlysses
+        plan = CfgParallel(ulysses_cls=lambda g, comm=None: CpuUlysses(None, g))
+        u = world // 2
+        ok = plan.cfg_rank == rank // u and plan.half_rank == rank % u
+        ok = ok and plan.ulysses.world_size == u and plan.ulysses.rank == rank % u
+        ok = ok and plan.full.world_size == world
+        mates = [torch.zeros(1, dtype=torch.int64) for _ in range(2)]
+        dist.all_gather(mates, torch.tensor([rank]), group=plan.pair_group)
+        ok = ok and [int(m) for m in mates] == [rank % u, u + rank % u]
+        # gather_cfg: [1, ...] of this rank's sample -> [2, ...] in sample order
+        local = torch.full((1, 3, 4), float(plan.cfg_rank), dtype=torch.bfloat16)
+        out = torch.empty(2, 3, 4, dtype=torch.bfloat16)
+        plan.gather_cfg(out, local)
+        ok = ok and torch.equal(out[0], torch.zeros(3, 4, dtype=torch.bfloat16)) and \
+            torch.equal(out[1], torch.ones(3, 4, dtype=torch.bfloat16))
+        q.put((rank, ok))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_cfg_parallel_plan_cpu_gloo_world4():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_cfg_cpu_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert all(ok is True for _, ok in res), res
+
+
+def _cfg_gpu_worker(rank, world, port, q):
+    """world ranks share cuda:0: CFG sample per half (Ulysses inside a half when world = 4), the
+    velocities all-gathered across halves == the single-GPU batch-2 forward, bit for bit; also with
+    skip-layer guidance (sample 1 skips block 1) and for a batch-1 forward (the Ulysses fallback)."""
+    try:
+        _init(rank, world, port)
+        from oracle import wan_oracle as O
+        from sp_util import HostStagedCfgParallel
+        from vstyler import model_fn_wan_video
+        from test_model_gpu import build
+        cfg = O.WAN_CONFIGS["tiny"]
+        W = O.random_weights(cfg, seed=5)
+        dit, vace = build(cfg, W, "cuda:0")
+        lat, cp, cn, vc = O.synthetic_inputs(cfg, 5, 128, 128)
+        t = torch.tensor([833.3333]).to(torch.bfloat16).cuda()
+        ctx = torch.cat([cp, cn]).cuda()
+        plan = HostStagedCfgParallel()
+        res = {}
+        cases = [("cfg", ctx, ()), ("cfg_slg", ctx, (1,))]
+        if world == 2:        # the fallback is Ulysses over all ranks: the tiny model has 2 heads
+            cases.append(("nocfg", ctx[0:1], ()))
+        for name, c, slg in cases:
+            single = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=c,
+                                        vace_context=vc.cuda(), slg_blocks=slg)
+            par = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=c,
+                                     vace_context=vc.cuda(), slg_blocks=slg, use_unified_sequence_parallel=True,
+                                     sp_group=plan)
+            torch.cuda.synchronize()
+            res[name] = torch.equal(single.cpu(), par.cpu())
+        res["gathers"] = plan.collective_calls
+        q.put((rank, res))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_cfg_parallel_model_bit_identical_on_one_gpu(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_cfg_gpu_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=600) for _ in procs)
+    for p in procs:
+        p.join(60)
+    for rank, r in res:
+        assert isinstance(r, dict), res
+        assert r["cfg"] is True and r["cfg_slg"] is True and r.get("nocfg", True) is True, res
+        assert r["gathers"] == 2, res

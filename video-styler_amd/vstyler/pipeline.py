@@ -37,17 +37,43 @@ _UNSUPPORTED = ("clip_feature", "y", "reference_latents", "audio_embeds", "motio
 def model_fn_wan_video(dit: WanModel, motion_controller=None, vace: VaceWanModel = None, animate_adapter=None,
                        latents: torch.Tensor = None, timestep: torch.Tensor = None, context: torch.Tensor = None,
                        vace_context=None, vace_scale=1.0, use_unified_sequence_parallel: bool = False,
-                       sp_group=None, slg_blocks=(), tea_cache=None, **kwargs):
+                       sp_group=None, slg_blocks=(), tea_cache=None, cfg_sample=0, **kwargs):
     """One DiT(+VACE) forward (wan_video_new.py:1338-1468) -> [B,16,T,H,W] bf16 velocity.
 
     slg_blocks: skip-layer guidance (config 5, ComfyUI WanVideoSLG): the listed main blocks are
-    skipped for CFG sample 1 (the unconditional pass), run for sample 0 only.
+    skipped for CFG sample 1 (the unconditional pass), run for sample 0 only.  cfg_sample: which
+    CFG sample a batch-1 forward computes (1: it skips the slg_blocks) -- set by the CFG-parallel
+    split below.
 
     `context` is [B, L, text_dim]; latents/timestep/vace_context with batch 1 are broadcast to B
-    (the cfg_merge convention of wan_video_new.py:1361-1364)."""
+    (the cfg_merge convention of wan_video_new.py:1361-1364).
+
+    sp_group may be a vstyler.usp.CfgParallel: a batch-2 (CFG) forward then runs as this rank's
+    sample only (batch 1, Ulysses over its half of the ranks) and the two samples' outputs are
+    all-gathered across the halves -- the same [2,16,T,H,W] as the batched forward."""
     for name in _UNSUPPORTED:
         if kwargs.get(name) is not None:
             raise NotImplementedError(f"model_fn_wan_video: '{name}' is outside the Ditto hot path")
+    if use_unified_sequence_parallel:
+        from .usp import CfgParallel, get_default_group
+        plan = sp_group if sp_group is not None else get_default_group()
+        if isinstance(plan, CfgParallel):
+            if context.shape[0] != 2 or tea_cache is not None:
+                sp_group = plan.full        # no CFG pair to split (or a TeaCache step): Ulysses over all
+            else:
+                c = plan.cfg_rank
+
+                def mine(tn):
+                    return tn[c:c + 1] if tn is not None and tn.dim() > 0 and tn.shape[0] == 2 else tn
+                ts = timestep.reshape(-1)
+                local = model_fn_wan_video(dit, motion_controller, vace, animate_adapter, latents=mine(latents),
+                                           timestep=mine(ts), context=context[c:c + 1],
+                                           vace_context=mine(vace_context), vace_scale=vace_scale,
+                                           use_unified_sequence_parallel=plan.ulysses is not None,
+                                           sp_group=plan.ulysses, slg_blocks=slg_blocks, cfg_sample=c, **kwargs)
+                out = torch.empty((2,) + tuple(local.shape[1:]), device=local.device, dtype=local.dtype)
+                plan.gather_cfg(out, local)
+                return out
     device = latents.device
     ws = _workspace(device)
     B, L = context.shape[0], context.shape[1]
@@ -94,13 +120,17 @@ def model_fn_wan_video(dit: WanModel, motion_controller=None, vace: VaceWanModel
         hints = vace(x, vace_x, t_mod, rc) if vace_x is not None else None
         vmap = vace.vace_layers_mapping if hints is not None else {}
         nblk = len(dit.blocks)
+        # a batch-1 forward of CFG sample 1 (CFG-parallel rank) skips the slg blocks outright
+        slg_here = B > 1 or cfg_sample == 1
         for i, blk in enumerate(dit.blocks):
+            if B == 1 and cfg_sample == 1 and i in slg_blocks:
+                continue
             hint = hints[vmap[i]] if i in vmap else None
             skip = B > 1 and i in slg_blocks
             # the next consumer of x, whose LayerNorm this block's FFN-down epilogue can take over
-            # (not a skip-layer-guidance block, which runs on one sample's rows only)
+            # (not a skip-layer-guidance block, which runs on one sample's rows only or not at all)
             if i + 1 < nblk:
-                nxt = None if (B > 1 and i + 1 in slg_blocks) else dit.blocks[i + 1]
+                nxt = None if (slg_here and i + 1 in slg_blocks) else dit.blocks[i + 1]
             else:
                 nxt = None if tea_cache is not None else dit.head
             blk(x, t_mod, rc, hint=hint, hint_scale=float(vace_scale), only_batch=0 if skip else None, nxt=nxt)

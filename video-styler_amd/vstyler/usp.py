@@ -41,9 +41,20 @@ def init_distributed():
 
 
 def get_default_group():
+    """The parallel plan of the whole world: CfgParallel when VSTYLER_CFG_PARALLEL selects it
+    ("auto", the default: at world size 2, where Ulysses would send half of every q|k|v over
+    one xGMI link per block while CFG parallelism needs one 2-sample velocity exchange per step;
+    "1": at every even world size, Ulysses inside each half; "0": never), else one UlyssesGroup."""
     global _DEFAULT
     if _DEFAULT is None and dist.is_initialized():
-        _DEFAULT = UlyssesGroup()
+        mode = os.environ.get("VSTYLER_CFG_PARALLEL", "auto")
+        if mode not in ("auto", "0", "1"):
+            raise ValueError(f"VSTYLER_CFG_PARALLEL must be auto, 0 or 1, not {mode!r}")
+        world = dist.get_world_size()
+        if world % 2 == 0 and (mode == "1" or (mode == "auto" and world == 2)):
+            _DEFAULT = CfgParallel()
+        else:
+            _DEFAULT = UlyssesGroup()
     return _DEFAULT
 
 
@@ -273,3 +284,37 @@ def _ws_of(t):
     if key not in _WS_BY_DEV:
         _WS_BY_DEV[key] = Workspace(t.device)
     return _WS_BY_DEV[key]
+
+
+class CfgParallel:
+    """CFG parallelism x Ulysses (SURVEY.md §8e's optional extra; not in the reference, whose USP is
+    Ulysses only).  World W = 2u: ranks [c*u, (c+1)*u) of `group` compute CFG sample c (c = 0 the
+    positive prompt, 1 the negative) as a batch-1 forward, its token axis sharded by Ulysses over
+    those u ranks (u = 1: no exchange inside the forward at all); after the head, rank j of half 0
+    and rank j of half 1 all-gather their samples' velocities, so every rank returns the batch-2
+    output of the single-GPU forward (model_fn_wan_video does this when handed a CfgParallel).
+    Per-row work is that of the batch-2 forward.  Batch-1 forwards (no CFG, cfg_scale 1) and
+    TeaCache steps fall back to `self.full`, a Ulysses group over all W ranks.  comm as UlyssesGroup."""
+
+    def __init__(self, group=None, comm=None, ulysses_cls=None):
+        ulysses_cls = ulysses_cls or UlyssesGroup
+        self.group = group
+        self.world_size = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if self.world_size % 2:
+            raise ValueError(f"CFG parallelism needs an even world size, not {self.world_size}")
+        u = self.world_size // 2
+        ranks = dist.get_process_group_ranks(group) if group is not None else list(range(self.world_size))
+        self.cfg_rank, self.half_rank = divmod(self.rank, u)
+        # every rank creates every subgroup, in the same order (torch.distributed.new_group contract)
+        halves = [dist.new_group([ranks[c * u + j] for j in range(u)]) for c in range(2)] if u > 1 else None
+        pairs = [dist.new_group([ranks[j], ranks[u + j]]) for j in range(u)]
+        self.pair_group = pairs[self.half_rank]
+        self.ulysses = ulysses_cls(halves[self.cfg_rank], comm=comm) if u > 1 else None
+        self.full = ulysses_cls(group, comm=comm)
+        self.collective_calls = 0
+
+    def gather_cfg(self, out_pair, out_local):
+        """out_local [1, ...] of this rank's CFG sample -> out_pair [2, ...] (sample 0, sample 1)."""
+        self.collective_calls += 1
+        dist.all_gather_into_tensor(out_pair, out_local.contiguous(), group=self.pair_group)
