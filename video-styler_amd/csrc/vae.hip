@@ -22,35 +22,42 @@ constexpr int BM = 128, BK = 32, CNTHR = 256;
 
 __device__ __forceinline__ int swz(int row, int ch) { return row * 64 + 16 * (ch ^ ((row >> 1) & 3)); }
 
-template <int NB, bool F32>
+template <int NB, bool F32, int PXB, int PRE>
 __global__ __launch_bounds__(CNTHR, 2) void vae_conv_kernel(vs_conv3d p, long long M, int ntn) {
-    constexpr int BN = 32 * NB;
+    // PRE = 2: two register stages, the global loads of step s+2 issued before step s's MFMAs (two
+    // steps of latency cover instead of one).
+    // PXB pixel blocks of 32 per wave: the workgroup tile is 128*PXB pixels x 32*NB channels and each
+    // wave's W fragment feeds PXB MFMAs (PXB = 2: 0.83 LDS fragment reads per MFMA at NB = 3 instead
+    // of 1.33).  The K order of every output's accumulation is the same for both PXB: bit-identical.
+    constexpr int BN = 32 * NB, BMT = BM * PXB;
     constexpr int NBL = (BN * 4 + CNTHR - 1) / CNTHR;
-    constexpr int STAGE = (BM + BN) * 64;
+    constexpr int STAGE = (BMT + BN) * 64;
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long long mt = blockIdx.x / ntn;
     const int n0 = (blockIdx.x % ntn) * BN;
     const int z = blockIdx.y;
-    const long long m0 = mt * BM;
+    const long long m0 = mt * BMT;
 
-    // ---- A (pixel) loader state: row tid>>1, chunks 2*(tid&1)+{0,1}
+    // ---- A (pixel) loader state: rows tid>>1 + 128*b, chunks 2*(tid&1)+{0,1}
     const int arow = tid >> 1, ach = (tid & 1) * 2;
-    const long long am = m0 + arow;
-    const bool avalid = am < M;
-    int ti0, yi0, xi0;
-    const bf16_t* xb;
-    {
-        long long q = avalid ? am : 0;
+    bool avalid[PXB];
+    int ti0[PXB], yi0[PXB], xi0[PXB];
+    const bf16_t* xb[PXB];
+#pragma unroll
+    for (int b = 0; b < PXB; ++b) {
+        const long long am = m0 + arow + BM * b;
+        avalid[b] = am < M;
+        long long q = avalid[b] ? am : 0;
         int xo = (int)(q % p.w_out); q /= p.w_out;
         int yo = (int)(q % p.h_out); q /= p.h_out;
         int to = (int)(q % p.t_out);
         long long nn = q / p.t_out;
-        xb = (const bf16_t*)p.x + z * p.x_zs + nn * p.x_ns + ach * 8;
-        ti0 = to * p.st - p.pt;
-        yi0 = yo * p.sh - p.ph;
-        xi0 = xo * p.sw - p.pw;
+        xb[b] = (const bf16_t*)p.x + z * p.x_zs + nn * p.x_ns + ach * 8;
+        ti0[b] = to * p.st - p.pt;
+        yi0[b] = yo * p.sh - p.ph;
+        xi0[b] = xo * p.sw - p.pw;
     }
     const int hv = p.up2 ? 2 * p.h_in : p.h_in, wv = p.up2 ? 2 * p.w_in : p.w_in;
     const bf16_t* wb = (const bf16_t*)p.w + z * p.w_zs;
@@ -59,27 +66,30 @@ __global__ __launch_bounds__(CNTHR, 2) void vae_conv_kernel(vs_conv3d p, long lo
     const int nsteps = p.kt * p.kh * p.kw * csteps;
     int lc = 0, lkx = 0, lky = 0, lkt = 0;  // loader position (uniform)
 
-    u32x4_t ra0, ra1, rb[NBL];
-    auto load = [&]() {
-        const int ti = ti0 + lkt, yi = yi0 + lky, xi = xi0 + lkx;
-        const bool v = avalid && ti >= p.t_lo && ti < p.t_in && yi >= 0 && yi < hv && xi >= 0 && xi < wv;
-        if (v) {
-            const int ys = p.up2 ? (yi >> 1) : yi, xs = p.up2 ? (xi >> 1) : xi;
-            const bf16_t* src = xb + ((long long)(ti * p.h_in + ys) * p.w_in + xs) * p.ldx + lc;
-            ra0 = *(const u32x4_t*)src;
-            ra1 = *(const u32x4_t*)(src + 8);
-        } else {
-            ra0 = u32x4_t{0, 0, 0, 0};
-            ra1 = ra0;
+    struct Stage { u32x4_t a0[PXB], a1[PXB], b[NBL]; };
+    auto load = [&](Stage& r) {
+#pragma unroll
+        for (int b = 0; b < PXB; ++b) {
+            const int ti = ti0[b] + lkt, yi = yi0[b] + lky, xi = xi0[b] + lkx;
+            const bool v = avalid[b] && ti >= p.t_lo && ti < p.t_in && yi >= 0 && yi < hv && xi >= 0 && xi < wv;
+            if (v) {
+                const int ys = p.up2 ? (yi >> 1) : yi, xs = p.up2 ? (xi >> 1) : xi;
+                const bf16_t* src = xb[b] + ((long long)(ti * p.h_in + ys) * p.w_in + xs) * p.ldx + lc;
+                r.a0[b] = *(const u32x4_t*)src;
+                r.a1[b] = *(const u32x4_t*)(src + 8);
+            } else {
+                r.a0[b] = u32x4_t{0, 0, 0, 0};
+                r.a1[b] = r.a0[b];
+            }
         }
         const int kofs = ((lkt * p.kh + lky) * p.kw + lkx) * p.cin + lc;
 #pragma unroll
         for (int i = 0; i < NBL; ++i) {
             const int c = tid + CNTHR * i;
-            rb[i] = u32x4_t{0, 0, 0, 0};
+            r.b[i] = u32x4_t{0, 0, 0, 0};
             if (c < BN * 4) {
                 const int nr = n0 + (c >> 2);
-                if (nr < p.cout) rb[i] = *(const u32x4_t*)(wb + (long long)nr * p.ldw + kofs + (c & 3) * 8);
+                if (nr < p.cout) r.b[i] = *(const u32x4_t*)(wb + (long long)nr * p.ldw + kofs + (c & 3) * 8);
             }
         }
         // advance (c0, kx, ky, kt)
@@ -92,113 +102,181 @@ __global__ __launch_bounds__(CNTHR, 2) void vae_conv_kernel(vs_conv3d p, long lo
             }
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](const Stage& r, int buf) {
         char* A = lds + buf * STAGE;
-        char* B = A + BM * 64;
-        *(u32x4_t*)(A + swz(arow, ach)) = ra0;
-        *(u32x4_t*)(A + swz(arow, ach + 1)) = ra1;
+        char* B = A + BMT * 64;
+#pragma unroll
+        for (int b = 0; b < PXB; ++b) {
+            *(u32x4_t*)(A + swz(arow + BM * b, ach)) = r.a0[b];
+            *(u32x4_t*)(A + swz(arow + BM * b, ach + 1)) = r.a1[b];
+        }
 #pragma unroll
         for (int i = 0; i < NBL; ++i) {
             const int c = tid + CNTHR * i;
-            if (c < BN * 4) *(u32x4_t*)(B + swz(c >> 2, c & 3)) = rb[i];
+            if (c < BN * 4) *(u32x4_t*)(B + swz(c >> 2, c & 3)) = r.b[i];
         }
     };
 
-    f32x16_t acc[NB];
+    f32x16_t acc[PXB][NB];
 #pragma unroll
-    for (int j = 0; j < NB; ++j)
+    for (int b = 0; b < PXB; ++b)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[b][j][r] = 0.f;
 
+    // wave w computes pixel blocks w*32 + 128*b of the tile
     auto compute = [&](int buf) {
         const char* A = lds + buf * STAGE;
-        const char* B = A + BM * 64;
+        const char* B = A + BMT * 64;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int ch = 2 * s + (lane >> 5);
-            const bf16x8_t xa = *(const bf16x8_t*)(A + swz(wave * 32 + (lane & 31), ch));
+            bf16x8_t xa[PXB];
+#pragma unroll
+            for (int b = 0; b < PXB; ++b) xa[b] = *(const bf16x8_t*)(A + swz(BM * b + wave * 32 + (lane & 31), ch));
 #pragma unroll
             for (int j = 0; j < NB; ++j) {
                 const bf16x8_t wf = *(const bf16x8_t*)(B + swz(j * 32 + (lane & 31), ch));
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xa, acc[j], 0, 0, 0);
+#pragma unroll
+                for (int b = 0; b < PXB; ++b)
+                    acc[b][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xa[b], acc[b][j], 0, 0, 0);
             }
         }
     };
 
-    load();
-    store(0);
-    __syncthreads();
-    for (int s = 0; s < nsteps; ++s) {
-        const bool more = s + 1 < nsteps;
-        if (more) load();
-        compute(s & 1);
-        if (more) store((s + 1) & 1);
+    if constexpr (PRE == 1) {
+        Stage r;
+        load(r);
+        store(r, 0);
         __syncthreads();
+        for (int s = 0; s < nsteps; ++s) {
+            const bool more = s + 1 < nsteps;
+            if (more) load(r);
+            compute(s & 1);
+            if (more) store(r, (s + 1) & 1);
+            __syncthreads();
+        }
+    } else if constexpr (PRE == 2) {
+        // step s's data is in LDS buffer s&1, step s+1's in flight in stage (s+1)&1
+        Stage r0, r1;
+        load(r0);
+        if (nsteps > 1) load(r1);
+        store(r0, 0);
+        __syncthreads();
+        auto step = [&](int s, Stage& mine, Stage& next) __attribute__((always_inline)) {
+            if (s + 2 < nsteps) load(mine);        // mine (step s) is already in LDS
+            compute(s & 1);
+            if (s + 1 < nsteps) store(next, (s + 1) & 1);
+            __syncthreads();
+        };
+        for (int s = 0; s < nsteps; s += 2) {
+            step(s, r0, r1);
+            if (s + 1 < nsteps) step(s + 1, r1, r0);
+        }
+    } else {
+        // three stages: steps s+1 and s+2 in flight while step s computes
+        Stage r0, r1, r2;
+        load(r0);
+        if (nsteps > 1) load(r1);
+        if (nsteps > 2) load(r2);
+        store(r0, 0);
+        __syncthreads();
+        auto step = [&](int s, Stage& mine, Stage& next) __attribute__((always_inline)) {
+            if (s + 3 < nsteps) load(mine);
+            compute(s & 1);
+            if (s + 1 < nsteps) store(next, (s + 1) & 1);
+            __syncthreads();
+        };
+        for (int s = 0; s < nsteps; s += 3) {
+            step(s, r0, r1);
+            if (s + 1 < nsteps) step(s + 1, r1, r2);
+            if (s + 2 < nsteps) step(s + 2, r2, r0);
+        }
     }
 
     // ---- epilogue: lane owns pixel m, channels n0 + 32j + 8g + 4h + {0..3}
-    const long long me = m0 + wave * 32 + (lane & 31);
-    if (me >= M) return;
-    long long q = me;
-    const int xo = (int)(q % p.w_out); q /= p.w_out;
-    const int yo = (int)(q % p.h_out); q /= p.h_out;
-    const int to = (int)(q % p.t_out);
-    const long long nn = q / p.t_out;
     const int h = lane >> 5;
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
+    for (int b = 0; b < PXB; ++b) {
+        const long long me = m0 + BM * b + wave * 32 + (lane & 31);
+        if (me >= M) continue;
+        long long q = me;
+        const int xo = (int)(q % p.w_out); q /= p.w_out;
+        const int yo = (int)(q % p.h_out); q /= p.h_out;
+        const int to = (int)(q % p.t_out);
+        const long long nn = q / p.t_out;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int n = n0 + 32 * j + 8 * g + 4 * h;
-            if (n >= p.cout) continue;
-            int co = n, sub = 0;
-            if (p.split > 0 && n >= p.split) { co = n - p.split; sub = 1; }
-            const int tt = to * p.t_mul + p.t_add + sub;
-            const long long off = z * p.y_zs + nn * p.y_ns + ((long long)(tt * p.h_out + yo) * p.w_out + xo) * p.ldy + co;
-            const int nv = min(4, p.cout - n);
-            if constexpr (F32) {
-                float* y = (float*)p.y + off;
-                if (nv == 4) {
-                    *(f32x4_t*)y = f32x4_t{p.alpha * acc[j][4 * g], p.alpha * acc[j][4 * g + 1],
-                                           p.alpha * acc[j][4 * g + 2], p.alpha * acc[j][4 * g + 3]};
-                } else {
-                    for (int e = 0; e < nv; ++e) y[e] = p.alpha * acc[j][4 * g + e];
-                }
-            } else {
-                float v[4];
+        for (int j = 0; j < NB; ++j) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    float a = acc[j][4 * g + e];
-                    if (p.bias && e < nv) a += bf2f(((const bf16_t*)p.bias)[n + e]);
-                    v[e] = rbf(a);
-                }
-                bf16_t* y = (bf16_t*)p.y + off;
-                if (p.res) {
-                    const bf16_t* r = (const bf16_t*)p.res + off;
-                    for (int e = 0; e < nv; ++e) v[e] = rbf(v[e] + bf2f(r[e]));
-                }
-                if (nv == 4) {
-                    *(u32x2_t*)y = u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
+            for (int g = 0; g < 4; ++g) {
+                const int n = n0 + 32 * j + 8 * g + 4 * h;
+                if (n >= p.cout) continue;
+                int co = n, sub = 0;
+                if (p.split > 0 && n >= p.split) { co = n - p.split; sub = 1; }
+                const int tt = to * p.t_mul + p.t_add + sub;
+                const long long off = z * p.y_zs + nn * p.y_ns + ((long long)(tt * p.h_out + yo) * p.w_out + xo) * p.ldy + co;
+                const int nv = min(4, p.cout - n);
+                if constexpr (F32) {
+                    float* y = (float*)p.y + off;
+                    if (nv == 4) {
+                        *(f32x4_t*)y = f32x4_t{p.alpha * acc[b][j][4 * g], p.alpha * acc[b][j][4 * g + 1],
+                                               p.alpha * acc[b][j][4 * g + 2], p.alpha * acc[b][j][4 * g + 3]};
+                    } else {
+                        for (int e = 0; e < nv; ++e) y[e] = p.alpha * acc[b][j][4 * g + e];
+                    }
                 } else {
-                    for (int e = 0; e < nv; ++e) y[e] = (bf16_t)f2bf(v[e]);
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float a = acc[b][j][4 * g + e];
+                        if (p.bias && e < nv) a += bf2f(((const bf16_t*)p.bias)[n + e]);
+                        v[e] = rbf(a);
+                    }
+                    bf16_t* y = (bf16_t*)p.y + off;
+                    if (p.res) {
+                        const bf16_t* r = (const bf16_t*)p.res + off;
+                        for (int e = 0; e < nv; ++e) v[e] = rbf(v[e] + bf2f(r[e]));
+                    }
+                    if (nv == 4) {
+                        *(u32x2_t*)y = u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
+                    } else {
+                        for (int e = 0; e < nv; ++e) y[e] = (bf16_t)f2bf(v[e]);
+                    }
                 }
             }
         }
     }
 }
 
-template <int NB>
-int launch_conv(const vs_conv3d& p, long long M, hipStream_t st) {
+template <int NB, int PXB, int PRE>
+int launch_conv_px(const vs_conv3d& p, long long M, hipStream_t st) {
     const int ntn = (p.cout + 32 * NB - 1) / (32 * NB);
-    const long long mt = (M + BM - 1) / BM;
+    const long long mt = (M + BM * PXB - 1) / (BM * PXB);
     if (mt * ntn > 0x7fffffffLL) return VS_E_UNSUPPORTED;
     dim3 grid((unsigned)(mt * ntn), p.nz);
     if (p.out_f32)
-        hipLaunchKernelGGL((vae_conv_kernel<NB, true>), grid, dim3(CNTHR), 0, st, p, M, ntn);
+        hipLaunchKernelGGL((vae_conv_kernel<NB, true, PXB, PRE>), grid, dim3(CNTHR), 0, st, p, M, ntn);
     else
-        hipLaunchKernelGGL((vae_conv_kernel<NB, false>), grid, dim3(CNTHR), 0, st, p, M, ntn);
+        hipLaunchKernelGGL((vae_conv_kernel<NB, false, PXB, PRE>), grid, dim3(CNTHR), 0, st, p, M, ntn);
     VS_CHECK_LAUNCH();
     return VS_OK;
+}
+
+// VS_VAE_PXB=1|2 pixel blocks per wave, VS_VAE_PRE=1|2|3 register stages of the global->LDS
+// pipeline (the im2col gathers are latency-bound: with one stage 256-pixel tiles ran 0.68x of
+// 128-pixel ones).  Default 2 / 3, measured at 832x480x73 (profiles/r2/vae_conv_ab.log): tiled encode
+// 452 -> 498 TF/s, decode 467 -> 518 TF/s.  All variants are bit-identical (same K order per output).
+template <int NB>
+int launch_conv(const vs_conv3d& p, long long M, hipStream_t st) {
+    const char* e1 = getenv("VS_VAE_PXB");
+    const char* e2 = getenv("VS_VAE_PRE");
+    const bool px2 = !(e1 && e1[0] == '1');
+    const int pre = e2 ? e2[0] - '0' : 3;
+    if (px2) return pre == 3 ? launch_conv_px<NB, 2, 3>(p, M, st) : pre == 2 ? launch_conv_px<NB, 2, 2>(p, M, st)
+                                                                             : launch_conv_px<NB, 2, 1>(p, M, st);
+    return pre == 3 ? launch_conv_px<NB, 1, 3>(p, M, st) : pre == 2 ? launch_conv_px<NB, 1, 2>(p, M, st)
+                                                                   : launch_conv_px<NB, 1, 1>(p, M, st);
 }
 
 // ------------------------------------------------------------------------------------------
