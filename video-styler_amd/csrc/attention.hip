@@ -37,6 +37,10 @@ constexpr int LDS_BYTES = 2 * (KT + VT);   // K ring 2 x 17408 + V ring 2 x 2048
 constexpr int QPRE_BYTES = 9 * NTHR * 16;  // persistent mode: next item's Q / previous item's O, lane-private
 constexpr int PROW = HD + 4;     // split-tail partial row: 128 fp32 O, m, l, 2 pad (16-B aligned)
 constexpr int PERSIST_MIN_TILES = 8;
+// items of fewer key tiles prefetch Q / drain O inside the tile loop.  0: never -- measured on the
+// 14B shapes the synchronous item switch wins for long items (self-attention 31.0 -> 29.1 ms) and
+// ties or wins for the 8-tile cross-attention items too (0.935 -> 0.92 ms), profiles/r2/attn_pf_ab.log
+constexpr int PF_MAX_TILES = 0;
 #ifndef VS_ATTN_MFMA16_DEFAULT
 #define VS_ATTN_MFMA16_DEFAULT true
 #endif       // the Q prefetch spreads its 8 chunks over the first 8 tiles
@@ -142,8 +146,14 @@ struct AttnArgs {
     int Sq, Skv, H, nqb, nmain, npers, nsplit, piece_tiles;
 };
 
-template <bool REBASE, bool M16>
+template <bool REBASE, bool M16, bool PF>
 __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
+    // PF (VS_ATTN_PF=1; the r2 persistent kernel): the next item's Q is prefetched and the finished
+    // item's O drained inside the first 8 tiles of each item (kernel comment at `tile`).  !PF
+    // (default): that per-tile code -- range-gated loads/stores and their descriptor arithmetic in
+    // every tile -- is compiled out; an item switch stores O and loads the next Q directly (one
+    // stall per item) while the K/V pipeline still runs across the boundary: -6 % self-attention
+    // time on the 14B shape.
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS images: M32 pads the rows (K 272 B, V 320 B); M16 (v_mfma_f32_16x16x32_bf16, see mfma16
     // below) stores K rows unpadded with the 16-B chunk XOR-swizzled by (row & 15) and pads V rows
@@ -302,18 +312,19 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             return (long long)r * ldq + 16 * cidx + 8 * hh;
     };
     bf16x8_t qf[8];
-    {
-        const bf16_t* qb0 = q_base(bh_cur);
+    // the item's Q rows from global memory (rows past Sq read row Sq - 1; their outputs are dropped)
+    auto load_q = [&](const bf16_t* qb0, int q0v) __attribute__((always_inline)) {
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-            const int qrow = q0 + (M16 ? 16 * (s >> 2) + lr : r);
-            const long long off = qoff(s) + (qrow < Sq ? (long long)q0 * ldq
-                                                      : (long long)(Sq - 1 - (qrow - q0)) * ldq);
+            const int qrow = q0v + (M16 ? 16 * (s >> 2) + lr : r);
+            const long long off = qoff(s) + (qrow < Sq ? (long long)q0v * ldq
+                                                      : (long long)(Sq - 1 - (qrow - q0v)) * ldq);
             const bf16x8_t raw = *reinterpret_cast<const bf16x8_t*>(qb0 + off);
 #pragma unroll
             for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)((float)raw[j] * c);
         }
-    }
+    };
+    load_q(q_base(bh_cur), q0);
     store_k(0);
     if (Ttot > 1) {
         load_k(ki * BKV);
@@ -766,9 +777,9 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
 #ifdef VS_ATTN_DIAG_NOQPREF
         const bool qpref = false;         // timing diagnostic only: the next item reuses this Q
 #else
-        const bool qpref = tj + 1 < n_items && ti < PERSIST_MIN_TILES;
+        const bool qpref = PF && tj + 1 < n_items && ti < PERSIST_MIN_TILES;
 #endif
-        const bool odrain = tj > 0 && ti < PERSIST_MIN_TILES;
+        const bool odrain = PF && tj > 0 && ti < PERSIST_MIN_TILES;
 #ifdef VS_ATTN_STAMPS
         stamp_it = T;
 #endif
@@ -777,9 +788,11 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
         // reader finished before the barrier that opened this phase), then the next global loads
         if (T + 1 < Ttot) store_k((T + 1) & 1);      // K(T+1), loaded at the start of A_{T-1}
         load_v(kv0);
-        const bf16x8_t qraw = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
-            make_rsrc(qb_nxt + (long long)q0_nxt * ldq, qpref ? (unsigned)(max(Sq - q0_nxt, 0) * ldq * 2) : 0u),
-            (unsigned)(qoff(ti & 7) * 2), 0, 0));
+        bf16x8_t qraw{};
+        if constexpr (PF)
+            qraw = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
+                make_rsrc(qb_nxt + (long long)q0_nxt * ldq, qpref ? (unsigned)(max(Sq - q0_nxt, 0) * ldq * 2) : 0u),
+                (unsigned)(qoff(ti & 7) * 2), 0, 0));
         qk(T & 1, kv0);
         ATTN_STAMP(1);
         phase_bar();
@@ -795,9 +808,16 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
         }
         pv_softmax((T - 1) & 1, !first0);
         if (!first0 && ti == 0) {
-            out_chunks([&](int cidx, u32x4_t w) __attribute__((always_inline)) {
-                *reinterpret_cast<u32x4_t*>(qslot(cidx == 0 ? 8 : cidx)) = w;
-            });
+            if constexpr (PF) {
+                out_chunks([&](int cidx, u32x4_t w) __attribute__((always_inline)) {
+                    *reinterpret_cast<u32x4_t*>(qslot(cidx == 0 ? 8 : cidx)) = w;
+                });
+            } else {
+                bf16_t* op = ob_prev + (long long)q0_prev * ldo;
+                out_chunks([&](int cidx, u32x4_t w) __attribute__((always_inline)) {
+                    if (out_row_ok(q0_prev, cidx)) *reinterpret_cast<u32x4_t*>(op + ooff(cidx)) = w;
+                });
+            }
             // the new item starts from O = 0, l = 0
             lq[0] = 0.f;
             lq[1] = 0.f;
@@ -806,7 +826,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
         }
-        {
+        if constexpr (PF) {
             // chunk ti of the previous item's O (range 0 unless draining: the store is dropped)
             const u32x4_t w = *reinterpret_cast<const u32x4_t*>(qslot(ti == 0 ? 8 : (ti & 7)));
 #ifndef VS_ATTN_DIAG_NOSTORE
@@ -841,8 +861,12 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             // is already on it
             ti = 0;
 #ifndef VS_ATTN_DIAG_NOQPREF
+            if constexpr (PF) {
 #pragma unroll
-            for (int s2 = 0; s2 < 8; ++s2) qf[s2] = *reinterpret_cast<const bf16x8_t*>(qslot(s2));
+                for (int s2 = 0; s2 < 8; ++s2) qf[s2] = *reinterpret_cast<const bf16x8_t*>(qslot(s2));
+            } else {
+                load_q(qb_nxt, q0_nxt);
+            }
 #endif
 #pragma unroll
             for (int i = 0; i < 16; ++i) negm[i] = 0.f;
@@ -1009,8 +1033,10 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
     if (nwg > 0x7fffffff) return VS_E_INVALID;
     static bool attr_set = false;
     if (!attr_set) {
-        for (const void* f : {(const void*)attn_fwd_d128<false, false>, (const void*)attn_fwd_d128<true, false>,
-                              (const void*)attn_fwd_d128<false, true>, (const void*)attn_fwd_d128<true, true>})
+        for (const void* f : {(const void*)attn_fwd_d128<false, false, true>, (const void*)attn_fwd_d128<true, false, true>,
+                              (const void*)attn_fwd_d128<false, true, true>, (const void*)attn_fwd_d128<true, true, true>,
+                              (const void*)attn_fwd_d128<false, false, false>, (const void*)attn_fwd_d128<true, false, false>,
+                              (const void*)attn_fwd_d128<false, true, false>, (const void*)attn_fwd_d128<true, true, false>})
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
         attr_set = true;
     }
@@ -1039,8 +1065,10 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
         (!no_persist && span_ok && ncu > 0 && nkv >= PERSIST_MIN_TILES && sp.nmain > ncu) ? ncu : sp.nmain;
 #ifdef VS_ATTN_STAMPS
     const int lds = LDS_BYTES + STAMP_LDS;
-    for (const void* f : {(const void*)attn_fwd_d128<false, false>, (const void*)attn_fwd_d128<true, false>,
-                          (const void*)attn_fwd_d128<false, true>, (const void*)attn_fwd_d128<true, true>})
+    for (const void* f : {(const void*)attn_fwd_d128<false, false, true>, (const void*)attn_fwd_d128<true, false, true>,
+                          (const void*)attn_fwd_d128<false, true, true>, (const void*)attn_fwd_d128<true, true, true>,
+                          (const void*)attn_fwd_d128<false, false, false>, (const void*)attn_fwd_d128<true, false, false>,
+                          (const void*)attn_fwd_d128<false, true, false>, (const void*)attn_fwd_d128<true, true, false>})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 #else
     const int lds = LDS_BYTES;      // + the kernel's static QPRE_BYTES Q buffer
@@ -1049,8 +1077,13 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
     const AttnArgs args{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, bsq, bsk, bsv, bso,
                         ldq, ldk, ldv, ldo, part, c, sq, skv, heads, nqb, sp.nmain, npers, sp.nsplit,
                         sp.piece_tiles};
-    auto kern = m16 ? (rebase ? attn_fwd_d128<true, true> : attn_fwd_d128<false, true>)
-                    : (rebase ? attn_fwd_d128<true, false> : attn_fwd_d128<false, false>);
+    // in-loop Q prefetch / O drain only for short items (VS_ATTN_PF=0|1 overrides)
+    const char* pf_env = getenv("VS_ATTN_PF");
+    const bool pf = pf_env ? pf_env[0] == '1' : nkv < PF_MAX_TILES;
+    auto kern = pf ? (m16 ? (rebase ? attn_fwd_d128<true, true, true> : attn_fwd_d128<false, true, true>)
+                          : (rebase ? attn_fwd_d128<true, false, true> : attn_fwd_d128<false, false, true>))
+                   : (m16 ? (rebase ? attn_fwd_d128<true, true, false> : attn_fwd_d128<false, true, false>)
+                          : (rebase ? attn_fwd_d128<true, false, false> : attn_fwd_d128<false, false, false>));
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NTHR), lds, (hipStream_t)stream, args);
     VS_CHECK_LAUNCH();
     if (sp.ntail) {
