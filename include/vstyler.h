@@ -100,6 +100,10 @@ int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, const void*
  * Q: [batch][sq] rows of stride ldq (head h at columns h*128..), K/V: [batch][skv], O like Q.
  * Replaces flash_attention() / AttentionModule.forward (diffsynth/models/wan_video_dit.py:28-61,
  * 114-121) for self-attention (skv = sq) and T5 cross-attention (skv = 512).
+ * With a kind-4 workspace bound on the stream (and O not overlapping Q/K/V) the launch runs the
+ * optimistic softmax (no running max; row sums on MFMA) and recomputes, with the checked online
+ * softmax, every (batch, head, 256-query) item whose row sum left [2^-64, 2^64] (VS_ATTN_NC=0:
+ * checked kernel only).
  */
 int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
                 int batch, int sq, int skv, int heads, int head_dim,
@@ -116,8 +120,9 @@ int vs_attn_split_plan(int batch, int sq, int skv, int heads, int cus, int* out)
 
 /*
  * Library scratch (kind 0: vs_attn_fwd split tail, 1: vs_gemm split tail, 2: vs_gemm's hipBLASLt
- * workspace, 3: vs_gemm epilogue staging, M*N*2 bytes of the largest staged GEMM).
- * vs_split_workspace_bytes(kind) is the size that covers every plan of kinds 0-2 (-1 for kind 3);
+ * workspace, 3: vs_gemm epilogue staging, M*N*2 bytes of the largest staged GEMM, 4: vs_attn_fwd
+ * item flags, one int per item, ZERO-FILLED by the caller when bound -- every launch leaves it zero).
+ * vs_split_workspace_bytes(kind) is the size that covers every plan of kinds 0-2 and 4 (-1 for kind 3);
  * vs_split_workspace_bind(kind, ptr, bytes, stream) registers a caller-owned
  * device buffer (16-B aligned) for launches of that kind on `stream` of the current device
  * (ptr = NULL unbinds).  The buffer must stay valid while bound, including in captured graphs.

@@ -19,10 +19,14 @@ def rnd(*shape, scale=1.0, seed=0):
     return (scale * torch.randn(*shape, generator=g)).to(BF16)
 
 
-@pytest.fixture(params=["32", "16"])
+@pytest.fixture(params=["32", "16", "16c"])
 def attn_mfma(request, monkeypatch):
-    """Every attention test runs both MFMA shapes of attn_fwd_d128 (VS_ATTN_MFMA)."""
-    monkeypatch.setenv("VS_ATTN_MFMA", request.param)
+    """Every attention test runs both MFMA shapes of attn_fwd_d128 (VS_ATTN_MFMA); the 16x16x32 one
+    with the optimistic softmax + redo (the default, "16") and with the checked kernel only ("16c",
+    VS_ATTN_NC=0)."""
+    monkeypatch.setenv("VS_ATTN_MFMA", request.param[:2])
+    if request.param == "16c":
+        monkeypatch.setenv("VS_ATTN_NC", "0")
     return request.param
 
 
@@ -423,6 +427,56 @@ def test_attention_persistent_matches_one_item_per_block(attn_mfma, K, monkeypat
             ref = torch.softmax(qs @ ks.t() * 128 ** -0.5, -1) @ vs
             mx = (out[b * Sq + rows, h * 128:(h + 1) * 128].float() - ref).abs().max().item()
             assert mx < 3e-2, (b, h, mx)
+
+
+def _flags_zero(K):
+    """The kind-4 workspaces' count, done and per-item flags (ints [0, 2 + cap)) are zero."""
+    bufs = [b for (kind, _, _), b in K._SPLIT_WS.items() if kind == 4]
+    def head(b):
+        ints = b.view(torch.int32)
+        return ints[:2 + (ints.numel() - 2) // 2]
+    return bool(bufs) and all(int(head(b).count_nonzero()) == 0 for b in bufs)
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_attention_nc_redo(K, monkeypatch, split):
+    """Optimistic softmax (no running max, row sums on MFMA) + redo: items with a row whose sum
+    leaves [2^-64, 2^64] -- an overflow spike (score ~ +590 in the exp2 domain), a row whose every
+    score is ~ -190 (all p underflow) -- are recomputed by the checked kernel and match it bit for
+    bit; the other items stay within the bf16 tolerance of it; the item flags are all zero again
+    afterwards.  split: the spikes sit in split-tail items (flagged by the combine kernel)."""
+    monkeypatch.setenv("VS_ATTN_MFMA", "16")
+    B, Sq, Skv, H = 1, 23040, 4000, 3          # 256 whole items + a 14-item split tail on 256 CUs
+    g = torch.Generator(device="cuda").manual_seed(75)
+    q = torch.randn(Sq, H * 128, device="cuda", generator=g).to(BF16)
+    k = torch.randn(Skv, H * 128, device="cuda", generator=g).to(BF16)
+    v = torch.randn(Skv, H * 128, device="cuda", generator=g).to(BF16)
+    u = torch.ones(128, device="cuda", dtype=BF16)
+    # (head, query row): spike rows against key 1234 of that head, low rows against every key
+    spikes = [(2, 20000), (2, 22000)] if split else [(0, 300), (1, 5000)]
+    lows = [(2, 21000)] if split else [(0, 9000)]
+    for h, r in lows:           # keys of that head ~ N(1, 1): the row's scores ~ -20 * 128 / sqrt(128)
+        k[:, h * 128:(h + 1) * 128] += 1.0
+        q[r, h * 128:(h + 1) * 128] = -20.0 * u
+    for h, r in spikes:
+        q[r, h * 128:(h + 1) * 128] = 6.0 * u
+        k[1234, h * 128:(h + 1) * 128] = 6.0 * u
+    out = torch.empty_like(q)
+    K.attention(q, k, v, out, H, B)
+    torch.cuda.synchronize()
+    assert _flags_zero(K)
+    monkeypatch.setenv("VS_ATTN_NC", "0")
+    monkeypatch.setenv("VS_ATTN_NO_SPLIT", "1")       # the redo runs every item unsplit
+    chk = torch.empty_like(q)
+    K.attention(q, k, v, chk, H, B)
+    torch.cuda.synchronize()
+    flagged = torch.zeros(Sq, H, dtype=torch.bool, device="cuda")
+    for h, r in spikes + lows:
+        flagged[r // 256 * 256:(r // 256 + 1) * 256, h] = True
+    o3, c3 = out.view(Sq, H, 128), chk.view(Sq, H, 128)
+    assert torch.equal(o3[flagged], c3[flagged])
+    assert (o3[~flagged].float() - c3[~flagged].float()).abs().max().item() < 2e-2
+    assert torch.isfinite(out.float()).all()
 
 
 def test_attention_strided_views(attn_mfma, K):

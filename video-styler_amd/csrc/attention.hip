@@ -22,6 +22,8 @@
 //    inside the phase that completes it -- no per-item prologue or drain (worth most on the
 //    cross-attention, whose 512 keys are only 8 tiles per item).
 #include "common.h"
+#include <algorithm>
+#include <set>
 
 namespace {
 
@@ -80,6 +82,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
 // shuffle and a two-deep S ring: ~850).  Epilogue: permlane32_swap pairs -> 16-B stores (T21).
 constexpr float SUM_THR = 256.0f;
 constexpr float SUM_MIN = 0x1p-60f;
+// ---------------------------------------------------------------------------------------------
+// Optimistic softmax (NC, r2, M16 only; the default when the caller bound an item-flag workspace):
+// no reference max at all -- p = exp2(c*qk) -- and no per-tile check, the row sums l on the matrix
+// pipe as the O^T rows of a ones block of V^T (4 extra MFMAs per tile instead of 32 fp32 adds and
+// the tile's check per lane: -24 % of the loop's VALU issue, +3.5...6 % self-attention throughput,
+// profiles/r2/attn_nc_ab.log).  Exact while no p overflows or underflows; an item whose final row
+// sum leaves [NC_LMIN, NC_LMAX] (a row max above 64 or below -64 in the exp2 domain) is flagged
+// and recomputed by the checked kernel (the redo launch), so the result is either the optimistic
+// one -- which sums the P actually multiplied with V -- or bit for bit the checked one.  With
+// l <= 2^64 the fp32 O accumulators stay finite for |v| < 2^64.
+constexpr float NC_LMIN = 0x1p-64f;
+constexpr float NC_LMAX = 0x1p64f;
 
 // v_mfma_f32_32x32x16_bf16.  VS_ATTN_DIAG_MFMA16 (timing diagnostic only, wrong results): the same
 // FLOPs as two v_mfma_f32_16x16x32_bf16 on the same operands, to measure the clock / issue effect
@@ -142,11 +156,23 @@ struct AttnArgs {
     long long bsq, bsk, bsv, bso;
     long long ldq, ldk, ldv, ldo;
     float* part;
+    int* flags;      // item-flag workspace (layout at NcWs): written by the NC kernel / the combine,
+                     // consumed and cleared by the redo launch
     float c;
     int Sq, Skv, H, nqb, nmain, npers, nsplit, piece_tiles;
+    int nc_cap;      // items the flag workspace holds (its list and its flags)
 };
 
-template <bool REBASE, bool M16, bool PF>
+// Item-flag workspace (kind 4, ints; count, done and flags zero between launches): [0] count of
+// listed items, [1] redo blocks done reading the count, [2, 2 + cap) one flag per item,
+// [2 + cap, 2 + 2 cap) the list of flagged items (an item is listed once: the first flagger's
+// atomicExch sees 0).  cap follows from the bound size, so the regions never move.
+__device__ __forceinline__ void nc_list_item(int* ws, int cap, int gi) {
+    if (atomicExch(ws + 2 + gi, 1) == 0) ws[2 + cap + atomicAdd(ws, 1)] = gi;
+}
+constexpr int MODE_CHK = 0, MODE_NC = 1, MODE_REDO = 2;
+
+template <bool REBASE, bool M16, bool PF, int MODE>
 __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
     // PF (VS_ATTN_PF=1; the r2 persistent kernel): the next item's Q is prefetched and the finished
     // item's O drained inside the first 8 tiles of each item (kernel comment at `tile`).  !PF
@@ -155,6 +181,9 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
     // stall per item) while the K/V pipeline still runs across the boundary: -6 % self-attention
     // time on the 14B shape.
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    // NC: optimistic softmax (comment at NC_LMIN); M16 only
+    // REDO: the checked kernel over the items the NC launch listed (grid-strided over the list)
+    constexpr bool NC = M16 && MODE == MODE_NC, REDO = MODE == MODE_REDO;
     // LDS images: M32 pads the rows (K 272 B, V 320 B); M16 (v_mfma_f32_16x16x32_bf16, see mfma16
     // below) stores K rows unpadded with the 16-B chunk XOR-swizzled by (row & 15) and pads V rows
     // to 288 B, so both of its read patterns are bank-conflict free
@@ -172,7 +201,26 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
 
     int piece = -1, kv_begin = 0, Skv = Skv_all;
     int g0, gstride, n_items;
-    if ((int)blockIdx.x < npers) {
+    const int* rlist = nullptr;
+    if constexpr (REDO) {
+        // block b takes list entries b, b + grid, ...; the last block to have read the count
+        // resets count and done, every block clears the flags of its items
+        int* const ws = args.flags;
+        const int cnt = *reinterpret_cast<volatile int*>(ws);
+        const int R = gridDim.x;
+        g0 = blockIdx.x;
+        gstride = R;
+        n_items = cnt > g0 ? (cnt - g0 + R - 1) / R : 0;
+        rlist = ws + 2 + args.nc_cap;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int j = 0; j < n_items; ++j) ws[2 + rlist[g0 + j * R]] = 0;
+            if (atomicAdd(ws + 1, 1) == R - 1) {
+                ws[0] = 0;
+                ws[1] = 0;
+            }
+        }
+    } else if ((int)blockIdx.x < npers) {
         const int x = blockIdx.x & 7, lb = blockIdx.x >> 3;
         const int qx = nmain >> 3, rx = nmain & 7, qbk = npers >> 3, rbk = npers & 7;
         const int cs = x < rx ? x * (qx + 1) : rx * (qx + 1) + (x - rx) * qx;
@@ -198,7 +246,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
     // column block, and the item's first query row (the wave's rows start 32 * wave further)
     auto item_bh = [&](int j, int& qrow0) {
         const int nqb = cold->nqb;
-        const int g = g0 + j * gstride;
+        const int g = REDO ? rlist[g0 + j * gstride] : g0 + j * gstride;
         const int qb = g % nqb, bh = g / nqb;
         qrow0 = qb * BQ;
         return bh;
@@ -354,6 +402,12 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
     // p = exp2(S).  m starts at 0; the exact path (on the first tile only when its sums leave
     // [SUM_MIN, SUM_THR]) moves it to a row max.  lq: the lane's partial row sums.
     float mq[2] = {0.f, 0.f}, lq[2] = {0.f, 0.f};
+    // NC: the row sums of the bf16 P as O^T rows of a ones block of V^T (4 extra MFMAs per tile);
+    // lane (lr, lg) holds row 16qb + lr's sum in every element of lsum[qb]
+    f32x4_t lsum[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    bf16x8_t ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
     f32x16_t negm;
 #pragma unroll
     for (int i = 0; i < 16; ++i) negm[i] = 0.f;
@@ -385,7 +439,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
         const bf16x2_t w0 = {(__bf16)p0, (__bf16)p1}, w1 = {(__bf16)p2, (__bf16)p3};
         if constexpr (M16) {
             const int grp = ss & 3, kbl = grp >> 1, qb = grp & 1;
-            (qb ? rs1 : rs0) += (p0 + p1) + (p2 + p3);
+            if constexpr (!NC) (qb ? rs1 : rs0) += (p0 + p1) + (p2 + p3);
             pk[2 * qb + t][2 * kbl] = __builtin_bit_cast(unsigned, w0);
             pk[2 * qb + t][2 * kbl + 1] = __builtin_bit_cast(unsigned, w1);
         } else {
@@ -456,7 +510,12 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
                 const int g = 2 * kbl + qb;
                 s[t] = mfma16g(kf[j], qf[4 * qb + ks], s[t], g, grp4(ks == 0 ? negm : s[t], g));
             }
-            if (t == 1) {
+            if (t == 1 && NC) {
+                const int e = 2 * (j - 8);
+                s[0][e] = __builtin_amdgcn_exp2f(s[0][e]);
+                s[0][e + 1] = __builtin_amdgcn_exp2f(s[0][e + 1]);
+                asm volatile("" : "+v"(s[0][e]), "+v"(s[0][e + 1]));
+            } else if (t == 1) {
                 const int e = 2 * (j - 8);
                 s[0][e] = __builtin_amdgcn_exp2f(s[0][e]);
                 s[0][e + 1] = __builtin_amdgcn_exp2f(s[0][e + 1]);
@@ -535,6 +594,14 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
                     o[ot] = mfma16g(vf[dt], __builtin_bit_cast(bf16x8_t, pk[2 * qb + cc]), o[ot], g, grp4(o[ot], g));
                 }
             }
+            if constexpr (NC) {
+                if ((ks & 1) == 0) {
+#pragma unroll
+                    for (int qb = 0; qb < 2; ++qb)
+                        lsum[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            ones, __builtin_bit_cast(bf16x8_t, pk[2 * qb + cc]), lsum[qb], 0, 0, 0);
+                }
+            }
         } else {
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
@@ -570,7 +637,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
                 if (st >= 2) {          // chunk 1's operands are free: the s[1] half, 2 groups a step
                     p_chunk(4 + 2 * (st - 2));
                     p_chunk(5 + 2 * (st - 2));
-                    asm volatile("" : "+v"(rs0), "+v"(rs1));
+                    if constexpr (!NC) asm volatile("" : "+v"(rs0), "+v"(rs1));
                     asm volatile("" :: "v"(pk[1]), "v"(pk[3]));
                 }
                 if (st == 3) {          // chunk 0's operands are free once the last MFMAs issue
@@ -711,7 +778,17 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
     //   M16: lane (lr, lg) holds columns 16db + 4lg .. +3 of rows 16qb + lr; column blocks
     //        (2dt, 2dt+1) through one permlane16_swap per dword give chunk c = 2dt + qb = columns
     //        16(2dt + (lg&1)) + 8(lg>>1) .. +7 of row 16qb + lr.
+    // NC: flag item gi for the redo launch when one of the wave's row sums left [NC_LMIN, NC_LMAX]
+    // (NaN included); every wave of the item may store the same 1
+    auto nc_flag = [&](int gi) __attribute__((always_inline)) {
+        if constexpr (NC) {
+            const float l0 = lsum[0][0], l1 = lsum[1][0];
+            const bool ok = l0 >= NC_LMIN && l0 <= NC_LMAX && l1 >= NC_LMIN && l1 <= NC_LMAX;
+            if (__any(!ok) && lane == 0) nc_list_item(cold->flags, cold->nc_cap, gi);
+        }
+    };
     auto row_l = [&](int qb) {
+        if constexpr (NC) return lsum[qb][0];
         float t = lq[qb];
         if constexpr (M16) t += __shfl_xor(t, 16);
         return t + __shfl_xor(t, 32);
@@ -808,6 +885,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
         }
         pv_softmax((T - 1) & 1, !first0);
         if (!first0 && ti == 0) {
+            nc_flag(g0 + (tj - 1) * gstride);      // the finished item's row sums
             if constexpr (PF) {
                 out_chunks([&](int cidx, u32x4_t w) __attribute__((always_inline)) {
                     *reinterpret_cast<u32x4_t*>(qslot(cidx == 0 ? 8 : cidx)) = w;
@@ -821,6 +899,8 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             // the new item starts from O = 0, l = 0
             lq[0] = 0.f;
             lq[1] = 0.f;
+            lsum[0] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            lsum[1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -844,7 +924,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             for (int j = 0; j < 8; ++j) qs[j] = (__bf16)((float)qraw[j] * c);
             *reinterpret_cast<bf16x8_t*>(qslot(ti)) = qs;
         }
-        {
+        if constexpr (!NC) {
             const float rt0 = row_tot(0), rt1 = M16 ? row_tot(1) : rt0;
             const bool low = first && !(fminf(rt0, rt1) >= SUM_MIN);
 #ifdef VS_ATTN_DIAG_MFMA16
@@ -853,8 +933,10 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             if (__any(fmaxf(rt0, rt1) > SUM_THR || low)) exact_split(first, kv0, low);
 #endif
         }
-        lq[0] += row_tot(0);
-        if constexpr (M16) lq[1] += row_tot(1);
+        if constexpr (!NC) {
+            lq[0] += row_tot(0);
+            if constexpr (M16) lq[1] += row_tot(1);
+        }
         if (++ti == nkv && ++tj < n_items) {
             // switch to the next item: its prescaled Q from the LDS slots, m = 0 (as in a fresh
             // block); the V loader and the exact-path recompute follow the QK item, the K loader
@@ -936,6 +1018,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
         return;
     }
     {
+        nc_flag(g0 + (n_items - 1) * gstride);     // (tj ran past the last item)
         bf16_t* op = ob_cur + (long long)q0 * ldo;
         out_chunks([&](int cidx, u32x4_t w) __attribute__((always_inline)) {
             if (out_row_ok(q0, cidx)) *reinterpret_cast<u32x4_t*>(op + ooff(cidx)) = w;
@@ -947,7 +1030,8 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
 // against their own reference max m_j (exp2 domain): O = sum_j 2^(m_j - M) O_j / sum_j 2^(m_j - M) l_j.
 __global__ __launch_bounds__(256) void attn_combine(const float* __restrict__ part, bf16_t* __restrict__ O,
                                                     int ntail, int nmain, int nsplit, int Sq, int H, int nqb,
-                                                    long long ldo, long long bso) {
+                                                    long long ldo, long long bso, int* __restrict__ flags,
+                                                    int nc_cap) {
     const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
     const int c4 = (int)(idx & 31);
     const long long rowid = idx >> 5;              // item * BQ + row
@@ -968,6 +1052,8 @@ __global__ __launch_bounds__(256) void attn_combine(const float* __restrict__ pa
         lsum += w * pj[HD + 1];
         acc += w * *reinterpret_cast<const f32x4_t*>(pj + 4 * c4);
     }
+    // NC pieces (all m_j = 0): a row sum outside [NC_LMIN, NC_LMAX] sends the item to the redo launch
+    if (flags && !(lsum >= NC_LMIN && lsum <= NC_LMAX)) nc_list_item(flags, nc_cap, g);
     const float inv = 1.f / lsum;
     bf16_t* op = O + (long long)b * bso + (long long)q * ldo + h * HD + 4 * c4;
     const unsigned lo = pack2(acc[0] * inv, acc[1] * inv), hi = pack2(acc[2] * inv, acc[3] * inv);
@@ -1031,15 +1117,6 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
     const int nqb = (sq + BQ - 1) / BQ;
     const long long nwg = (long long)nqb * heads * batch;
     if (nwg > 0x7fffffff) return VS_E_INVALID;
-    static bool attr_set = false;
-    if (!attr_set) {
-        for (const void* f : {(const void*)attn_fwd_d128<false, false, true>, (const void*)attn_fwd_d128<true, false, true>,
-                              (const void*)attn_fwd_d128<false, true, true>, (const void*)attn_fwd_d128<true, true, true>,
-                              (const void*)attn_fwd_d128<false, false, false>, (const void*)attn_fwd_d128<true, false, false>,
-                              (const void*)attn_fwd_d128<false, true, false>, (const void*)attn_fwd_d128<true, true, false>})
-            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        attr_set = true;
-    }
     // MFMA shape of the QK / PV products (VS_ATTN_MFMA=16|32)
     const char* shape_env = getenv("VS_ATTN_MFMA");
     const bool m16 = shape_env ? shape_env[0] == '1' : VS_ATTN_MFMA16_DEFAULT;
@@ -1063,34 +1140,83 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
     const bool span_ok = (long long)sq * ldq * 2 < (1LL << 32) && (long long)sq * ldo * 2 < (1LL << 32);
     const int npers =
         (!no_persist && span_ok && ncu > 0 && nkv >= PERSIST_MIN_TILES && sp.nmain > ncu) ? ncu : sp.nmain;
+    // optimistic softmax (NC, comment at NC_LMIN): M16 only, needs the caller's item-flag workspace
+    // (kind 4, zero-filled) and an O that does not overlap Q / K / V (the redo launch re-reads
+    // them); VS_ATTN_NC=0 keeps the checked kernel
+    const char* nc_env = getenv("VS_ATTN_NC");
+    int* flags = nullptr;
+    int nc_cap = 0;
+    if (m16 && !(nc_env && nc_env[0] == '0')) {
+        auto span = [&](const void* p, long long bs, long long ld, int rows) {
+            const char* b = (const char*)p;
+            return std::make_pair(b, b + 2 * ((long long)(batch - 1) * bs + (long long)(rows - 1) * ld + heads * HD));
+        };
+        const auto so = span(o, bso, ldo, sq);
+        bool overlap = false;
+        for (const auto& s : {span(q, bsq, ldq, sq), span(k, bsk, ldk, skv), span(v, bsv, ldv, skv)})
+            overlap = overlap || (so.first < s.second && s.first < so.second);
+        int dev = 0;
+        long long bytes = 0;
+        int* ws = (!overlap && hipGetDevice(&dev) == hipSuccess)
+                      ? (int*)vs_bound_workspace(4, dev, (hipStream_t)stream, &bytes) : nullptr;
+        const long long cap = bytes / 4 > 2 ? (bytes / 4 - 2) / 2 : 0;
+        if (ws && cap >= nwg) {
+            flags = ws;
+            nc_cap = (int)std::min(cap, (long long)0x7fffffff);
+        }
+    }
 #ifdef VS_ATTN_STAMPS
     const int lds = LDS_BYTES + STAMP_LDS;
-    for (const void* f : {(const void*)attn_fwd_d128<false, false, true>, (const void*)attn_fwd_d128<true, false, true>,
-                          (const void*)attn_fwd_d128<false, true, true>, (const void*)attn_fwd_d128<true, true, true>,
-                          (const void*)attn_fwd_d128<false, false, false>, (const void*)attn_fwd_d128<true, false, false>,
-                          (const void*)attn_fwd_d128<false, true, false>, (const void*)attn_fwd_d128<true, true, false>})
-        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 #else
     const int lds = LDS_BYTES;      // + the kernel's static QPRE_BYTES Q buffer
 #endif
     const long long grid = (long long)npers + (long long)sp.ntail * sp.nsplit;
-    const AttnArgs args{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, bsq, bsk, bsv, bso,
-                        ldq, ldk, ldv, ldo, part, c, sq, skv, heads, nqb, sp.nmain, npers, sp.nsplit,
-                        sp.piece_tiles};
+    AttnArgs args{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, bsq, bsk, bsv, bso,
+                  ldq, ldk, ldv, ldo, part, flags, c, sq, skv, heads, nqb, sp.nmain, npers, sp.nsplit,
+                  sp.piece_tiles, nc_cap};
     // in-loop Q prefetch / O drain only for short items (VS_ATTN_PF=0|1 overrides)
     const char* pf_env = getenv("VS_ATTN_PF");
     const bool pf = pf_env ? pf_env[0] == '1' : nkv < PF_MAX_TILES;
-    auto kern = pf ? (m16 ? (rebase ? attn_fwd_d128<true, true, true> : attn_fwd_d128<false, true, true>)
-                          : (rebase ? attn_fwd_d128<true, false, true> : attn_fwd_d128<false, false, true>))
-                   : (m16 ? (rebase ? attn_fwd_d128<true, true, false> : attn_fwd_d128<false, true, false>)
-                          : (rebase ? attn_fwd_d128<true, false, false> : attn_fwd_d128<false, false, false>));
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NTHR), lds, (hipStream_t)stream, args);
-    VS_CHECK_LAUNCH();
+    auto pick = [&](int mode, bool pfv) -> void (*)(AttnArgs) {
+        constexpr int C = MODE_CHK, N = MODE_NC, R = MODE_REDO;
+        if (mode == R)
+            return rebase ? attn_fwd_d128<true, true, false, R> : attn_fwd_d128<false, true, false, R>;
+        if (mode == N)
+            return pfv ? (rebase ? attn_fwd_d128<true, true, true, N> : attn_fwd_d128<false, true, true, N>)
+                       : (rebase ? attn_fwd_d128<true, true, false, N> : attn_fwd_d128<false, true, false, N>);
+        return pfv ? (m16 ? (rebase ? attn_fwd_d128<true, true, true, C> : attn_fwd_d128<false, true, true, C>)
+                          : (rebase ? attn_fwd_d128<true, false, true, C> : attn_fwd_d128<false, false, true, C>))
+                   : (m16 ? (rebase ? attn_fwd_d128<true, true, false, C> : attn_fwd_d128<false, true, false, C>)
+                          : (rebase ? attn_fwd_d128<true, false, false, C> : attn_fwd_d128<false, false, false, C>));
+    };
+    auto launch = [&](void (*kern)(AttnArgs), long long nblk, const AttnArgs& a) {
+        static std::mutex mu;
+        static std::set<const void*> attr_done;
+        {
+            std::lock_guard<std::mutex> lock(mu);
+            if (attr_done.insert((const void*)kern).second)
+                (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        }
+        hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(NTHR), lds, (hipStream_t)stream, a);
+        return hipGetLastError() == hipSuccess;
+    };
+    if (!launch(pick(flags ? MODE_NC : MODE_CHK, pf), grid, args)) return VS_E_LAUNCH;
     if (sp.ntail) {
         const long long threads = (long long)sp.ntail * BQ * 32;
         hipLaunchKernelGGL(attn_combine, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                           part, (bf16_t*)o, sp.ntail, sp.nmain, sp.nsplit, sq, heads, nqb, ldo, bso);
+                           part, (bf16_t*)o, sp.ntail, sp.nmain, sp.nsplit, sq, heads, nqb, ldo, bso, flags, nc_cap);
         VS_CHECK_LAUNCH();
+    }
+    if (flags) {
+        // redo: the checked kernel over the listed items, one block per CU walking the list (with
+        // none listed every block returns at once); leaves the workspace's count and flags zero
+        AttnArgs r = args;
+        r.part = nullptr;
+        r.nsplit = 1;
+        r.piece_tiles = 0;
+        const long long rgrid = std::min<long long>(nwg, ncu > 0 ? ncu : 256);
+        r.nmain = r.npers = (int)rgrid;
+        if (!launch(pick(MODE_REDO, false), rgrid, r)) return VS_E_LAUNCH;
     }
     return VS_OK;
 }
@@ -1110,11 +1236,12 @@ extern "C" long long vs_split_workspace_bytes(int kind) {
     if (kind == 0) return (long long)MAX_PIECES * BQ * PROW * (long long)sizeof(float);
     if (kind == 1) return vs_gemm_split_workspace_bytes_impl();
     if (kind == 2) return 128LL << 20;          // hipBLASLt (stream-K partials)
+    if (kind == 4) return 1LL << 20;            // attention item flags (int per item; zero-filled)
     return -1;                                  // kind 3: m * n * 2 bytes of the largest routed GEMM
 }
 
 extern "C" int vs_split_workspace_bind(int kind, void* ptr, long long bytes, void* stream) {
-    if (kind < 0 || kind > 3 || bytes < 0 || (ptr && ((uintptr_t)ptr & 15))) return VS_E_INVALID;
+    if (kind < 0 || kind > 4 || bytes < 0 || (ptr && ((uintptr_t)ptr & 15))) return VS_E_INVALID;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return VS_E_LAUNCH;
     std::mutex* mu;

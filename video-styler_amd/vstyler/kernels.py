@@ -23,7 +23,7 @@ _SPLIT_WS = {}
 
 def _split_ws(kind, t, nbytes=None):
     """Bind library scratch of `kind` (0 attention split tail, 1 GEMM split tail, 2 hipBLASLt
-    workspace, 3 epilogue staging of `nbytes`) for the current stream of t's device from the torch
+    workspace, 3 epilogue staging of `nbytes`, 4 attention item flags) for the current stream of t's device from the torch
     allocator (vs_split_workspace_bind: the library never allocates).  Re-bound larger when a
     bigger one is needed; never inside a graph capture (the library then takes its fallback)."""
     stream = _stream(t)
@@ -37,7 +37,8 @@ def _split_ws(kind, t, nbytes=None):
         return
     if torch.cuda.is_current_stream_capturing():
         return
-    buf = torch.empty(nbytes, dtype=torch.uint8, device=t.device)
+    # kind 4 (attention item flags) must be zero when bound; the library keeps it zero
+    buf = (torch.zeros if kind == 4 else torch.empty)(nbytes, dtype=torch.uint8, device=t.device)
     _lib.check(_lib.load().vs_split_workspace_bind(kind, buf.data_ptr(), nbytes, stream))
     _SPLIT_WS[key] = buf
 
@@ -167,6 +168,7 @@ def attention(q, k, v, out, num_heads, batch, scale=None):
     if scale is None:
         scale = hd ** -0.5
     _split_ws(0, q)
+    _split_ws(4, q)
     _lib.check(_lib.load().vs_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), batch, sq,
                                        skv, num_heads, hd, ldq, ldk, ldv, ldo, sq * ldq, skv * ldk,
                                        skv * ldv, sq * ldo, float(scale), _stream(q)))
