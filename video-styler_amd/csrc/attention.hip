@@ -514,7 +514,9 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
                 const int e = 2 * (j - 8);
                 s[0][e] = __builtin_amdgcn_exp2f(s[0][e]);
                 s[0][e + 1] = __builtin_amdgcn_exp2f(s[0][e + 1]);
+#ifndef VS_ATTN_NC_NOTIE
                 asm volatile("" : "+v"(s[0][e]), "+v"(s[0][e + 1]));
+#endif
             } else if (t == 1) {
                 const int e = 2 * (j - 8);
                 s[0][e] = __builtin_amdgcn_exp2f(s[0][e]);
@@ -595,7 +597,11 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
                 }
             }
             if constexpr (NC) {
+#ifndef VS_ATTN_ONES_ODD
                 if ((ks & 1) == 0) {
+#else
+                if ((ks & 1) == 1) {
+#endif
 #pragma unroll
                     for (int qb = 0; qb < 2; ++qb)
                         lsum[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
