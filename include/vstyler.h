@@ -131,6 +131,13 @@ long long vs_split_workspace_bytes(int kind);
 int vs_split_workspace_bind(int kind, void* ptr, long long bytes, void* stream);
 
 /*
+ * The hipBLASLt build vs_gemm's library route runs on: the path of the copy opened by the library
+ * (default $ROCM_PATH/lib/libhipblaslt.so.1, VS_LT_LIB overrides), or "linked" when that failed and
+ * the link-time binding (in a torch process: torch's bundled hipBLASLt) is used.
+ */
+const char* vs_blaslt_library(void);
+
+/*
  * out = bf16(LN(x)) [affine: weight/bias] then, if shift/scale given, modulate:
  * bf16(bf16(n * bf16(1+scale)) + shift) with shift/scale rows selected per batch.
  * Replaces WanAutoCastLayerNorm (layers.py:63-92) + modulate (wan_video_dit.py:64-65,225,228,268).

@@ -156,7 +156,10 @@ def test_gemm_route_rule(monkeypatch):
     assert lib.vs_gemm_route(59280, 5120, 13824) == 1       # 4640 tiles
     assert lib.vs_gemm_route(7410, 5120, 5120) == 1         # 580 tiles, K 5120
     assert lib.vs_gemm_route(3705, 5120, 5120) == 1         # 300 tiles
-    assert lib.vs_gemm_route(7410, 5120, 13824) == 0        # 580 tiles, K 13824
+    # 580 tiles, K 13824: hipBLASLt only on the private ROCm-7.2 copy (gemm.hip lt_route, r2)
+    private = lib.vs_blaslt_library().decode() != "linked"
+    assert lib.vs_gemm_route(7410, 5120, 13824) == (1 if private else 0)
+    assert lib.vs_gemm_route(3705, 5120, 13824) == (1 if private else 0)
     assert lib.vs_gemm_route(1024, 10240, 5120) == 1        # 160 tiles: cross k|v over the context
     assert lib.vs_gemm_route(2, 30720, 5120) == 1           # time projection
     assert lib.vs_gemm_route(512, 4096, 10240) == 0         # 32 tiles, K 10240 (UMT5 FFN-down)

@@ -969,12 +969,17 @@ KSplit plan_ksplit(int ntiles, int nh, int cus) {
 // embedding), the time projection (M = 2) and the UMT5 layers -- also go to hipBLASLt: 1.05-2.4x
 // the 128^2 kernel (profiles/r1/gemm_backend_ab_ctx_r1s.log); the narrow head (N = 64) and the
 // patch embeddings (K = 64 / 384) are unmeasured there and stay on the MFMA kernels.
+// r2: on the private ROCm-7.2 hipBLASLt copy (blaslt.hip) the K = 13824 FFN-down at 3705 rows runs
+// at 0.404-0.411 ms against 0.466-0.474 on the MFMA kernel (profiles/r2/lt_lib_ab_r2l.log), so with
+// that library the 256-1023-tile grids go to hipBLASLt at any K.
+bool vs_lt_is_private();
 static bool lt_route(int m, int n, int k) {
     const char* e = getenv("VS_GEMM_BACKEND");
     const int mode = !e ? 2 : (e[0] == 'v' ? 0 : (e[0] == 'l' ? 1 : 2));   // 0 never, 1 always, 2 auto
     if (mode != 2) return mode == 1;
     const long long tiles = (long long)((m + 255) / 256) * ((n + 255) / 256);
-    return tiles >= 1024 || (k <= 8192 && (tiles >= 256 || (n >= 2048 && k >= 1024)));
+    return tiles >= 1024 || (tiles >= 256 && (k <= 8192 || vs_lt_is_private())) ||
+           (k <= 8192 && n >= 2048 && k >= 1024);
 }
 
 // hipBLASLt for bf16(A W^T [* scale] + bias) (gemm(y, ldy)), then the rest of the epilogue with

@@ -62,6 +62,7 @@ SIGNATURES = {
     "vs_gemm_split_plan": [_I, _I, _I, _I, _P],
     "vs_gemm_route": [_I, _I, _I],
     "vs_split_workspace_bytes": [_I],
+    "vs_blaslt_library": [],
     "vs_split_workspace_bind": [_I, _P, _LL, _P],
     "vs_layernorm_modulate": [_P, _LL, _P, _LL, _I, _I, _I, _P, _P, _LL, _P, _P, _F, _P],
     "vs_residual_layernorm": [_P, _LL, _P, _LL, _P, _LL, _I, _I, _I, ctypes.POINTER(VsEpilogue), _I, _P, _P, _LL,
@@ -99,7 +100,7 @@ SIGNATURES = {
     "vs_sp_comm_destroy": [_P],
     "vs_sp_last_error": [],
 }
-_RESTYPES = {"vs_strerror": ctypes.c_char_p, "vs_split_workspace_bytes": ctypes.c_longlong,
+_RESTYPES = {"vs_strerror": ctypes.c_char_p, "vs_blaslt_library": ctypes.c_char_p, "vs_split_workspace_bytes": ctypes.c_longlong,
              "vs_sp_last_error": ctypes.c_char_p}
 
 _lib = None
