@@ -51,7 +51,8 @@ struct LtPlan {
     int pick = 0;                                       // index of the algorithm in use in cand
     int m = 0, n = 0, k = 0;                            // the problem (swept candidates, signature)
     long long ldc = 0;
-    bool fp8 = false;
+    bool fp8 = false, bias = false, gelu = false;
+    bool path_linked = false;                           // planned on the link-time library
     std::vector<hipblasLtMatmulHeuristicResult_t> cand;
 };
 
@@ -184,17 +185,36 @@ hipblasLtHandle_t handle_for(int dev) {
 // Solutions the heuristic's first 16 do not hold but an exhaustive sweep (tests/probes/lt_sweep.cpp
 // over all 2081 bf16 TN solutions that support the problem, profiles/r2/lt_sweep.log) found
 // fastest on the 14B block shapes: 4-7.5 % over the heuristic's best at 59280 rows, 8-19 % at the
-// 3705-row Ulysses SP = 8 shapes.  Library solution indices (valid for the hipBLASLt build of this
-// image; an index that does not resolve or does not support the problem is skipped), appended to
-// the autotune's candidates of large bf16 GEMMs.  VS_LT_SWEPT=0 keeps the heuristic list alone.
-constexpr int kSweptAlgos[] = {438309, 438310, 438346, 438347, 438515, 438529, 438583, 438789, 438921,
-                               439045, 439048, 439079, 439093, 439112, 439200, 439212, 439265, 439274,
-                               439282, 439302, 439303, 439305, 439313, 439321, 439324, 439326, 439352,
-                               439363, 439383, 439391, 439398, 439399, 439402, 439421, 440236};
+// 3705-row Ulysses SP = 8 shapes.  Library solution indices of the ROCm-7.2 build (an index that
+// does not resolve or does not support the problem is skipped), appended to the autotune's
+// candidates.  ONLY for the swept problems -- the four 14B block GEMMs with their bias / GELU_BIAS
+// epilogue at 3705-59280 rows, where all 2081 solutions ran without a fault at 3705, 7410, 29640 and
+// 59280 rows, and the 1.3B q|k|v and o GEMMs at 59280 rows (profiles/r2/lt_sweep.log,
+// lt_sweep2.log): a solution the library reports as supporting a
+// problem can still fault on it (one did on the 1.3B FFN-up, N 8960 K 1536 with GELU_BIAS), and an
+// output check cannot catch a memory fault.  VS_LT_SWEPT=0 keeps the heuristic list alone.
+constexpr int kSweptAlgos[] = {438309, 438310, 438346, 438347, 438386, 438515, 438529, 438583, 438789,
+                               438921, 438983, 439036, 439044, 439045, 439048, 439059, 439079, 439093,
+                               439110, 439112, 439200, 439212, 439228, 439260, 439265, 439266, 439269,
+                               439274, 439282, 439285, 439287, 439301, 439302, 439303, 439304, 439305,
+                               439306, 439313, 439316, 439321, 439323, 439324, 439325, 439326, 439352,
+                               439357, 439361, 439363, 439383, 439391, 439398, 439399, 439402, 439421,
+                               440058, 440230, 440236};
+struct SweptShape {
+    int n, k;
+    bool gelu;
+    int m_lo, m_hi;       // the row counts the sweep covered without a fault
+};
+constexpr SweptShape kSweptShapes[] = {{15360, 5120, false, 3705, 59280}, {5120, 5120, false, 3705, 59280},
+                                       {13824, 5120, true, 3705, 59280},  {5120, 13824, false, 3705, 59280},
+                                       {4608, 1536, false, 59280, 59280}, {1536, 1536, false, 59280, 59280}};
 
-// (called by the autotune, once the call's bias pointer is bound to the descriptor)
 void add_swept_candidates(LtPlan& p, hipblasLtHandle_t h, size_t ws_bytes) {
-    if (p.fp8 || (double)p.m * p.n * p.k < 1.6e10) return;
+    if (p.fp8 || !p.bias || p.path_linked) return;
+    bool swept = false;
+    for (const SweptShape& s : kSweptShapes)
+        swept |= s.n == p.n && s.k == p.k && s.gelu == p.gelu && p.m >= s.m_lo && p.m <= s.m_hi;
+    if (!swept) return;
     if (const char* e = std::getenv("VS_LT_SWEPT"); e && e[0] == '0') return;
     std::vector<int> idx(std::begin(kSweptAlgos), std::end(kSweptAlgos));
     std::vector<hipblasLtMatmulHeuristicResult_t> ex;
@@ -232,6 +252,9 @@ LtPlan* plan_for(const LtKey& key, size_t ws_bytes) {
     p.k = key.k;
     p.ldc = key.ldc;
     p.fp8 = key.fp8;
+    p.bias = key.bias;
+    p.gelu = key.gelu;
+    p.path_linked = lt().path == "linked";
     hipblasLtHandle_t h = handle_for(key.dev);
     if (!h) return nullptr;
     if (lt().MatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return nullptr;
