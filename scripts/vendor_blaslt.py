@@ -60,9 +60,10 @@ def patch(src, dst):
     return n
 
 
-def main():
-    out = sys.argv[1]
-    lib = sys.argv[2] if len(sys.argv) > 2 else os.path.join(os.environ.get("ROCM_PATH") or "/opt/rocm", "lib")
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    out = argv[0]
+    lib = argv[1] if len(argv) > 1 else os.path.join(os.environ.get("ROCM_PATH") or "/opt/rocm", "lib")
     os.makedirs(out, exist_ok=True)
     for src, dst in FILES.items():
         s, d = os.path.join(lib, src), os.path.join(out, dst)
