@@ -303,6 +303,9 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             kst[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, kvo0, 0, 0);
             kst[1] = __builtin_amdgcn_raw_buffer_load_b128(rs, kvo1, 0, 0);
         } else {
+#ifdef VS_ATTN_DIAG_HOTKV
+            kv0 &= BKV;      // timing diagnostic only (wrong results): every tile reads tile 0 or 1 (L2-hot)
+#endif
             const int ks = kv0 * ldk32 * 2;
             kst[0] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo0, ks, 0);
             kst[1] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo1, ks, 0);
@@ -314,6 +317,9 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             vst[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, vvo0, 0, 0);
             vst[1] = __builtin_amdgcn_raw_buffer_load_b128(rs, vvo1, 0, 0);
         } else {
+#ifdef VS_ATTN_DIAG_HOTKV
+            kv0 &= BKV;
+#endif
             const int vs = kv0 * ldv32 * 2;
             vst[0] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo0, vs, 0);
             vst[1] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo1, vs, 0);
