@@ -188,8 +188,8 @@ hipblasLtHandle_t handle_for(int dev) {
 // 3705-row Ulysses SP = 8 shapes.  Library solution indices of the ROCm-7.2 build (an index that
 // does not resolve or does not support the problem is skipped), appended to the autotune's
 // candidates.  ONLY for the swept problems -- the four 14B block GEMMs with their bias / GELU_BIAS
-// epilogue at 3705-59280 rows, where all 2081 solutions ran without a fault at 3705, 7410, 29640 and
-// 59280 rows (profiles/r2/lt_sweep.log, lt_sweep2.log): a solution the library reports as supporting a
+// epilogue at 3705, 7410, 29640 and 59280 rows, where all 2081 solutions ran without a fault
+// (profiles/r2/lt_sweep.log, lt_sweep2.log): a solution the library reports as supporting a
 // problem can still fault on it (one did on the 1.3B FFN-up, N 8960 K 1536 with GELU_BIAS), and an
 // output check cannot catch a memory fault.  VS_LT_SWEPT=0 keeps the heuristic list alone.
 constexpr int kSweptAlgos[] = {438309, 438310, 438346, 438347, 438386, 438515, 438529, 438583, 438789,
@@ -202,19 +202,21 @@ constexpr int kSweptAlgos[] = {438309, 438310, 438346, 438347, 438386, 438515, 4
 struct SweptShape {
     int n, k;
     bool gelu;
-    int m_lo, m_hi;       // the row counts the sweep covered without a fault
 };
 // (the 1.3B q|k|v and o problems were swept fault-free too, but with their swept picks the C2 step
-// measured 1 % slower than without them -- the faster GEMMs cost the following attention launches
-// clock, profiles/r2/lt_lib_workloads_ab_r2m.log vs _r2n.log -- so they keep the heuristic list)
-constexpr SweptShape kSweptShapes[] = {{15360, 5120, false, 3705, 59280}, {5120, 5120, false, 3705, 59280},
-                                       {13824, 5120, true, 3705, 59280}, {5120, 13824, false, 3705, 59280}};
+// measured 1 % slower -- the faster GEMMs cost the following attention launches clock,
+// profiles/r2/lt_lib_workloads_ab_r2m.log vs _r2n.log -- so they keep the heuristic list)
+constexpr SweptShape kSweptShapes[] = {{15360, 5120, false}, {5120, 5120, false}, {13824, 5120, true},
+                                       {5120, 13824, false}};
+// the row counts the sweeps covered (every solution ran without a fault): SP = 1 (2 x 29640), CFG
+// parallel (29640), Ulysses SP = 4 / 8 per CFG sample (7410 / 3705)
+constexpr int kSweptRows[] = {3705, 7410, 29640, 59280};
 
 void add_swept_candidates(LtPlan& p, hipblasLtHandle_t h, size_t ws_bytes) {
     if (p.fp8 || !p.bias || p.path_linked) return;
     bool swept = false;
-    for (const SweptShape& s : kSweptShapes)
-        swept |= s.n == p.n && s.k == p.k && s.gelu == p.gelu && p.m >= s.m_lo && p.m <= s.m_hi;
+    for (const SweptShape& s : kSweptShapes) swept |= s.n == p.n && s.k == p.k && s.gelu == p.gelu;
+    swept &= std::find(std::begin(kSweptRows), std::end(kSweptRows), p.m) != std::end(kSweptRows);
     if (!swept) return;
     if (const char* e = std::getenv("VS_LT_SWEPT"); e && e[0] == '0') return;
     std::vector<int> idx(std::begin(kSweptAlgos), std::end(kSweptAlgos));
