@@ -4,7 +4,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 PROBE=${PROBE:-attn_bench.py}
-for i in 1 2; do
+for i in $(seq 1 ${REPS:-2}); do
   echo "== base"; timeout -k 10 300 python tests/probes/$PROBE || exit 1
   for d in build/var_*/; do
     [ -f $d/libvstyler.so ] || continue
