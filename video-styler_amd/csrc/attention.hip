@@ -130,6 +130,19 @@ __device__ __forceinline__ f32x16_t mfma16g(bf16x8_t a, bf16x8_t b, f32x16_t c, 
     return c;
 }
 
+// scheduling fences inside the QK / PV step sequences (VS_ATTN_SB_FREE_QK / _PV: A/B builds that let
+// the machine scheduler move instructions across k-steps)
+#ifdef VS_ATTN_SB_FREE_QK
+#define ATTN_SB_QK() do {} while (0)
+#else
+#define ATTN_SB_QK() __builtin_amdgcn_sched_barrier(0)
+#endif
+#ifdef VS_ATTN_SB_FREE_PV
+#define ATTN_SB_PV() do {} while (0)
+#else
+#define ATTN_SB_PV() __builtin_amdgcn_sched_barrier(0)
+#endif
+
 #ifdef VS_ATTN_STAMPS
 // debug build: s_memtime at the 4 phase boundaries of tiles 2..33 for wave 0 (group 0) and wave 4
 // (group 1) of workgroup 0, kept in an LDS tail during the loop (no loop-carried registers) and
@@ -509,7 +522,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
         for (int j = 0; j < 16; ++j) {
             if (j + DEP < 16) kf[j + DEP] = *reinterpret_cast<const bf16x8_t*>(kaddr(j + DEP));
             if (j == 8 && last) mask_half(0, kv0);
-            __builtin_amdgcn_sched_barrier(0);
+            ATTN_SB_QK();
             const int t = j >> 3, ks = (j >> 1) & 3, kbl = j & 1;
 #pragma unroll
             for (int qb = 0; qb < 2; ++qb) {
@@ -642,7 +655,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             bf16x8_t* nxt = (st & 1) ? va : vb;
             if (with_pv) {
                 if (st + 1 < 4) read_vt(base, order[st + 1], nxt);
-                __builtin_amdgcn_sched_barrier(0);
+                ATTN_SB_PV();
                 pv_step(ks, cur);
             }
             if constexpr (M16) {
@@ -671,7 +684,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
                 // branch and keeps the fp32 p values live through the PV phase
                 asm volatile("" :: "v"(pk[ks]));
             }
-            __builtin_amdgcn_sched_barrier(0);
+            ATTN_SB_PV();
             if (with_pv) ATTN_STAMP(3 + st);
         }
     };
