@@ -110,7 +110,7 @@ def pmc_traffic(path=os.path.join(os.path.dirname(os.path.abspath(__file__)), "p
         txt = open(path).read()
         rd = float(re.search(r"HBM read\s+~\s+([0-9.]+) GB/dispatch", txt).group(1))
         wr = float(re.search(r"HBM write\s+~\s+([0-9.]+) GB/dispatch", txt).group(1))
-        return (rd + wr) * 1e9
+        return int(round((rd + wr) * 1e9))
     except (OSError, AttributeError):
         return None
 
