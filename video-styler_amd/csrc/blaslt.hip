@@ -188,17 +188,17 @@ hipblasLtHandle_t handle_for(int dev) {
 // 3705-row Ulysses SP = 8 shapes.  Library solution indices of the ROCm-7.2 build (an index that
 // does not resolve or does not support the problem is skipped), appended to the autotune's
 // candidates.  ONLY for the swept problems -- the four 14B block GEMMs with their bias / GELU_BIAS
-// epilogue at 3705, 7410, 29640 and 59280 rows, where all 2081 solutions ran without a fault
-// (profiles/r2/lt_sweep.log, lt_sweep2.log): a solution the library reports as supporting a
+// epilogue at 3705, 7410, 14820, 29640 and 59280 rows, where all 2081 solutions ran without a fault
+// (profiles/r2/lt_sweep.log, lt_sweep2.log, lt_sweep3.log): a solution the library reports as supporting a
 // problem can still fault on it (one did on the 1.3B FFN-up, N 8960 K 1536 with GELU_BIAS), and an
 // output check cannot catch a memory fault.  VS_LT_SWEPT=0 keeps the heuristic list alone.
 constexpr int kSweptAlgos[] = {438309, 438310, 438346, 438347, 438386, 438515, 438529, 438583, 438789,
                                438921, 438983, 439036, 439044, 439045, 439048, 439059, 439079, 439093,
-                               439110, 439112, 439200, 439212, 439228, 439260, 439265, 439266, 439269,
-                               439274, 439282, 439285, 439287, 439301, 439302, 439303, 439304, 439305,
-                               439306, 439313, 439316, 439321, 439323, 439324, 439325, 439326, 439352,
-                               439357, 439361, 439363, 439383, 439391, 439398, 439399, 439402, 439421,
-                               440058, 440230, 440236};
+                               439110, 439112, 439200, 439212, 439217, 439228, 439229, 439260, 439265,
+                               439266, 439269, 439274, 439282, 439285, 439287, 439296, 439297, 439301,
+                               439302, 439303, 439304, 439305, 439306, 439313, 439316, 439321, 439323,
+                               439324, 439325, 439326, 439352, 439357, 439361, 439363, 439383, 439391,
+                               439397, 439398, 439399, 439402, 439421, 440058, 440230, 440236};
 struct SweptShape {
     int n, k;
     bool gelu;
@@ -209,8 +209,9 @@ struct SweptShape {
 constexpr SweptShape kSweptShapes[] = {{15360, 5120, false}, {5120, 5120, false}, {13824, 5120, true},
                                        {5120, 13824, false}};
 // the row counts the sweeps covered (every solution ran without a fault): SP = 1 (2 x 29640), CFG
-// parallel (29640), Ulysses SP = 4 / 8 per CFG sample (7410 / 3705)
-constexpr int kSweptRows[] = {3705, 7410, 29640, 59280};
+// parallel (29640), Ulysses SP = 4 / 8 per CFG sample (7410 / 3705) and their two-sample merged
+// phases (14820 / 7410; profiles/r2/lt_sweep3.log)
+constexpr int kSweptRows[] = {3705, 7410, 14820, 29640, 59280};
 
 void add_swept_candidates(LtPlan& p, hipblasLtHandle_t h, size_t ws_bytes) {
     if (p.fp8 || !p.bias || p.path_linked) return;
