@@ -5,8 +5,8 @@ One step = the reference's CFG denoising step (wan_video_new.py:518-542): DiT(40
 and the Euler update.  Synthetic data: random-init weights (N(0,0.02), seed 5), seeded latents /
 contexts / VACE context of the real shapes (no checkpoints or datasets are reachable offline).
 
-  python bench.py [--gpus N --steps K --warmup W]        (N>1: torchrun over RCCL; N=2 CFG-parallel,
-                                                         N=4/8 Ulysses SP; VSTYLER_CFG_PARALLEL overrides)
+  python bench.py [--gpus N --steps K --warmup W]        (N>1: torchrun over RCCL, Ulysses SP over all
+                                                         N ranks; VSTYLER_CFG_PARALLEL=1 selects CFG parallel)
 
 Prints one JSON line with `roofline` (self-attention kernel, HIP-event timed inside the timed
 region) and, on rank 0 at N=1, `cpu_baseline` (the CPU oracle on a bounded token sample).
@@ -40,12 +40,25 @@ def step_flops(m, S, L=512, B=2):
     return B * fwd
 
 
-def cpu_baseline(m, S, rows=1024, repeats=2):
-    """Oracle (PyTorch-CPU restatement) on a bounded sample: one DiT block's per-token work for
-    `rows` query tokens (their projections, norms, RoPE, attention against the full S-token K/V,
-    cross-attention, FFN), extrapolated x S/rows x (main+VACE blocks) x 2 (CFG)."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(m, S, rows=2048):
+    """Oracle (PyTorch-CPU restatement, oracle/wan_oracle.py) on a bounded sample of the step: one
+    main DiT block and one VACE block (DiT block + after_proj, wan_video_vace.py:13-24) for `rows`
+    query tokens each -- their projections, norms, RoPE, attention against the full S-token K/V,
+    cross-attention, FFN -- extrapolated as (N_main t_main + N_vace t_vace) x S/rows x 2 (CFG).
+    Threads: OMP_NUM_THREADS when set (the GPU box's CPU share), else the CPUs this process may run
+    on (os.sched_getaffinity); the CPU model and os.cpu_count() are reported beside it."""
     from oracle import wan_oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     torch.set_num_threads(threads)
     D, F, H = m["dim"], m["ffn_dim"], m["num_heads"]
     g = torch.Generator().manual_seed(0)
@@ -61,14 +74,16 @@ def cpu_baseline(m, S, rows=1024, repeats=2):
     Wb["norm3.weight"], Wb["norm3.bias"] = 1 + w(D), w(D)
     Wb["ffn.0.weight"], Wb["ffn.0.bias"], Wb["ffn.2.weight"], Wb["ffn.2.bias"] = w(F, D), w(F), w(D, F), w(D)
     Wb["modulation"] = w(1, 6, D)
-    x = torch.randn(1, rows, D, generator=g).to(bf)
+    Wb["after_proj.weight"], Wb["after_proj.bias"] = w(D, D), w(D)
     kfull = torch.randn(1, S, D, generator=g).to(bf)
     vfull = torch.randn(1, S, D, generator=g).to(bf)
     ctx = torch.randn(1, 512, D, generator=g).to(bf)
     t_mod = w(1, 6, D)
-    freqs = O.rope_freqs(1, 1, rows)
 
-    def one():
+    def block(n, vace):
+        x = torch.randn(1, n, D, generator=g).to(bf)
+        freqs = O.rope_freqs(1, 1, n)
+        t0 = time.perf_counter()
         mod = O.bf(Wb["modulation"].float() + t_mod.float())
         sh, sc, ga, sh2, sc2, ga2 = mod.chunk(6, dim=1)
         h = O.modulate(O.layer_norm(x), sh, sc)
@@ -77,28 +92,29 @@ def cpu_baseline(m, S, rows=1024, repeats=2):
         k = O.rope_apply(O.rms_norm(O.linear(h, Wb["self_attn.k.weight"], Wb["self_attn.k.bias"]),
                                     Wb["self_attn.norm_k.weight"]), freqs, H)
         v = O.linear(h, Wb["self_attn.v.weight"], Wb["self_attn.v.bias"])
-        kk = torch.cat([k, kfull[:, rows:]], 1)
-        vv = torch.cat([v, vfull[:, rows:]], 1)
+        kk = torch.cat([k, kfull[:, n:]], 1)
+        vv = torch.cat([v, vfull[:, n:]], 1)
         o = O.attention(q, kk, vv, H)
         y = O.gate_residual(x, ga, O.linear(o, Wb["self_attn.o.weight"], Wb["self_attn.o.bias"]))
         y = O.add(y, O.cross_attention(O.layer_norm(y, 1e-6, Wb["norm3.weight"], Wb["norm3.bias"]), ctx, Wb,
                                        "cross_attn.", H))
         f = O.linear(O.gelu_tanh(O.linear(O.modulate(O.layer_norm(y), sh2, sc2), Wb["ffn.0.weight"],
                                           Wb["ffn.0.bias"])), Wb["ffn.2.weight"], Wb["ffn.2.bias"])
-        return O.gate_residual(y, ga2, f)
+        y = O.gate_residual(y, ga2, f)
+        if vace:
+            O.linear(y, Wb["after_proj.weight"], Wb["after_proj.bias"])
+        return time.perf_counter() - t0
 
-    one()
-    best = float("inf")
-    for _ in range(repeats):
-        t0 = time.perf_counter()
-        one()
-        best = min(best, time.perf_counter() - t0)
-    blocks = m["num_layers"] + len(m["vace_layers"])
-    sec_per_step = best * (S / rows) * blocks * 2
+    block(rows, True)                   # warm-up at full size (allocator, thread pool, caches)
+    t_main = block(rows, False)
+    t_vace = block(rows, True)
+    nm, nv = m["num_layers"], len(m["vace_layers"])
+    sec_per_step = (nm * t_main + nv * t_vace) * (S / rows) * 2
     return {"value": 1.0 / sec_per_step, "unit": "steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle DiT block, {rows} of {S} query tokens vs full {S}-token K/V, best of {repeats} "
-                      f"({best:.2f}s), extrapolated x{S}/{rows} tokens x{blocks} blocks x2 CFG "
-                      f"= {sec_per_step:.0f} s/step"}
+            "cpu": _cpu_model(), "os_cpu_count": os.cpu_count(),
+            "sample": f"oracle main DiT block ({t_main:.2f} s) and VACE block ({t_vace:.2f} s), each on {rows} of "
+                      f"{S} query tokens ({100.0 * rows / S:.1f} %) against the full {S}-token K/V, extrapolated "
+                      f"({nm} x main + {nv} x VACE) x {S}/{rows} tokens x 2 CFG = {sec_per_step:.0f} s/step"}
 
 
 def pmc_traffic(path=os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2", "pmc_attn_ilp",
@@ -179,7 +195,7 @@ def main():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--width", type=int, default=832)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=1024)
+    ap.add_argument("--cpu-rows", type=int, default=2048)
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
     ap.add_argument("--progress", action="store_true", help="sync + stderr line after every timed step")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end sec/video components")
@@ -265,14 +281,16 @@ def main():
                                    use_unified_sequence_parallel=sp is not None, sp_group=sp)
             K.cfg_euler_dev(v[0:1], v[1:2], latents, 5.0, d_buf)
 
-        # the product's step runner: step 0 eager, then one hipGraph capture replayed per step (single
-        # GPU; Ulysses SP steps run eagerly).  Capture happens inside the warmup.
-        use_graph = world == 1 and not args.no_graph and args.warmup >= 1
+        # the product's step runner: step 0 eager, then one hipGraph capture replayed per step (under
+        # Ulysses SP with the RCCL collectives inside the graph).  Capture happens inside the warmup.
+        from vstyler.pipeline import sp_graph_ok
+        use_graph = not args.no_graph and args.warmup >= 1 and (world == 1 or sp_graph_ok(sp))
         stepper = DenoiseStepper(step_fn, ts, ds, use_graph=use_graph)
         for i in range(args.warmup):
             stepper(i)
             torch.cuda.synchronize()
             print(f"[bench] warmup step {i} done", file=sys.stderr, flush=True)
+        use_graph = use_graph and stepper.graph is not None     # a failed capture falls back to eager
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

@@ -235,7 +235,8 @@ int vs_ulysses_permute_rows(const void* src, void* dst, int batch, int s_local, 
 typedef struct vs_sp_comm vs_sp_comm;
 /* rank 0 creates the id and hands it to every rank out of band (the torch store, MPI, a file) */
 int vs_sp_unique_id(void* out_id);
-/* collective over all `world` ranks; binds the communicator to HIP device `device` */
+/* collective over all `world` ranks; binds the communicator to HIP device `device` (the calling
+ * thread's current device is restored before returning) */
 int vs_sp_init(int rank, int world, const void* unique_id, int device, vs_sp_comm** out);
 /* recv chunk j <- chunk `rank` of rank j's send (grouped send/recv, all_to_all_single semantics) */
 int vs_sp_all_to_all(vs_sp_comm* comm, const void* send, void* recv, long long bytes_per_rank, void* stream);

@@ -83,7 +83,8 @@ def sinusoidal_embedding_1d(dim, position):
     """wan_video_dit.py:68-72: fp64 [cos || sin] of t*10000^(-i/(dim/2)), cast to position dtype."""
     half = dim // 2
     sinusoid = torch.outer(position.to(torch.float64),
-                           torch.pow(10000, -torch.arange(half, dtype=torch.float64).div(half)))
+                           torch.pow(10000, -torch.arange(half, dtype=torch.float64,
+                                                          device=position.device).div(half)))
     x = torch.cat([torch.cos(sinusoid), torch.sin(sinusoid)], dim=1)
     return x.to(position.dtype)
 
@@ -115,7 +116,7 @@ def rope_apply(x, freqs, num_heads):
     """wan_video_dit.py:92-97: interleaved pairs as complex128, multiply, cast back to bf16."""
     b, s, dm = x.shape
     xc = torch.view_as_complex(x.to(torch.float64).reshape(b, s, num_heads, -1, 2))
-    out = torch.view_as_real(xc * freqs).flatten(2)
+    out = torch.view_as_real(xc * freqs.to(x.device)).flatten(2)
     return out.to(x.dtype)
 
 
@@ -161,7 +162,14 @@ def linear(x, w, b=None):
 FP8_BLOCK_LINEARS = False
 
 
+# Hot-loaded (un-merged) LoRA terms of AutoWrappedLinear (layers.py:180-182): {id(weight): (alpha*A, B)};
+# a block linear whose weight is listed runs lora_linear.
+HOTLOAD = {}
+
+
 def blk_linear(x, w, b=None):
+    if id(w) in HOTLOAD:
+        return lora_linear(x, w, b, *HOTLOAD[id(w)])
     return fp8_linear(x, w, b) if FP8_BLOCK_LINEARS else linear(x, w, b)
 
 
@@ -173,6 +181,12 @@ def silu(x):
     return bf(F.silu(x.float()))
 
 
+# attention() evaluates the score matrix per (batch, head) and in query-row chunks once it would
+# exceed this many elements (production shapes on the GPU: S = 29 640 -> 281 GB at once); the
+# per-row arithmetic is the same softmax(q k^T / sqrt(d)) v in ACC_DTYPE either way.
+ATTN_CHUNK_ELEMS = 1 << 28
+
+
 def attention(q, k, v, num_heads):
     """wan_video_dit.py:28-61: softmax(q k^T / sqrt(d)) v, non-causal, no mask; fp32 math."""
     b, sq, dm = q.shape
@@ -180,8 +194,19 @@ def attention(q, k, v, num_heads):
     qh = q.to(ACC_DTYPE).view(b, sq, num_heads, d).transpose(1, 2)
     kh = k.to(ACC_DTYPE).view(b, k.shape[1], num_heads, d).transpose(1, 2)
     vh = v.to(ACC_DTYPE).view(b, v.shape[1], num_heads, d).transpose(1, 2)
-    p = torch.softmax((qh @ kh.transpose(-1, -2)) / math.sqrt(d), dim=-1)
-    o = p @ vh
+    skv = k.shape[1]
+    if b * num_heads * sq * skv <= ATTN_CHUNK_ELEMS:
+        p = torch.softmax((qh @ kh.transpose(-1, -2)) / math.sqrt(d), dim=-1)
+        o = p @ vh
+    else:
+        o = torch.empty(b, num_heads, sq, d, dtype=ACC_DTYPE, device=q.device)
+        rows = max(1, ATTN_CHUNK_ELEMS // skv)
+        for i in range(b):
+            for h in range(num_heads):
+                kt = kh[i, h].transpose(0, 1)
+                for r0 in range(0, sq, rows):
+                    p = torch.softmax((qh[i, h, r0:r0 + rows] @ kt) / math.sqrt(d), dim=-1)
+                    o[i, h, r0:r0 + rows] = p @ vh[i, h]
     return bf(o.transpose(1, 2).reshape(b, sq, dm))
 
 

@@ -1,0 +1,49 @@
+"""A/B: the 8-phase hand-written GEMM (VS_GEMM_IMPL default) vs the r2 ping-pong kernel (pp) vs the
+hipBLASLt route (lt), per 14B block GEMM with its real epilogue; interleaved rounds, one process.
+usage: gemm8p_ab.py [M ...]"""
+import os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "video-styler_amd"))
+import torch
+from vstyler import kernels as K
+
+
+def timed(fn, reps=3):
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(); fn(); e1.record(); torch.cuda.synchronize(); ts.append(e0.elapsed_time(e1))
+    return min(ts)
+
+
+SHAPES = (("qkv", 15360, 5120, K.VS_EPI_BIAS), ("o-proj", 5120, 5120, K.VS_EPI_GATE_RES),
+          ("ffn-up", 13824, 5120, K.VS_EPI_GELU), ("ffn-down", 5120, 13824, K.VS_EPI_GATE_RES))
+VARIANTS = [v for v in os.environ.get("AB_VARIANTS", "8p,pp,lt").split(",")]
+for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
+    for name, N, Kd, epi in SHAPES:
+        g = torch.Generator(device="cuda").manual_seed(1)
+        a = torch.randn(M, Kd, device="cuda", generator=g).to(torch.bfloat16)
+        w = (0.05 * torch.randn(N, Kd, device="cuda", generator=g)).to(torch.bfloat16)
+        b = (0.1 * torch.randn(N, device="cuda", generator=g)).to(torch.bfloat16)
+        gate = (0.1 * torch.randn(2, N, device="cuda", generator=g)).to(torch.bfloat16)
+        x = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+        kw = dict(epilogue=epi, bias=b)
+        if epi == K.VS_EPI_GATE_RES:
+            kw.update(residual=x, gate=gate, gate_bstride=N, rows_per_batch=(M + 1) // 2)
+        out = x if epi == K.VS_EPI_GATE_RES else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+
+        def setv(v):
+            os.environ["VS_GEMM_BACKEND"] = "lt" if v == "lt" else "vstyler"
+            os.environ["VS_GEMM_IMPL"] = v
+            os.environ["VSTYLER_GEMM_TILE"] = "256"
+        t = {v: [] for v in VARIANTS}
+        for v in VARIANTS:             # warm (hipBLASLt autotune happens here)
+            setv(v); K.gemm(a, w, out, **kw); torch.cuda.synchronize()
+        for r in range(4):
+            for v in VARIANTS:
+                setv(v); t[v].append(timed(lambda: K.gemm(a, w, out, **kw)))
+        fl = 2.0 * M * N * Kd
+        s = "  ".join(f"{v} {min(t[v]):.3f} ms ({fl / min(t[v]) / 1e9:.0f} TF/s)" for v in VARIANTS)
+        print(f"M={M} {name:8s} N={N} K={Kd}: {s}", flush=True)
+        del a, w, b, gate, x, out
+for k in ("VS_GEMM_BACKEND", "VS_GEMM_IMPL", "VSTYLER_GEMM_TILE"):
+    os.environ.pop(k, None)

@@ -30,6 +30,7 @@ def permute_ref(src, dst, batch, s_local, world, cpr, ld_local, jstride, mode, p
 
 class CpuUlysses(UlyssesGroup):
     """Ulysses exchange on CPU tensors with gloo; attention by a supplied function."""
+    capturable = False
 
     def __init__(self, attn_fn, group=None):
         super().__init__(group)
@@ -48,7 +49,9 @@ class CpuUlysses(UlyssesGroup):
 
 class HostStagedUlysses(UlyssesGroup):
     """The product UlyssesGroup (HIP permutes + HIP attention) with its collectives staged through
-    host memory over gloo, so several ranks can share one GPU in a test."""
+    host memory over gloo, so several ranks can share one GPU in a test (host syncs: not capturable
+    into a hipGraph)."""
+    capturable = False
 
     def _all_to_all(self, recv, send):
         torch.cuda.synchronize()
@@ -67,6 +70,7 @@ class HostStagedUlysses(UlyssesGroup):
 class HostStagedCfgParallel(CfgParallel):
     """The product CfgParallel with host-staged gloo collectives (Ulysses halves: HostStagedUlysses),
     so its ranks can share one GPU in a test."""
+    capturable = False
 
     def __init__(self, group=None):
         super().__init__(group, ulysses_cls=HostStagedUlysses)

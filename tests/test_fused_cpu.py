@@ -77,3 +77,23 @@ def test_fp8_row_scale_rounds_quotient_to_bf16():
     assert s.dtype == torch.float32
     assert torch.equal(s.view(-1), torch.tensor([2.234375, 6.71875, 1.0]))
     assert s[0].item() != 1000.0 / 448.0
+
+
+def test_hotload_refuses_fp8_layers_atomically():
+    """hotload_lora on a model with an fp8 layer raises before touching ANY module:
+    the bf16 layer listed first keeps no adapter."""
+    import pytest
+    from vstyler.lora import hotload_lora
+    blk, _ = _block()
+    blk.cross_attn.o.weight_fp8 = torch.zeros(256, 256, dtype=torch.uint8)
+    r = 16
+    lora = {}
+    for n in ("self_attn.q", "cross_attn.o"):
+        lora[f"{n}.lora_A.default.weight"] = torch.ones(r, 256, dtype=BF16)
+        lora[f"{n}.lora_B.default.weight"] = torch.ones(256, r, dtype=BF16)
+    with pytest.raises(NotImplementedError, match="cross_attn.o"):
+        hotload_lora(blk, lora)
+    assert getattr(blk.self_attn.q, "lora_A", None) is None
+    del blk.cross_attn.o.weight_fp8
+    assert hotload_lora(blk, lora) == 2
+    assert blk.self_attn.q.lora_A.shape == (64, 256) and blk.cross_attn.o.lora_B.shape == (256, 64)

@@ -1,0 +1,118 @@
+"""The 256x256 8-phase GEMM (gemm_bf16_tn_8p, csrc/gemm.hip) through vs_gemm, forced onto the
+hand-written kernel (VS_GEMM_BACKEND=vstyler, VSTYLER_GEMM_TILE=256).
+
+Integer-valued operands keep every fp32 sum exact, so every output must equal the exact product
+bit for bit (through each epilogue's reference rounding points, oracle/wan_oracle.py) for:
+K-tile counts 1..6 (both buffer parities and every prefetch-tail branch of the phase schedule),
+partial last row / column tiles, the un-merged LoRA second K phase (layers.py:180-182) and the
+split tail (grid larger than the CU count).  Reference linears: wan_video_dit.py:131-134,157-160,
+209-210 through AutoWrappedLinear (vram_management/layers.py:173-188)."""
+import pytest
+import torch
+
+from oracle import wan_oracle as O
+from gpu_util import BF16
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def K(monkeypatch):
+    monkeypatch.setenv("VS_GEMM_BACKEND", "vstyler")
+    monkeypatch.setenv("VSTYLER_GEMM_TILE", "256")
+    from vstyler import kernels
+    return kernels
+
+
+def ints(*shape, g, lo=-3, hi=4):
+    return torch.randint(lo, hi, shape, generator=g, device="cuda").to(BF16)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 64), (300, 260, 128), (513, 256, 192), (256, 520, 256),
+                                    (700, 300, 320), (257, 1000, 384), (1024, 512, 5120)])
+def test_gemm8p_integer_exact(K, M, N, Kd):
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + Kd)
+    a, w = ints(M, Kd, g=g), ints(N, Kd, g=g)
+    w[:, 0] += (torch.arange(N, device="cuda") % 7).to(BF16)      # asymmetric: catches transposes
+    b = ints(N, g=g, lo=-8, hi=9)
+    out = torch.full((M, N), 7.0, dtype=BF16, device="cuda")
+    K.gemm(a, w, out, bias=b)
+    ref = (a.float() @ w.float().t() + b.float()).to(BF16)
+    assert torch.equal(out, ref)
+
+
+def test_gemm8p_epilogues_exact(K):
+    M, N, Kd, S = 600, 520, 448, 300
+    g = torch.Generator(device="cuda").manual_seed(3)
+    a, w, b = ints(M, Kd, g=g), ints(N, Kd, g=g), ints(N, g=g, lo=-8, hi=9)
+    y = (a.float() @ w.float().t() + b.float()).to(BF16).cpu()
+    res = torch.randn(M, N, generator=torch.Generator().manual_seed(4)).to(BF16)
+    gate = (0.25 * torch.randn(2, N, generator=torch.Generator().manual_seed(5))).to(BF16)
+    hint = torch.randn(M, N, generator=torch.Generator().manual_seed(6)).to(BF16)
+    out = torch.empty(M, N, dtype=BF16, device="cuda")
+    K.gemm(a, w, out, epilogue=K.VS_EPI_GELU, bias=b)
+    # GELU: the kernel's sigma form vs torch's tanh form differ by <= 1 ulp on the cancellation zone
+    ref = O.gelu_tanh(y)
+    d = (out.cpu().float() - ref.float()).abs()
+    assert (d <= ref.float().abs() * 2 ** -7 + 1e-6).all()
+    x = res.cuda()
+    K.gemm(a, w, x, epilogue=K.VS_EPI_GATE_RES, bias=b, residual=x, gate=gate.cuda(), gate_bstride=N,
+           rows_per_batch=S, hint=hint.cuda(), hint_scale=0.5)
+    ref = torch.cat([O.gate_residual(res[:S], gate[0], y[:S]), O.gate_residual(res[S:], gate[1], y[S:])])
+    ref = O.add(ref, O.bf(hint.float() * 0.5))
+    assert torch.equal(x.cpu(), ref)
+    x = res.cuda()
+    K.gemm(a, w, x, epilogue=K.VS_EPI_RES, bias=b, residual=x, alpha=0.125)
+    assert torch.equal(x.cpu(), O.add(res, O.bf(0.125 * y.float())))
+
+
+@pytest.mark.parametrize("Kd,r", [(256, 64), (320, 128), (5120, 128)])
+def test_gemm8p_lora_second_phase_exact(K, Kd, r):
+    M, N = 520, 384
+    g = torch.Generator(device="cuda").manual_seed(Kd + r)
+    x, w, b = ints(M, Kd, g=g), ints(N, Kd, g=g), ints(N, g=g, lo=-8, hi=9)
+    t, lb = ints(M, r, g=g, lo=-2, hi=3), ints(N, r, g=g, lo=-2, hi=3)
+    out = torch.empty(M, N, dtype=BF16, device="cuda")
+    K.gemm(x, w, out, bias=b, a2=t, w2=lb)
+    ref = (x.float() @ w.float().t() + t.float() @ lb.float().t() + b.float()).to(BF16)
+    assert torch.equal(out, ref)
+
+
+def test_gemm8p_split_tail_exact(K, monkeypatch):
+    """272 tiles on 256 CUs: 256 whole tiles + 16 tail tiles as K pieces, summed by the combine."""
+    M, N, Kd = 4352, 4096, 4096
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    g = torch.Generator(device="cuda").manual_seed(9)
+    a, w, b = ints(M, Kd, g=g), ints(N, Kd, g=g), ints(N, g=g, lo=-8, hi=9)
+    res = torch.randn(M, N, device="cuda", generator=g).to(BF16)
+    gate = (0.25 * torch.randn(2, N, device="cuda", generator=g)).to(BF16)
+    outs = {}
+    for split in (True, False):
+        if split:
+            monkeypatch.delenv("VS_GEMM_NO_SPLIT", raising=False)
+        else:
+            monkeypatch.setenv("VS_GEMM_NO_SPLIT", "1")
+        y = torch.empty(M, N, dtype=BF16, device="cuda")
+        K.gemm(a, w, y, bias=b)
+        x = res.clone()
+        K.gemm(a, w, x, epilogue=K.VS_EPI_GATE_RES, bias=b, residual=x, gate=gate, gate_bstride=N,
+               rows_per_batch=M // 2, hint=res, hint_scale=0.5)
+        outs[split] = (y, x)
+    monkeypatch.delenv("VS_GEMM_NO_SPLIT", raising=False)
+    assert torch.equal(outs[True][0], (a.float() @ w.float().t() + b.float()).to(BF16))
+    for s_, u_ in zip(outs[True], outs[False]):
+        assert torch.equal(s_, u_)
+    if cus == 256:
+        assert K.gemm_split_plan(M, N, Kd, cus)[1] == 16
+
+
+def test_gemm8p_random_vs_fp32(K):
+    M, N, Kd = 2000, 1536, 5120
+    g = torch.Generator(device="cuda").manual_seed(11)
+    a = torch.randn(M, Kd, device="cuda", generator=g).to(BF16)
+    w = (0.05 * torch.randn(N, Kd, device="cuda", generator=g)).to(BF16)
+    out = torch.empty(M, N, dtype=BF16, device="cuda")
+    K.gemm(a, w, out)
+    ref = a.float() @ w.float().t()
+    rel = ((out.float() - ref).norm() / ref.norm()).item()
+    assert rel < 4e-3, rel

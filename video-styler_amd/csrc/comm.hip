@@ -109,6 +109,10 @@ extern "C" int vs_sp_init(int rank, int world, const void* unique_id, int device
     *out = nullptr;
     const Rccl* r = lib();
     if (!r) return VS_E_COMM;
+    // RCCL creates the communicator on the thread's current device: bind `device` for the call and
+    // restore the caller's device afterwards (no side effect on the calling thread)
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
     if (hipSetDevice(device) != hipSuccess) {
         set_error("hipSetDevice failed", nullptr);
         return VS_E_INVALID;
@@ -117,6 +121,7 @@ extern "C" int vs_sp_init(int rank, int world, const void* unique_id, int device
     memcpy(&id, unique_id, VS_SP_UNIQUE_ID_BYTES);
     ncclComm_t comm = nullptr;
     const int rc = check(*r, r->init_rank(&comm, world, id, rank), "ncclCommInitRank");
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
     if (rc != VS_OK) return rc;
     *out = new vs_sp_comm{comm, rank, world, device};
     return VS_OK;

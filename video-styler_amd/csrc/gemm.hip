@@ -547,6 +547,239 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
 
 
 // ---------------------------------------------------------------------------------------------
+// gemm_bf16_tn_8p: 256x256x64 tile, 8 waves, 4 phases per K-tile (cdna_hip_programming.md §5,
+// "The 256² 8-phase template", written for this epilogue / split-tail / LoRA contract).
+//
+// LDS: two buffers (even / odd K-tile) of four 16-KB half-tiles each: A rows 0-127 (A0), A rows
+// 128-255 (A1), W rows 0-127 (B0), W rows 128-255 (B1); 128-B rows (64 bf16 of K) with the 16-B
+// chunk swizzle c ^ (row & 7) (conflict-free 16x16x32 fragment reads), filled by LDS-DMA
+// (buffer_load ... lds, one 1-KB piece = 8 rows per wave-instruction, swizzle on the source).
+// The tile's four 128x128 quadrants are computed one per phase by all 8 waves (wave (wr, wc) =
+// rows 64 wr.. of the A half x columns 32 wc.. of the W half: 16 MFMAs per phase):
+//   ph0 (A0,B0): read A-frags (8 ds_read_b128) + B0-frags (4)    ph1 (A0,B1): read B1-frags (4)
+//   ph2 (A1,B1): read A-frags (8)                                ph3 (A1,B0): no reads
+// so half-tile A0/B0 of a buffer is dead after ph0, B1 after ph1, A1 after ph2, and each phase
+// restages one half-tile whose last read is >= 1 phase (and one workgroup barrier) behind it:
+//   ph0: A1 of tile t+1, ph1: A0 of t+2, ph2: B0 of t+2, ph3: B1 of t+2.
+// Phase = [fragment reads; 2 DMA pieces; (ph3: s_waitcnt vmcnt(6)); s_barrier; lgkmcnt(0);
+// setprio 1; 16 MFMAs; setprio 0; s_barrier]: the ph3 wait retires tile t+1 while the three
+// half-tiles issued after it stay in flight across the barriers (counted vmcnt, raw s_barrier,
+// never vmcnt(0) in the main loop).  Product D[n][m] = W.A^T (16x16x32, W fragment as the A
+// operand) so each lane owns 4 consecutive output columns for the fused epilogue.
+// ---------------------------------------------------------------------------------------------
+constexpr int T8 = 256, HT8 = 128 * 128, BUF8 = 4 * HT8, LDS8 = 2 * BUF8;   // 16 KB, 64 KB, 128 KB
+constexpr int R_A0 = 0, R_A1 = HT8, R_B0 = 2 * HT8, R_B1 = 3 * HT8;
+
+__device__ __forceinline__ int q_off(int row, int ch) { return row * 128 + 16 * (ch ^ (row & 7)); }
+
+template <bool LORA>
+__global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
+    const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
+    bf16_t* C, long long ldc, int M, int N, int K, const bf16_t* __restrict__ A2, long long lda2,
+    const bf16_t* __restrict__ W2, long long ldw2, int K2, Epi ep, int ntm, int ntn, int nmain, int ksplit,
+    int piece_k, float* __restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    // blocks [0, nmain) own whole tiles (XCD-remapped); the blocks after them run the last tiles of
+    // the grid as ksplit K ranges of piece_k each (fp32 partial tiles for gemm_split_combine)
+    int pid, piece = -1;
+    if ((int)blockIdx.x < nmain) {
+        pid = xcd_remap(blockIdx.x, nmain);
+    } else {
+        const int t = blockIdx.x - nmain;
+        pid = nmain + t / ksplit;
+        piece = t % ksplit;
+    }
+    int tm, tn;
+    tile_of(pid, ntm, ntn, tm, tn);
+    const int m0 = tm * T8, n0 = tn * T8;
+    const int kb = piece < 0 ? 0 : piece * piece_k;
+    const int Kp = piece < 0 ? K : min(K - kb, piece_k);
+    const int nk1 = Kp / 64;
+    const int nt = nk1 + (piece < 0 ? K2 / 64 : 0);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 2, wc = wave & 3;
+
+    f32x4_t acc[2][2][4][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    // DMA: a half-tile is 16 pieces of 1 KB; wave w issues pieces 2w, 2w+1 = rows 16w + 8j + L/8,
+    // lane L lands in physical chunk L%8 of its row and fetches logical chunk (L%8) ^ (L/8).
+    // Buffer descriptors are rebased on the tile's first row, so a voffset is < 256 rows x ld.
+    const int prow = 16 * wave + (lane >> 3);
+    const unsigned pcol = 16u * ((lane & 7) ^ (lane >> 3));
+    auto rsrc = [](const void* base) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t ra = rsrc(A + (long long)m0 * lda + kb);
+    const __amdgpu_buffer_rsrc_t rw = rsrc(W + (long long)n0 * ldw + kb);
+    unsigned voa[2][2], vow[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int r = h * 128 + prow + 8 * j;
+            voa[h][j] = (unsigned)(min(m0 + r, M - 1) - m0) * (unsigned)(lda * 2) + pcol;
+            vow[h][j] = (unsigned)(min(n0 + r, N - 1) - n0) * (unsigned)(ldw * 2) + pcol;
+        }
+    // stage half-tile `which` (0 A0, 1 A1, 2 B0, 3 B1) of K-tile t into buffer t & 1
+    auto stage = [&](int t, int which) {
+        char* dst = smem + (t & 1) * BUF8 + which * HT8 + wave * 2048;
+        const bool isw = which >= 2;
+        const int h = which & 1;
+        if (!LORA || t < nk1) {
+            const unsigned ko = (unsigned)t * 128u;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(isw ? rw : ra, (LDS_AS void*)(dst + j * 1024), 16,
+                                                         isw ? vow[h][j] : voa[h][j], ko, 0, 0);
+        } else {
+            // second K phase (un-merged LoRA): A2 . W2^T, rank-sized, addresses formed here
+            const unsigned ko = (unsigned)(t - nk1) * 128u;
+            const __amdgpu_buffer_rsrc_t r2 = rsrc(isw ? W2 + (long long)n0 * ldw2 : A2 + (long long)m0 * lda2);
+            const int lim = (isw ? N : M) - 1, r0 = isw ? n0 : m0;
+            const unsigned ld2 = (unsigned)((isw ? ldw2 : lda2) * 2);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int r = h * 128 + prow + 8 * j;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(r2, (LDS_AS void*)(dst + j * 1024), 16,
+                                                         (unsigned)(min(r0 + r, lim) - r0) * ld2 + pcol, ko, 0, 0);
+            }
+        }
+    };
+
+    const int frow = lane & 15, fch = lane >> 4;
+    bf16x8_t af[4][2], bf0[2][2], bf1[2][2];
+    auto read_a = [&](const char* buf, int region) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+                af[i][s] = *reinterpret_cast<const bf16x8_t*>(buf + region + q_off(wr * 64 + i * 16 + frow, 4 * s + fch));
+    };
+    auto read_b = [&](const char* buf, int region, bf16x8_t (&bf)[2][2]) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+                bf[j][s] = *reinterpret_cast<const bf16x8_t*>(buf + region + q_off(wc * 32 + j * 16 + frow, 4 * s + fch));
+    };
+    auto mfma16 = [&](f32x4_t (&c)[4][2], const bf16x8_t (&bf)[2][2]) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][s], af[i][s], c[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar_wait_lgkm = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // prologue: tile 0 (A0 B0 B1 A1) and tile 1 (A0 B0 B1) in flight, wait for tile 0
+    stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
+    if (nt > 1) {
+        stage(1, 0); stage(1, 2); stage(1, 3);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+
+    // one K-tile = 4 phases; the body is written for a pair of tiles so the buffer is a constant
+    auto tile4 = [&](int t, const char* buf) {
+        // ph0: quadrant (A0, B0)
+        read_a(buf, R_A0);
+        read_b(buf, R_B0, bf0);
+        if (t + 1 < nt) stage(t + 1, 1);
+        bar_wait_lgkm();
+        mfma16(acc[0][0], bf0);
+        bar();
+        // ph1: quadrant (A0, B1)
+        read_b(buf, R_B1, bf1);
+        if (t + 2 < nt) stage(t + 2, 0);
+        bar_wait_lgkm();
+        mfma16(acc[0][1], bf1);
+        bar();
+        // ph2: quadrant (A1, B1)
+        read_a(buf, R_A1);
+        if (t + 2 < nt) stage(t + 2, 2);
+        bar_wait_lgkm();
+        mfma16(acc[1][1], bf1);
+        bar();
+        // ph3: quadrant (A1, B0); retire tile t+1 (the 3 half-tiles of t+2 stay in flight)
+        if (t + 2 < nt) {
+            stage(t + 2, 3);
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else if (t + 1 < nt) {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        bar_wait_lgkm();
+        mfma16(acc[1][0], bf0);
+        bar();
+    };
+#pragma nounroll
+    for (int t = 0; t < nt; t += 2) {
+        tile4(t, smem);
+        if (t + 1 < nt) tile4(t + 1, smem + BUF8);
+    }
+
+    // output: acc[qa][qb][i][j][e] = C[m][n], m = m0 + 128 qa + 64 wr + 16 i + (lane & 15),
+    // n = n0 + 128 qb + 32 wc + 16 j + 4 (lane >> 4) + e
+    if (piece >= 0) {
+        float* pp = part + ((long long)(pid - nmain) * ksplit + piece) * T8 * T8;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        *reinterpret_cast<f32x4_t*>(pp + (128 * a + 64 * wr + 16 * i + (lane & 15)) * T8 + 128 * b +
+                                                    32 * wc + 16 * j + 4 * (lane >> 4)) = acc[a][b][i][j];
+        return;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = m0 + 128 * a + 64 * wr + 16 * i + (lane & 15);
+            if (m >= M) continue;
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int n = n0 + 128 * b + 32 * wc + 16 * j + 4 * (lane >> 4);
+                    if (n >= N) continue;
+                    epilogue_store(acc[a][b][i][j], m, n, C, ldc, ep);
+                }
+        }
+}
+
+
+// ---------------------------------------------------------------------------------------------
 // 256x256 tile, 4 waves (one per SIMD), 128x128 output per wave: the accumulators (256 fp32 per
 // lane) live in AGPRs, which the MFMAs read and write directly, so a wave owns 64 MFMAs
 // (16x16x32) per 32-deep K half-step against 16 fragment reads (vs 32 against 12 in the 8-wave
@@ -926,7 +1159,7 @@ extern "C" int vs_debug_gemm_stamps(unsigned long long* host_out) {
 constexpr int MAX_SPLIT_PIECES = 512;        // 512 x 256 KB fp32 partial tiles
 struct KSplit { int nmain = 0, ntail = 0, ksplit = 1, piece_k = 0; };
 
-KSplit plan_ksplit(int ntiles, int nh, int cus) {
+KSplit plan_ksplit(int ntiles, int nh, int cus, int step = HK) {
     // Cost model in microseconds, calibrated on MI355X (tests/probes/split_ab.py): a whole tile
     // takes t = K * 0.029 us at ~1150 TF/s; a round of pieces costs t/f plus ~18 us (prologue and
     // the fp32 partial-tile writes, 256 KB per piece); the combine ~5 us + 0.065 us per partial
@@ -936,10 +1169,10 @@ KSplit plan_ksplit(int ntiles, int nh, int cus) {
     if (cus <= 0 || ntiles < cus) return p;
     const int tail = ntiles % cus;
     if (tail == 0) return p;
-    const double t = nh * HK * 0.029;
+    const double t = nh * step * 0.029;
     double best = 0.85 * t;
     int bf = 1;
-    for (int f = 2; f <= 16 && tail * f <= MAX_SPLIT_PIECES && nh / f >= 16; ++f) {
+    for (int f = 2; f <= 16 && tail * f <= MAX_SPLIT_PIECES && nh * step / f >= 512; ++f) {
         const int rounds = (tail * f + cus - 1) / cus;
         const double cost = rounds * (t / f + 18.0) + 5.0 + 0.065 * tail * f;
         if (cost < best) { best = cost; bf = f; }
@@ -948,7 +1181,7 @@ KSplit plan_ksplit(int ntiles, int nh, int cus) {
     const int piece_h = (nh + bf - 1) / bf;
     p.ntail = tail;
     p.nmain = ntiles - tail;
-    p.piece_k = piece_h * HK;
+    p.piece_k = piece_h * step;
     p.ksplit = (nh + piece_h - 1) / piece_h;
     return p;
 }
@@ -1059,11 +1292,8 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
     if (rc) return rc;
     // 256x256 schedule once there are enough tiles to fill the chip, 128x128 otherwise
     // (VSTYLER_GEMM_TILE=128|256 forces one for A/B measurements)
-    static int force = -1;
-    if (force < 0) {
-        const char* e = getenv("VSTYLER_GEMM_TILE");
-        force = e ? atoi(e) : 0;
-    }
+    const char* tile_env = getenv("VSTYLER_GEMM_TILE");
+    const int force = tile_env ? atoi(tile_env) : 0;
     const bool big = force ? force == 256
                           : k >= 4096 && (long long)((m + BT - 1) / BT) * ((n + BT - 1) / BT) >= 240;
     // GELU on the hipBLASLt route: the library's fused GELU_BIAS epilogue (GELU-tanh of the fp32
@@ -1103,6 +1333,38 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
                                (bf16_t*)c, ldc, m, n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2,
                                k2, ep, tm, tn);
             VS_CHECK_LAUNCH();
+            return VS_OK;
+        }
+        static bool attr8 = false;
+        if (!attr8) {
+            (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_8p<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      LDS8);
+            (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_8p<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      LDS8);
+            attr8 = true;
+        }
+        const char* impl_env = getenv("VS_GEMM_IMPL");   // pp: the r2 ping-pong kernel (A/B only)
+        const bool pp = impl_env && impl_env[0] == 'p';
+        if (!pp) {
+            KSplit sp = k2 ? KSplit{tm * tn, 0, 1, 0}
+                           : plan_ksplit(tm * tn, k / 64, vs_cus_for_split("VS_GEMM_NO_SPLIT"), 64);
+            float* part = nullptr;
+            if (sp.ntail) {
+                part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
+                if (!part) sp = KSplit{tm * tn, 0, 1, 0};
+            }
+            hipLaunchKernelGGL(k2 ? gemm_bf16_tn_8p<true> : gemm_bf16_tn_8p<false>,
+                               dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(512), LDS8, (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw, (bf16_t*)c, ldc, m,
+                               n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2, k2, ep, tm, tn, sp.nmain,
+                               sp.ksplit, sp.piece_k, part);
+            VS_CHECK_LAUNCH();
+            if (sp.ntail) {
+                const long long threads = (long long)sp.ntail * BT * (BT / 4);
+                hipLaunchKernelGGL(gemm_split_combine, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                                   (hipStream_t)stream, part, (bf16_t*)c, ldc, m, n, ep, tm, tn, sp.nmain, sp.ntail,
+                                   sp.ksplit);
+                VS_CHECK_LAUNCH();
+            }
             return VS_OK;
         }
         static int buf_ok = -1;

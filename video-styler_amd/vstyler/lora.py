@@ -105,22 +105,29 @@ def merge_lora(model, lora, alpha=1.0):
 def hotload_lora(model, lora, alpha=1.0):
     """Attach (alpha*A, B) to each matching Linear (layers.py:180-182 appends to the layer's lists);
     an adapter already attached stays and the new one is stacked onto it.  The GEMM adds them all as
-    one fused K phase.  fp8 layers take no hot-loaded LoRA (linear() raises): merge instead."""
-    updated = 0
+    one fused K phase.  fp8 layers take no hot-loaded LoRA (gap vs the reference's AutoWrappedLinear,
+    layers.py:168-180, which adds the unmerged term after fp8_linear): merge instead.  Every matching
+    module is checked before any is touched, so a refused call leaves the model unchanged."""
+    targets = []
     for name, module in model.named_modules():
         if not isinstance(module, Linear):
             continue
         ka, kb = f"{name}.lora_A.default.weight", f"{name}.lora_B.default.weight"
         if ka in lora and kb in lora:
-            if getattr(module, "weight_fp8", None) is not None:
-                raise NotImplementedError(f"hot-loaded LoRA on the fp8 layer {name}: merge the LoRA instead")
-            a = (lora[ka].to(device=module.weight.device, dtype=BF16) * alpha).to(BF16)   # [r, in]
-            b = lora[kb].to(device=module.weight.device, dtype=BF16)                       # [out, r]
-            rp = (a.shape[0] + 63) // 64 * 64
-            a, b = _padded(a, rows=rp), _padded(b, cols=rp)   # [rp, in], [out, rp]
-            if getattr(module, "lora_A", None) is not None:
-                a = torch.cat([module.lora_A, a], dim=0)
-                b = torch.cat([module.lora_B, b], dim=1).contiguous()
-            module.lora_A, module.lora_B = a, b
-            updated += 1
+            targets.append((name, module, ka, kb))
+    fp8 = [name for name, module, _, _ in targets if getattr(module, "weight_fp8", None) is not None]
+    if fp8:
+        raise NotImplementedError(f"hot-loaded LoRA on fp8 layers ({', '.join(fp8[:3])}"
+                                  f"{', ...' if len(fp8) > 3 else ''}): merge the LoRA instead")
+    updated = 0
+    for name, module, ka, kb in targets:
+        a = (lora[ka].to(device=module.weight.device, dtype=BF16) * alpha).to(BF16)   # [r, in]
+        b = lora[kb].to(device=module.weight.device, dtype=BF16)                       # [out, r]
+        rp = (a.shape[0] + 63) // 64 * 64
+        a, b = _padded(a, rows=rp), _padded(b, cols=rp)   # [rp, in], [out, rp]
+        if getattr(module, "lora_A", None) is not None:
+            a = torch.cat([module.lora_A, a], dim=0)
+            b = torch.cat([module.lora_B, b], dim=1).contiguous()
+        module.lora_A, module.lora_B = a, b
+        updated += 1
     return updated

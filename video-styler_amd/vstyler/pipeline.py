@@ -184,6 +184,21 @@ class ModelConfig:
         self.path = files[0] if len(files) == 1 else files
 
 
+def sp_graph_ok(plan):
+    """True when the sequence-parallel plan's collectives can be captured into the step's hipGraph:
+    device-side RCCL collectives (torch.distributed 'nccl' or libvstyler's vs_sp_*) -- not
+    host-staged substitutes (tests) -- and VSTYLER_SP_GRAPH is not 0."""
+    if os.environ.get("VSTYLER_SP_GRAPH", "1") == "0":
+        return False
+    if plan is None:
+        from .usp import get_default_group
+        plan = get_default_group()
+    if plan is None:
+        return True
+    return all(getattr(p, "capturable", True) for p in
+               (plan, getattr(plan, "ulysses", None), getattr(plan, "full", None)) if p is not None)
+
+
 class DenoiseStepper:
     """Runs CFG denoising steps over device-resident state.  `step_fn(t_buf, d_buf)` enqueues one
     whole step (model_fn + fused CFG/Euler) reading the bf16 timestep and the fp32 dsigma from the
@@ -219,8 +234,14 @@ class DenoiseStepper:
 
     def capture(self):
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=self.stream):
-            self.step_fn(self.t_buf, self.d_buf)
+        try:
+            with torch.cuda.graph(g, stream=self.stream):
+                self.step_fn(self.t_buf, self.d_buf)
+        except Exception as e:      # e.g. a collective backend that cannot be captured: stay eager
+            import warnings
+            warnings.warn(f"hipGraph capture of the denoising step failed ({e!r}); running eager steps")
+            self.use_graph = False
+            return
         self.graph = g
 
 
@@ -344,15 +365,17 @@ class WanVideoPipeline:
         CFG as one batch-2 forward) + fused CFG/Euler update -- is then captured once into a hipGraph
         (torch.cuda.CUDAGraph over hipStreamBeginCapture) and replayed for every later step.  The
         graph reads the step's bf16 timestep and fp32 dsigma from two device slots refreshed before
-        each replay, so one capture serves all steps.  Eager under Ulysses SP (RCCL collectives are
-        issued eagerly) and when use_graph=False / VSTYLER_GRAPH=0."""
+        each replay, so one capture serves all steps.  Under Ulysses SP the RCCL collectives (async
+        all-to-alls on RCCL's stream, event-ordered) are captured with the step (sp_graph_ok); eager
+        with use_graph=False / VSTYLER_GRAPH=0, and under SP with VSTYLER_SP_GRAPH=0."""
         self.scheduler.set_timesteps(num_inference_steps, denoising_strength=denoising_strength, shift=sigma_shift)
         n_steps = len(self.scheduler.timesteps)
         use_cfg = cfg_scale != 1.0
         if use_graph is None:
             use_graph = os.environ.get("VSTYLER_GRAPH", "1") != "0"
         # TeaCache decides per step on the host (wan_video_new.py:1173-1192): eager steps
-        use_graph = use_graph and not self.use_unified_sequence_parallel and n_steps > 1 and tea_cache is None
+        use_graph = use_graph and n_steps > 1 and tea_cache is None and \
+            (not self.use_unified_sequence_parallel or sp_graph_ok(self.sp_group))
         ctx = torch.cat([context_posi, context_nega], 0) if use_cfg else context_posi
         latents = latents.to(device=self.device, dtype=BF16).contiguous().clone()
         ts = self.scheduler.timesteps.to(dtype=BF16).to(self.device)                     # :526

@@ -41,13 +41,15 @@ def init_distributed():
 
 
 def get_default_group():
-    """The parallel plan of the whole world: CfgParallel when VSTYLER_CFG_PARALLEL selects it
-    ("auto", the default: at world size 2, where Ulysses would send half of every q|k|v over
-    one xGMI link per block while CFG parallelism needs one 2-sample velocity exchange per step;
-    "1": at every even world size, Ulysses inside each half; "0": never), else one UlyssesGroup."""
+    """The parallel plan of the whole world: one UlyssesGroup over all ranks (the reference's USP,
+    "0", the default), or CfgParallel when VSTYLER_CFG_PARALLEL selects it ("1": at every even world
+    size, Ulysses inside each half; "auto": at world size 2 only, where Ulysses would send half of
+    every q|k|v over one xGMI link per block while CFG parallelism needs one 2-sample velocity
+    exchange per step).  CfgParallel stays opt-in until a multi-GPU RCCL run has shown its output
+    bit-identical to the single-GPU forward (the tests cover it with host-staged collectives)."""
     global _DEFAULT
     if _DEFAULT is None and dist.is_initialized():
-        mode = os.environ.get("VSTYLER_CFG_PARALLEL", "auto")
+        mode = os.environ.get("VSTYLER_CFG_PARALLEL", "0")
         if mode not in ("auto", "0", "1"):
             raise ValueError(f"VSTYLER_CFG_PARALLEL must be auto, 0 or 1, not {mode!r}")
         world = dist.get_world_size()
@@ -78,14 +80,18 @@ class _EventWork:
 class NativeComm:
     """RCCL through libvstyler's own C ABI (vs_sp_* in include/vstyler.h) instead of
     torch.distributed's process group -- the path a non-Python host binds.  torch.distributed is
-    used once, to hand rank 0's RCCL unique id to the other ranks.  All-to-alls run on a dedicated
-    stream ordered after the work enqueued so far (RCCL's async pattern); all-gathers run in place on
-    the current stream.  Selected with VSTYLER_SP_COMM=native."""
+    used once, to hand rank 0's RCCL unique id to the other ranks.  Every collective of the
+    communicator runs on ONE dedicated stream, ordered after the work enqueued so far on the caller's
+    stream (RCCL's async pattern), so collectives of one communicator never reorder; all_gather then
+    makes the caller's stream wait for it (synchronous to the caller, as torch's all_gather).  The
+    communicator is destroyed by close() or when the object is collected.  Selected with
+    VSTYLER_SP_COMM=native."""
 
     def __init__(self, group=None):
         from . import _lib
         self._lib = _lib
         lib = _lib.load()
+        self.handle = ctypes.c_void_p()
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         uid = ctypes.create_string_buffer(128)
         if self.rank == 0:
@@ -94,7 +100,6 @@ class NativeComm:
         src = 0 if group is None else dist.get_global_rank(group, 0)
         dist.broadcast_object_list(box, src=src, group=group)
         uid = ctypes.create_string_buffer(box[0], 128)
-        self.handle = ctypes.c_void_p()
         self._check(lib.vs_sp_init(self.rank, self.world, uid, torch.cuda.current_device(),
                                    ctypes.byref(self.handle)))
         self.stream = torch.cuda.Stream()
@@ -120,14 +125,23 @@ class NativeComm:
         return _EventWork(ev)
 
     def all_gather(self, recv, send):
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)
         self._check(self._lib.load().vs_sp_all_gather(self.handle, send.data_ptr(), recv.data_ptr(),
                                                       send.numel() * send.element_size(),
-                                                      torch.cuda.current_stream().cuda_stream))
+                                                      self.stream.cuda_stream))
+        cur.wait_stream(self.stream)
 
     def close(self):
-        if self.handle:
+        if getattr(self, "handle", None):
             self._check(self._lib.load().vs_sp_comm_destroy(self.handle))
             self.handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:       # interpreter shutdown: the library may already be unloaded
+            pass
 
 
 class _Exchange:
@@ -143,6 +157,8 @@ class UlyssesGroup:
     (tests use it to drive the real collectives on a one-GPU box).  comm: "torch" (torch.distributed
     on the process group, default) or "native" (NativeComm: RCCL through libvstyler's vs_sp_* ABI);
     default from VSTYLER_SP_COMM."""
+
+    capturable = True       # device-side RCCL collectives: the step's hipGraph may capture them
 
     def __init__(self, group=None, force_collectives=False, comm=None):
         self.group = group
@@ -312,9 +328,15 @@ class CfgParallel:
         self.pair_group = pairs[self.half_rank]
         self.ulysses = ulysses_cls(halves[self.cfg_rank], comm=comm) if u > 1 else None
         self.full = ulysses_cls(group, comm=comm)
+        comm = comm or os.environ.get("VSTYLER_SP_COMM", "torch")
+        # the velocity exchange goes through the same comm kind as the Ulysses exchanges
+        self.pair_native = NativeComm(self.pair_group) if comm == "native" else None
         self.collective_calls = 0
 
     def gather_cfg(self, out_pair, out_local):
         """out_local [1, ...] of this rank's CFG sample -> out_pair [2, ...] (sample 0, sample 1)."""
         self.collective_calls += 1
+        if self.pair_native is not None:
+            self.pair_native.all_gather(out_pair, out_local.contiguous())
+            return
         dist.all_gather_into_tensor(out_pair, out_local.contiguous(), group=self.pair_group)
