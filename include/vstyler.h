@@ -57,12 +57,13 @@ typedef struct vs_epilogue {
  * (layers.py:180-182): pass A2 = alpha * x A^T (computed by a previous vs_gemm) and W2 = B.
  * K and K2 must be multiples of 64, lda/ldw/lda2/ldw2 multiples of 8, N a multiple of 4.
  * Execution: grids of >= 1024 256x256 tiles (or >= 256 with K <= 8192) without a LoRA phase run
- * bf16(A W^T + bias) on hipBLASLt (needs a kind-2 workspace bound on the stream; the first eager
- * call of a shape times the heuristic's candidates and keeps the fastest, VS_LT_TUNE=0 disables)
- * and finish the epilogue with the same
- * code as the fused kernels (gate-residual / residual stage y in a kind-3 buffer of M*N*2 bytes);
- * otherwise, or when those are not bound, the MFMA kernels (with the kind-1 split tail).  Every
- * route has the same rounding points; results differ only in fp32 summation order.
+ * bf16(A W^T + bias) on hipBLASLt (needs a kind-2 workspace bound on the stream; the heuristic's
+ * first algorithm for the shape, deterministic) and finish the epilogue with the same code as the
+ * fused kernels (gate-residual / residual stage y in a kind-3 buffer of M*N*2 bytes); otherwise, or
+ * when those are not bound, the MFMA kernels (with the kind-1 split tail).  Every route keeps the
+ * reference's rounding points and differs only in fp32 summation order -- except the opt-in
+ * VS_LT_GELU=1, which runs GELU on hipBLASLt's GELU_BIAS epilogue (the GELU of the fp32 acc + bias,
+ * one rounding, instead of the reference's bf16 linear output followed by the GELU).
  */
 int vs_gemm(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc,
             int m, int n, int k, int epilogue, const vs_epilogue* epi,
@@ -132,8 +133,10 @@ int vs_split_workspace_bind(int kind, void* ptr, long long bytes, void* stream);
 
 /*
  * The hipBLASLt build vs_gemm's library route runs on: the path of the copy opened by the library
- * (default $ROCM_PATH/lib/libhipblaslt.so.1, VS_LT_LIB overrides), or "linked" when that failed and
- * the link-time binding (in a torch process: torch's bundled hipBLASLt) is used.
+ * (default: the private ROCm copy lt72/libvsblaslt7.so.1 next to libvstyler.so, made by
+ * scripts/vendor_blaslt.py; VS_LT_LIB=<path> overrides), or "linked" when that failed (the reason is
+ * printed to stderr once) and the link-time binding (in a torch process: torch's bundled hipBLASLt)
+ * is used.
  */
 const char* vs_blaslt_library(void);
 

@@ -74,6 +74,15 @@ def main(argv=None):
             continue
         n = patch(os.path.realpath(s), d)
         print(f"vendor_blaslt: {d} ({n} names renamed)")
+    # the copy finds its kernel library at <its dir>/hipblaslt/library (dladdr): a link to the ROCm
+    # tree (same path on the GPU box: same image), made here so libvstyler never writes at run time
+    link = os.path.join(out, "hipblaslt")
+    target = os.path.join(lib, "hipblaslt")
+    if os.path.islink(link) and os.readlink(link) != target:
+        os.remove(link)
+    if not os.path.lexists(link):
+        os.symlink(target, link)
+        print(f"vendor_blaslt: {link} -> {target}")
 
 
 if __name__ == "__main__":

@@ -131,3 +131,22 @@ def test_attention_nc_redo_at_production_grid(K, monkeypatch):
         r1 = min(b * S + (r // 256 + 1) * 256, (b + 1) * S)
         assert torch.equal(o3[r0:r1, h], c3[r0:r1, h]), (b, h, r)
     check(out, q, k, v, [(0, 0), (0, 3), (1, 38), (1, 39)], S, S, "NC redo grid")
+
+
+@pytest.mark.parametrize("variant", ["default", "VS_ATTN_NC=0", "VS_ATTN_NO_SPLIT=1", "VS_ATTN_NO_PERSIST=1"])
+def test_attention_14b_fused_qkv_views(K, monkeypatch, variant):
+    """The model's layout: q/k/v are column slices of ONE [B*S, 3D] q|k|v buffer (row stride 15 360,
+    batch stride 455 M elements), at the 14B CFG shape, under every kernel route."""
+    if variant != "default":
+        name, val = variant.split("=")
+        monkeypatch.setenv(name, val)
+    B, S, H = 2, 29640, 40
+    D3 = 3 * H * D
+    g = torch.Generator(device="cuda").manual_seed(5)
+    qkv = torch.randn(B * S, D3, device="cuda", generator=g).to(BF16)
+    qkv[:, :H * D] *= 2.0
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    out = torch.empty(B * S, H * D, device="cuda", dtype=BF16)
+    K.attention(q, k, v, out, H, B)
+    torch.cuda.synchronize()
+    check(out, q, k, v, [(0, 0), (0, 21), (1, 5), (1, 39)], S, S, f"fused q|k|v views {variant}")

@@ -116,3 +116,59 @@ def test_gemm8p_random_vs_fp32(K):
     ref = a.float() @ w.float().t()
     rel = ((out.float() - ref).norm() / ref.norm()).item()
     assert rel < 4e-3, rel
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 128), (300, 520, 256), (1000, 768, 640), (520, 300, 5120)])
+def test_gemm_fp8_8p_integer_exact(M, N, Kd, monkeypatch):
+    """gemm_fp8_tn_8p (VS_FP8_BACKEND=vstyler): integer operands exact in e4m3 with exact fp32 sums
+    must reproduce oracle.fp8_linear (layers.py:115-151) bit for bit: pins the MX 32x32x64 operand
+    maps, the fp8 chunk swizzle and the per-row scale."""
+    from vstyler import kernels as K
+    monkeypatch.setenv("VS_FP8_BACKEND", "vstyler")
+    g = torch.Generator().manual_seed(M + N + Kd)
+    x = torch.randint(-4, 5, (M, Kd), generator=g).to(BF16)
+    x[::5] *= 512          # rows whose max exceeds 448: scale 2**k > 1
+    w = torch.randint(-3, 4, (N, Kd), generator=g).to(BF16)
+    w[:, 0] += (torch.arange(N) % 5).to(BF16)
+    b = torch.randint(-8, 9, (N,), generator=g).to(BF16)
+    ref = O.fp8_linear(x, w, b)
+    x8 = torch.empty(M, Kd, dtype=torch.uint8, device="cuda")
+    sc = torch.empty(M, dtype=torch.float32, device="cuda")
+    K.quant_fp8_rows(x.cuda(), x8, sc)
+    out = torch.empty(M, N, dtype=BF16, device="cuda")
+    K.gemm_fp8(x8, sc, w.to(torch.float8_e4m3fn).view(torch.uint8).cuda(), out, bias=b.cuda())
+    assert torch.equal(out.cpu(), ref)
+
+
+def test_gemm_fp8_8p_split_tail_and_epilogue(monkeypatch):
+    """272 tiles: the split-tail pieces + combine (per-row scale applied after the sum) equal the
+    unsplit kernel on integer data; gate-residual + hint epilogue bit-exact vs the oracle."""
+    from vstyler import kernels as K
+    monkeypatch.setenv("VS_FP8_BACKEND", "vstyler")
+    M, N, Kd, S = 4352, 4096, 1024, 2176
+    g = torch.Generator().manual_seed(21)
+    x = torch.randint(-4, 5, (M, Kd), generator=g).to(BF16)
+    w = torch.randint(-3, 4, (N, Kd), generator=g).to(BF16)
+    b = torch.randint(-8, 9, (N,), generator=g).to(BF16)
+    res = torch.randn(M, N, generator=g).to(BF16)
+    gate = (0.25 * torch.randn(2, N, generator=g)).to(BF16)
+    hint = torch.randn(M, N, generator=g).to(BF16)
+    y = O.fp8_linear(x, w, b)
+    ref = torch.cat([O.gate_residual(res[:S], gate[0], y[:S]), O.gate_residual(res[S:], gate[1], y[S:])])
+    ref = O.add(ref, O.bf(hint.float() * 0.5))
+    x8 = torch.empty(M, Kd, dtype=torch.uint8, device="cuda")
+    sc = torch.empty(M, dtype=torch.float32, device="cuda")
+    K.quant_fp8_rows(x.cuda(), x8, sc)
+    w8 = w.to(torch.float8_e4m3fn).view(torch.uint8).cuda()
+    outs = []
+    for split in (True, False):
+        if split:
+            monkeypatch.delenv("VS_GEMM_NO_SPLIT", raising=False)
+        else:
+            monkeypatch.setenv("VS_GEMM_NO_SPLIT", "1")
+        xo = res.cuda()
+        K.gemm_fp8(x8, sc, w8, xo, epilogue=K.VS_EPI_GATE_RES, bias=b.cuda(), residual=xo, gate=gate.cuda(),
+                   gate_bstride=N, rows_per_batch=S, hint=hint.cuda(), hint_scale=0.5)
+        outs.append(xo.cpu())
+    monkeypatch.delenv("VS_GEMM_NO_SPLIT", raising=False)
+    assert torch.equal(outs[0], ref) and torch.equal(outs[1], ref)

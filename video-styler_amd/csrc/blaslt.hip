@@ -1,13 +1,22 @@
 // hipBLASLt for the plain part of the block GEMMs (host code only).
 //
 // The task's rule for MI355X: hand-written MFMA kernels for fused hot ops, the vendor library for
-// plain library GEMMs.  Measured on MI355X (profiles/r1/gemm_backend_ab_*.log), hipBLASLt's
-// stream-K 256x256x64 kernels run the 14B block GEMMs at 1240-1500 TF/s where gemm_bf16_tn_256
-// reaches 1040-1210, so vs_gemm routes C = A W^T + bias to hipBLASLt (one bf16 rounding of
-// acc + bias, exactly the first rounding point of every vs_gemm epilogue) and finishes any
-// further epilogue (GELU, SiLU, gate-residual [+ VACE hint], residual) with gemm_epi_apply,
-// which continues from that rounded value with the same code as the fused epilogue -- so both
-// paths have the reference's rounding points and differ only in fp32 summation order.
+// plain library GEMMs.  vs_gemm routes C = A W^T + bias of the large block GEMMs here (one bf16
+// rounding of acc + bias, exactly the first rounding point of every vs_gemm epilogue) and finishes
+// any further epilogue (GELU, SiLU, gate-residual [+ VACE hint], residual) with gemm_epi_apply8,
+// which continues from that rounded value with the same code as the fused epilogue -- so the route
+// keeps the reference's rounding points and differs from the MFMA kernels only in fp32 summation
+// order.  (The optional hipBLASLt GELU_BIAS epilogue, VS_LT_GELU=1, drops the rounding before the
+// GELU; it is off by default.)
+//
+// Algorithm choice (r3): the heuristic's FIRST pick for each shape, nothing else.  The r1/r2
+// in-process autotune timed up to 76 candidates per shape (the heuristic's 16 plus solutions from
+// an offline sweep) and kept the fastest whose output signature matched: at the 14B q|k|v shape
+// (59280 x 15360 x 5120) it picked a swept solution that computes WRONG outputs which the signature
+// check (two weighted sums) did not see -- the 14B-dim block pair then missed the oracle by a
+// relative L2 error of 0.38 (tests/test_production_model_gpu.py; profiles/r3/lt_autotune_bug.log).
+// A timing pick also made the fp32 summation order run-dependent.  The first pick is
+// deterministic and the one the parity tests cover.
 //
 // Column-major view: C[m][n] row-major is D = W^T(op T on the [k x n] col-major view of W[n][k])
 // times A (op N on the [k x m] col-major view of A[m][k]): D is n x m col-major with ld = ldc,
@@ -47,13 +56,10 @@ struct LtPlan {
     hipblasLtMatrixLayout_t lw = nullptr, la = nullptr, lc = nullptr;
     hipblasLtMatmulAlgo_t algo;
     size_t ws_need = 0;
-    bool ok = false, tuned = false;
-    int pick = 0;                                       // index of the algorithm in use in cand
-    int m = 0, n = 0, k = 0;                            // the problem (swept candidates, signature)
+    bool ok = false;
+    int m = 0, n = 0, k = 0;
     long long ldc = 0;
     bool fp8 = false, bias = false, gelu = false;
-    bool path_linked = false;                           // planned on the link-time library
-    std::vector<hipblasLtMatmulHeuristicResult_t> cand;
 };
 
 // The hipBLASLt in use.  In a Python process torch has already loaded its own bundled hipBLASLt
@@ -80,14 +86,7 @@ struct LtApi {
     decltype(&hipblasLtMatmulPreferenceSetAttribute) MatmulPreferenceSetAttribute =
         &hipblasLtMatmulPreferenceSetAttribute;
     decltype(&hipblasLtMatrixLayoutCreate) MatrixLayoutCreate = &hipblasLtMatrixLayoutCreate;
-    hipblasStatus_t (*getAlgosFromIndex)(hipblasLtHandle_t, std::vector<int>&,
-                                         std::vector<hipblasLtMatmulHeuristicResult_t>&) =
-        &hipblaslt_ext::getAlgosFromIndex;
     int (*getIndexFromAlgo)(hipblasLtMatmulAlgo_t&) = &hipblaslt_ext::getIndexFromAlgo;
-    hipblasStatus_t (*matmulIsAlgoSupported)(hipblasLtHandle_t, hipblasLtMatmulDesc_t, const void*,
-                                             hipblasLtMatrixLayout_t, hipblasLtMatrixLayout_t, const void*,
-                                             hipblasLtMatrixLayout_t, hipblasLtMatrixLayout_t, hipblasLtMatmulAlgo_t&,
-                                             size_t&) = &hipblaslt_ext::matmulIsAlgoSupported;
     std::string path = "linked";
 };
 
@@ -115,21 +114,23 @@ LtApi load_lt_api() {
         const std::string d = own_dir() + "/lt72";
         path = d + "/libvsblaslt7.so.1";
         roller = d + "/libvsroller7.so.1";
+        // the copy finds its kernel library through <its dir>/hipblaslt, a link to the ROCm tree that
+        // scripts/vendor_blaslt.py makes at build time (nothing is written here at run time)
         const std::string kl = d + "/hipblaslt";
-        if (access(kl.c_str(), F_OK) != 0) (void)symlink((rocm_lib + "/hipblaslt").c_str(), kl.c_str());
         if (access((kl + "/library").c_str(), F_OK) != 0) {
-            if (lt_debug()) std::fprintf(stderr, "[lt] no kernel library at %s/library\n", kl.c_str());
+            std::fprintf(stderr, "[vstyler] private hipBLASLt copy unusable (no kernel library at %s/library): "
+                                 "using the link-time hipBLASLt\n", kl.c_str());
             return api;
         }
     }
     if (path == "linked") return api;
     if (!roller.empty() && !dlopen(roller.c_str(), RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND)) {
-        if (lt_debug()) std::fprintf(stderr, "[lt] dlopen %s: %s\n", roller.c_str(), dlerror());
+        std::fprintf(stderr, "[vstyler] hipBLASLt dlopen %s: %s (using the link-time hipBLASLt)\n", roller.c_str(), dlerror());
         return api;
     }
     void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
     if (!h) {
-        if (lt_debug()) std::fprintf(stderr, "[lt] dlopen %s: %s\n", path.c_str(), dlerror());
+        std::fprintf(stderr, "[vstyler] hipBLASLt dlopen %s: %s (using the link-time hipBLASLt)\n", path.c_str(), dlerror());
         return api;
     }
     LtApi d;
@@ -151,15 +152,14 @@ LtApi load_lt_api() {
     sym(d.MatmulPreferenceDestroy, "hipblasLtMatmulPreferenceDestroy");
     sym(d.MatmulPreferenceSetAttribute, "hipblasLtMatmulPreferenceSetAttribute");
     sym(d.MatrixLayoutCreate, "hipblasLtMatrixLayoutCreate");
-    sym(d.getAlgosFromIndex, "_ZN13hipblaslt_ext17getAlgosFromIndexEPvRSt6vectorIiSaIiEERS1_I33_"
-                             "hipblasLtMatmulHeuristicResult_tSaIS5_EE");
     sym(d.getIndexFromAlgo, "_ZN13hipblaslt_ext16getIndexFromAlgoER22_hipblasLtMatmulAlgo_t");
-    sym(d.matmulIsAlgoSupported, "_ZN13hipblaslt_ext21matmulIsAlgoSupportedEPvP27hipblasLtMatmulDescOpaque_tPKvP29"
-                                 "hipblasLtMatrixLayoutOpaque_tS6_S4_S6_S6_R22_hipblasLtMatmulAlgo_tRm");
     if (!ok) {
+        std::fprintf(stderr, "[vstyler] hipBLASLt copy %s lacks symbols: using the link-time hipBLASLt\n",
+                     path.c_str());
         dlclose(h);
         return api;
     }
+    if (lt_debug()) std::fprintf(stderr, "[lt] using %s\n", path.c_str());
     d.path = path;
     return d;
 }
@@ -182,71 +182,8 @@ hipblasLtHandle_t handle_for(int dev) {
     return h;
 }
 
-// Solutions the heuristic's first 16 do not hold but an exhaustive sweep (tests/probes/lt_sweep.cpp
-// over all 2081 bf16 TN solutions that support the problem, profiles/r2/lt_sweep.log) found
-// fastest on the 14B block shapes: 4-7.5 % over the heuristic's best at 59280 rows, 8-19 % at the
-// 3705-row Ulysses SP = 8 shapes.  Library solution indices of the ROCm-7.2 build (an index that
-// does not resolve or does not support the problem is skipped), appended to the autotune's
-// candidates.  ONLY for the swept problems -- the four 14B block GEMMs with their bias / GELU_BIAS
-// epilogue at 3705, 7410, 14820, 29640 and 59280 rows, where all 2081 solutions ran without a fault
-// (profiles/r2/lt_sweep.log, lt_sweep2.log, lt_sweep3.log): a solution the library reports as supporting a
-// problem can still fault on it (one did on the 1.3B FFN-up, N 8960 K 1536 with GELU_BIAS), and an
-// output check cannot catch a memory fault.  VS_LT_SWEPT=0 keeps the heuristic list alone.
-constexpr int kSweptAlgos[] = {438309, 438310, 438346, 438347, 438386, 438515, 438529, 438583, 438789,
-                               438921, 438983, 439036, 439044, 439045, 439048, 439059, 439079, 439093,
-                               439110, 439112, 439200, 439212, 439217, 439228, 439229, 439260, 439265,
-                               439266, 439269, 439274, 439282, 439285, 439287, 439296, 439297, 439301,
-                               439302, 439303, 439304, 439305, 439306, 439313, 439316, 439321, 439323,
-                               439324, 439325, 439326, 439352, 439357, 439361, 439363, 439383, 439391,
-                               439397, 439398, 439399, 439402, 439421, 440058, 440230, 440236};
-struct SweptShape {
-    int n, k;
-    bool gelu;
-};
-// (the 1.3B q|k|v and o problems were swept fault-free too, but with their swept picks the C2 step
-// measured 1 % slower -- the faster GEMMs cost the following attention launches clock,
-// profiles/r2/lt_lib_workloads_ab_r2m.log vs _r2n.log -- so they keep the heuristic list)
-constexpr SweptShape kSweptShapes[] = {{15360, 5120, false}, {5120, 5120, false}, {13824, 5120, true},
-                                       {5120, 13824, false}};
-// the row counts the sweeps covered (every solution ran without a fault): SP = 1 (2 x 29640), CFG
-// parallel (29640), Ulysses SP = 4 / 8 per CFG sample (7410 / 3705) and their two-sample merged
-// phases (14820 / 7410; profiles/r2/lt_sweep3.log)
-constexpr int kSweptRows[] = {3705, 7410, 14820, 29640, 59280};
-
-void add_swept_candidates(LtPlan& p, hipblasLtHandle_t h, size_t ws_bytes) {
-    if (p.fp8 || !p.bias || p.path_linked) return;
-    bool swept = false;
-    for (const SweptShape& s : kSweptShapes) swept |= s.n == p.n && s.k == p.k && s.gelu == p.gelu;
-    swept &= std::find(std::begin(kSweptRows), std::end(kSweptRows), p.m) != std::end(kSweptRows);
-    if (!swept) return;
-    if (const char* e = std::getenv("VS_LT_SWEPT"); e && e[0] == '0') return;
-    std::vector<int> idx(std::begin(kSweptAlgos), std::end(kSweptAlgos));
-    std::vector<hipblasLtMatmulHeuristicResult_t> ex;
-    const hipblasStatus_t gs = lt().getAlgosFromIndex(h, idx, ex);
-    if (lt_debug()) std::fprintf(stderr, "[lt] m=%d n=%d k=%d: getAlgosFromIndex status %d, %zu of %zu resolved\n", p.m, p.n,
-                                 p.k, (int)gs, ex.size(), idx.size());
-    if (gs != HIPBLAS_STATUS_SUCCESS) return;
-    std::vector<int> have;
-    for (auto& c : p.cand) have.push_back(lt().getIndexFromAlgo(c.algo));
-    const float alpha = 1.f, beta = 0.f;
-    for (auto& r : ex) {
-        const int ix = lt().getIndexFromAlgo(r.algo);
-        if (ix < 0 || std::find(have.begin(), have.end(), ix) != have.end()) continue;
-        size_t need = 0;
-        const hipblasStatus_t ss =
-            lt().matmulIsAlgoSupported(h, p.desc, &alpha, p.lw, p.la, &beta, p.lc, p.lc, r.algo, need);
-        if (ss != HIPBLAS_STATUS_SUCCESS || need > ws_bytes) {
-            if (lt_debug()) std::fprintf(stderr, "[lt]   index %d: supported status %d, workspace %zu\n", ix, (int)ss, need);
-            continue;
-        }
-        r.workspaceSize = need;
-        p.cand.push_back(r);
-        have.push_back(ix);
-    }
-}
-
 // builds (once per shape) the descriptor, the layouts and the heuristic's first algorithm that
-// fits `ws_bytes` of workspace, plus the swept candidates
+// fits `ws_bytes` of workspace
 LtPlan* plan_for(const LtKey& key, size_t ws_bytes) {
     auto it = g_plans.find(key);
     if (it != g_plans.end()) return it->second.ok ? &it->second : nullptr;
@@ -258,7 +195,6 @@ LtPlan* plan_for(const LtKey& key, size_t ws_bytes) {
     p.fp8 = key.fp8;
     p.bias = key.bias;
     p.gelu = key.gelu;
-    p.path_linked = lt().path == "linked";
     hipblasLtHandle_t h = handle_for(key.dev);
     if (!h) return nullptr;
     if (lt().MatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return nullptr;
@@ -289,127 +225,18 @@ LtPlan* plan_for(const LtKey& key, size_t ws_bytes) {
     if (lt().MatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return nullptr;
     const uint64_t wsb = ws_bytes;
     lt().MatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb));
-    // candidates the autotune times: 16 (VS_LT_NCAND = 1..64 for A/B runs)
-    constexpr int MAXCAND = 64;
-    int ncand = 16;
-    if (const char* e = std::getenv("VS_LT_NCAND")) ncand = std::min(MAXCAND, std::max(1, std::atoi(e)));
-    hipblasLtMatmulHeuristicResult_t res[MAXCAND];
+    hipblasLtMatmulHeuristicResult_t res[1];
     int found = 0;
-    const hipblasStatus_t st =
-        lt().MatmulAlgoGetHeuristic(h, p.desc, p.lw, p.la, p.lc, p.lc, pref, ncand, res, &found);
+    const hipblasStatus_t st = lt().MatmulAlgoGetHeuristic(h, p.desc, p.lw, p.la, p.lc, p.lc, pref, 1, res, &found);
     lt().MatmulPreferenceDestroy(pref);
     if (st != HIPBLAS_STATUS_SUCCESS || found < 1) return nullptr;
-    p.cand.assign(res, res + found);
     p.algo = res[0].algo;
     p.ws_need = res[0].workspaceSize;
     p.ok = true;
-    return &p;
-}
-
-// Output signature of a candidate: sum |c| and sum c * r(i, j) with a fixed pseudo-random weight
-// r in [-0.5, 0.5), fp64 partials.  Two correct algorithms differ only in fp32 summation order (a
-// bf16 ulp on some outputs: relative differences ~1e-6 of sum |c|); wrong or misplaced outputs move
-// the weighted sum by ~1/sqrt(m n) of sum |c|.
-__global__ void lt_signature(const unsigned short* __restrict__ c, long long ldc, int m, int n, double* out) {
-    double s0 = 0.0, s1 = 0.0;
-    const long long total = (long long)m * n;
-    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-         e += (long long)gridDim.x * blockDim.x) {
-        const int i = (int)(e / n), j = (int)(e % n);
-        const float x = __uint_as_float((unsigned)c[(long long)i * ldc + j] << 16);
-        unsigned hs = (unsigned)i * 2654435761u ^ (unsigned)j * 40503u;
-        hs ^= hs >> 15;
-        hs *= 0x2c1b3c6du;
-        hs ^= hs >> 12;
-        s0 += fabs((double)x);
-        s1 += (double)x * ((double)(hs & 1023) / 1024.0 - 0.5);
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        s0 += __shfl_xor(s0, o);
-        s1 += __shfl_xor(s1, o);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(out, s0);
-        atomicAdd(out + 1, s1);
-    }
-}
-
-// Autotune (once per shape, on its first eager call): time every candidate (the heuristic's list
-// and the swept solutions) on the call's own operands and keep the fastest whose output signature
-// matches the first candidate's (|d sum c r| <= 1e-5 sum |c|, |d sum |c|| <= 1e-3 sum |c|): an
-// algorithm the library lists but that computes something else is never picked.  The heuristic's
-// first pick is not the fastest on every block shape (profiles/r1/gemm_lt_tune_*.log).  Skipped
-// while the stream is being captured into a graph (no host sync possible) and with VS_LT_TUNE=0.
-void autotune(LtPlan& p, hipblasLtHandle_t h, const void* a, const void* w, void* c, float* ws, size_t ws_bytes,
-              hipStream_t stream) {
-    if (p.cand.size() < 2) { p.tuned = true; return; }
-    const char* env = std::getenv("VS_LT_TUNE");
-    if (env && env[0] == '0') { p.tuned = true; return; }
-    // inside a graph capture: keep the heuristic pick for now and tune on a later eager call
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
-    p.tuned = true;
-    add_swept_candidates(p, h, ws_bytes);
-    hipEvent_t e0, e1;
-    if (hipEventCreate(&e0) != hipSuccess) return;
-    if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return; }
-    const float alpha = 1.f, beta = 0.f;
-    float best = 1e30f, first = 1e30f;
-    size_t bi = 0;
-    double ref[2] = {0.0, 0.0};
-    bool have_ref = false;
-    const int sm = p.m, sn = p.n;
-    for (size_t i = 0; i < p.cand.size(); ++i) {
-        if (p.cand[i].workspaceSize > ws_bytes) continue;
-        auto run = [&]() {
-            return lt().Matmul(h, p.desc, &alpha, w, p.lw, a, p.la, &beta, c, p.lc, c, p.lc, &p.cand[i].algo, ws,
-                                   ws_bytes, stream);
-        };
-        if (run() != HIPBLAS_STATUS_SUCCESS) continue;
-        // the candidate's output signature (in the workspace head, free once the GEMM is done)
-        double sig[2] = {0.0, 0.0};
-        if (hipMemsetAsync(ws, 0, 2 * sizeof(double), stream) != hipSuccess) continue;
-        lt_signature<<<1024, 256, 0, stream>>>(static_cast<const unsigned short*>(c), p.ldc, sm, sn,
-                                               reinterpret_cast<double*>(ws));
-        if (hipMemcpyAsync(sig, ws, sizeof(sig), hipMemcpyDeviceToHost, stream) != hipSuccess ||
-            hipStreamSynchronize(stream) != hipSuccess)
-            continue;
-        if (!have_ref) {
-            if (!(sig[0] == sig[0]) || !(sig[1] == sig[1])) continue;
-            ref[0] = sig[0];
-            ref[1] = sig[1];
-            have_ref = true;
-        } else if (!(std::fabs(sig[1] - ref[1]) <= 1e-5 * ref[0]) || !(std::fabs(sig[0] - ref[0]) <= 1e-3 * ref[0])) {
-            if (lt_debug())
-                std::fprintf(stderr, "[lt]   cand %zu: signature (%.6g, %.6g) vs (%.6g, %.6g), rejected\n", i, sig[0],
-                             sig[1], ref[0], ref[1]);
-            continue;
-        }
-        (void)hipEventRecord(e0, stream);
-        bool ok = true;
-        for (int r = 0; r < 3 && ok; ++r) ok = run() == HIPBLAS_STATUS_SUCCESS;
-        (void)hipEventRecord(e1, stream);
-        if (!ok || hipEventSynchronize(e1) != hipSuccess) continue;
-        float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, e0, e1);
-        if (i == 0) first = ms;
-        if (ms < best) { best = ms; bi = i; }
-        if (lt_debug())
-            std::fprintf(stderr, "[lt]   cand %zu index %d: %.3f ms (3 calls)\n", i,
-                         lt().getIndexFromAlgo(p.cand[i].algo), ms);
-    }
-    // keep the heuristic's (deterministic) first pick unless another candidate is clearly faster,
-    // so that timing noise between near-equal candidates does not change the algorithm -- and the
-    // fp32 summation order -- from run to run or rank to rank
-    if (best > 0.97f * first) bi = 0;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    p.algo = p.cand[bi].algo;
-    p.ws_need = p.cand[bi].workspaceSize;
-    p.pick = (int)bi;
     if (lt_debug())
-        std::fprintf(stderr, "[lt] m=%d n=%d k=%d: %zu candidates, pick %zu (%.3f ms vs first %.3f)\n", p.m, p.n, p.k,
-                     p.cand.size(), bi, best, first);
+        std::fprintf(stderr, "[lt] m=%d n=%d k=%d: heuristic pick index %d\n", p.m, p.n, p.k,
+                     lt().getIndexFromAlgo(p.algo));
+    return &p;
 }
 
 }  // namespace
@@ -430,7 +257,6 @@ int lt_gemm(const void* a, long long lda, const void* w, long long ldw, void* c,
         lt().MatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
     if (scale_a)
         lt().MatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_B_SCALE_POINTER, &scale_a, sizeof(scale_a));
-    if (!p->tuned) autotune(*p, handle_for(dev), a, w, c, ws, (size_t)ws_bytes, stream);
     const float alpha = 1.f, beta = 0.f;
     const hipblasStatus_t st = lt().Matmul(handle_for(dev), p->desc, &alpha, w, p->lw, a, p->la, &beta, c, p->lc,
                                                c, p->lc, &p->algo, ws, (size_t)ws_bytes, stream);

@@ -295,7 +295,8 @@ __device__ __forceinline__ void tile_of(int pid, int ntm, int ntn, int& tm, int&
 // piece order, then the same epilogue as the unsplit kernel
 __global__ __launch_bounds__(256) void gemm_split_combine(const float* __restrict__ part, bf16_t* C, long long ldc,
                                                           int M, int N, Epi ep, int ntm, int ntn, int nmain,
-                                                          int ntail, int ksplit) {
+                                                          int ntail, int ksplit,
+                                                          const float* __restrict__ scale_a = nullptr) {
     const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
     if (idx >= (long long)ntail * BT * (BT / 4)) return;
     const int t = (int)(idx / (BT * (BT / 4)));
@@ -308,6 +309,7 @@ __global__ __launch_bounds__(256) void gemm_split_combine(const float* __restric
     const float* pp = part + (long long)t * ksplit * BT * BT + row * BT + 4 * c4;
     f32x4_t a = *reinterpret_cast<const f32x4_t*>(pp);
     for (int j = 1; j < ksplit; ++j) a += *reinterpret_cast<const f32x4_t*>(pp + (long long)j * BT * BT);
+    if (scale_a) a *= scale_a[m];
     epilogue_store(a, m, n, C, ldc, ep);
 }
 
@@ -568,11 +570,15 @@ __global__ __launch_bounds__(NTHR8, 2) void gemm_bf16_tn_256(
 // operand) so each lane owns 4 consecutive output columns for the fused epilogue.
 // ---------------------------------------------------------------------------------------------
 constexpr int T8 = 256, HT8 = 128 * 128, BUF8 = 4 * HT8, LDS8 = 2 * BUF8;   // 16 KB, 64 KB, 128 KB
-constexpr int R_A0 = 0, R_A1 = HT8, R_B0 = 2 * HT8, R_B1 = 3 * HT8;
+// half-tiles (0 A0, 1 A1, 2 B0, 3 B1) of the two buffers interleaved: [A0 b0][A0 b1][A1 b0][A1 b1]
+// [B0 b0]...  so every A read of either buffer lies within the 16-bit ds_read offset of one base
+// VGPR per k-step, and every B read within that of a second one
+constexpr int R_A0 = 0, R_A1 = 1, R_B0 = 2, R_B1 = 3;
+__device__ __forceinline__ constexpr int hoff(int which, int b) { return (2 * which + b) * HT8; }
 
 __device__ __forceinline__ int q_off(int row, int ch) { return row * 128 + 16 * (ch ^ (row & 7)); }
 
-template <bool LORA>
+template <bool LORA, int SCHED>     // SCHED 0: reads at phase start, 1: prefetch, 2: prefetch + one barrier
 __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
     const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
     bf16_t* C, long long ldc, int M, int N, int K, const bf16_t* __restrict__ A2, long long lda2,
@@ -622,26 +628,27 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
     };
     const __amdgpu_buffer_rsrc_t ra = rsrc(A + (long long)m0 * lda + kb);
     const __amdgpu_buffer_rsrc_t rw = rsrc(W + (long long)n0 * ldw + kb);
-    unsigned voa[2][2], vow[2][2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int r = h * 128 + prow + 8 * j;
-            voa[h][j] = (unsigned)(min(m0 + r, M - 1) - m0) * (unsigned)(lda * 2) + pcol;
-            vow[h][j] = (unsigned)(min(n0 + r, N - 1) - n0) * (unsigned)(ldw * 2) + pcol;
-        }
-    // stage half-tile `which` (0 A0, 1 A1, 2 B0, 3 B1) of K-tile t into buffer t & 1
+    const int alim = M - 1 - m0, wlim = N - 1 - n0;
+    const unsigned ldab = (unsigned)(lda * 2), ldwb = (unsigned)(ldw * 2);
+    // stage half-tile `which` (0 A0, 1 A1, 2 B0, 3 B1) of K-tile t into buffer t & 1.  The two row
+    // offsets are formed here from two live VGPRs (row, chunk) -- kept opaque so the compiler does
+    // not hoist eight loop-invariant offsets into registers the fragment prefetch needs
     auto stage = [&](int t, int which) {
-        char* dst = smem + (t & 1) * BUF8 + which * HT8 + wave * 2048;
+        char* dst = smem + hoff(which, t & 1) + wave * 2048;
         const bool isw = which >= 2;
         const int h = which & 1;
         if (!LORA || t < nk1) {
             const unsigned ko = (unsigned)t * 128u;
+            int pr = prow;
+            unsigned pc = pcol;
+            asm volatile("" : "+v"(pr), "+v"(pc));
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(isw ? rw : ra, (LDS_AS void*)(dst + j * 1024), 16,
-                                                         isw ? vow[h][j] : voa[h][j], ko, 0, 0);
+            for (int j = 0; j < 2; ++j) {
+                const int r = h * 128 + pr + 8 * j;
+                const unsigned vo = isw ? (unsigned)min(r, wlim) * ldwb + pc : (unsigned)min(r, alim) * ldab + pc;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(isw ? rw : ra, (LDS_AS void*)(dst + j * 1024), 16, vo, ko,
+                                                         0, 0);
+            }
         } else {
             // second K phase (un-merged LoRA): A2 . W2^T, rank-sized, addresses formed here
             const unsigned ko = (unsigned)(t - nk1) * 128u;
@@ -659,19 +666,40 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
 
     const int frow = lane & 15, fch = lane >> 4;
     bf16x8_t af[4][2], bf0[2][2], bf1[2][2];
+    bf16x8_t ag[4][2], bg0[2][2];       // PRE: the A1 set and the next tile's B0 set
+    // fragment addresses: q_off(row0 + 16 i + frow, 4 s + fch) = q_off(row0 + frow, 4 s + fch) + 2048 i
+    // (row & 7 = frow & 7); one base per (buffer, operand, k-step) -- the second buffer lies past the
+    // 16-bit ds_read offset field -- kept opaque so the compiler keeps exactly these 8 bases
+    int abase[2], bbase[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        abase[s] = (int)(uintptr_t)smem + q_off(wr * 64 + frow, 4 * s + fch);
+        bbase[s] = (int)(uintptr_t)smem + hoff(R_B0, 0) + q_off(wc * 32 + frow, 4 * s + fch);
+        asm volatile("" : "+v"(abase[s]), "+v"(bbase[s]));
+    }
+    auto lds_frag = [&](int addr) {
+        return *reinterpret_cast<const LDS_AS bf16x8_t*>((const LDS_AS char*)(uintptr_t)(unsigned)addr);
+    };
     auto read_a = [&](const char* buf, int region) {
+        const int b = buf == smem ? 0 : 1;     // (buf: smem or smem + BUF8)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int s = 0; s < 2; ++s)
-                af[i][s] = *reinterpret_cast<const bf16x8_t*>(buf + region + q_off(wr * 64 + i * 16 + frow, 4 * s + fch));
+            for (int s = 0; s < 2; ++s) af[i][s] = lds_frag(abase[s] + hoff(region, b) + 2048 * i);
+    };
+    auto read_a_to = [&](const char* buf, int region, bf16x8_t (&a)[4][2]) {
+        const int b = buf == smem ? 0 : 1;     // (buf: smem or smem + BUF8)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) a[i][s] = lds_frag(abase[s] + hoff(region, b) + 2048 * i);
     };
     auto read_b = [&](const char* buf, int region, bf16x8_t (&bf)[2][2]) {
+        const int b = buf == smem ? 0 : 1;     // (buf: smem or smem + BUF8)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int s = 0; s < 2; ++s)
-                bf[j][s] = *reinterpret_cast<const bf16x8_t*>(buf + region + q_off(wc * 32 + j * 16 + frow, 4 * s + fch));
+            for (int s = 0; s < 2; ++s) bf[j][s] = lds_frag(bbase[s] + hoff(region, b) - hoff(R_B0, 0) + 2048 * j);
     };
     auto mfma16 = [&](f32x4_t (&c)[4][2], const bf16x8_t (&bf)[2][2]) {
         __builtin_amdgcn_s_setprio(1);
@@ -684,6 +712,25 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
                     c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][s], af[i][s], c[i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
     };
+    auto mfma16x = [&](f32x4_t (&c)[4][2], const bf16x8_t (&a)[4][2], const bf16x8_t (&bf)[2][2]) {
+#ifdef VS_G8_DIAG_NOMFMA    // timing diagnostics only: operands consumed, no MFMA issued
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                asm volatile("" : "+v"(c[i][j]) : "v"(a[i][0]), "v"(a[i][1]), "v"(bf[j][0]), "v"(bf[j][1]));
+        return;
+#endif
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][s], a[i][s], c[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
     auto bar = [&]() {
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_barrier" ::: "memory");
@@ -691,22 +738,46 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
     };
     auto bar_wait_lgkm = [&]() {
         __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("s_barrier" ::: "memory");
+        // the builtin form (not asm): the compiler's wait-count pass then knows every earlier LDS read
+        // has landed and adds no lgkmcnt(0) of its own in front of this phase's MFMAs
+        __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0)
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // SCHED 2: wait for my own reads BEFORE the barrier (the barrier then proves every wave's)
+    auto bar_wait_lgkm_pre = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0)
+#ifndef VS_G8_DIAG_NOBAR    // timing diagnostics only (races): no phase barrier
+        asm volatile("s_barrier" ::: "memory");
+#endif
         __builtin_amdgcn_sched_barrier(0);
     };
 
-    // prologue: tile 0 (A0 B0 B1 A1) and tile 1 (A0 B0 B1) in flight, wait for tile 0
-    stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
-    if (nt > 1) {
-        stage(1, 0); stage(1, 2); stage(1, 3);
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    constexpr bool PRE = SCHED >= 1;
+    if constexpr (SCHED == 2) {
+        // prologue: tiles 0 and 1 in flight (A0 B0 B1 A1 each), wait for tile 0
+        stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
+        if (nt > 1) {
+            stage(1, 0); stage(1, 2); stage(1, 3); stage(1, 1);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
     } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // prologue: tile 0 (A0 B0 B1 A1) and tile 1 (A0 B0 B1) in flight, wait for tile 0
+        stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
+        if (nt > 1) {
+            stage(1, 0); stage(1, 2); stage(1, 3);
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
     }
     bar();
 
     // one K-tile = 4 phases; the body is written for a pair of tiles so the buffer is a constant
-    auto tile4 = [&](int t, const char* buf) {
+    auto tile4 = [&](int t, const char* buf) __attribute__((always_inline)) {
         // ph0: quadrant (A0, B0)
         read_a(buf, R_A0);
         read_b(buf, R_B0, bf0);
@@ -739,10 +810,126 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
         mfma16(acc[1][0], bf0);
         bar();
     };
+    // PRE: every phase first waits for the fragments the previous phase prefetched, then issues the
+    // reads of the NEXT phase's new fragments and runs its MFMAs under them (the LDS reads of a tile,
+    // 192 KB per CU, then overlap the matrix pipe instead of preceding it).  Register sets: af = A0
+    // rows, ag = A1 rows, bf1 = B1, bf0 / bg0 = B0 of even / odd tiles (ph3 reads the next tile's A0
+    // and B0 while its own A1 x B0 MFMAs still need the current B0).  Last reads of a half-tile:
+    // A0, B0 in ph3 of the previous tile, B1 in ph0, A1 in ph1, each waited for one phase later --
+    // so the restaging schedule (ph1: A0, ph2: B0, ph3: B1, next ph0: A1 of tile t+2) stays one phase
+    // and one barrier behind every read of the same half-tile.
+    auto tile4p = [&](int t, const char* buf, const char* nbuf, bf16x8_t (&b0)[2][2],
+                      bf16x8_t (&b0n)[2][2]) __attribute__((always_inline)) {
+        // ph0: (A0, B0); prefetch B1
+        if (t + 1 < nt) stage(t + 1, 1);
+        bar_wait_lgkm();
+        read_b(buf, R_B1, bf1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma16x(acc[0][0], af, b0);
+        bar();
+        // ph1: (A0, B1); prefetch A1
+        if (t + 2 < nt) stage(t + 2, 0);
+        bar_wait_lgkm();
+        read_a_to(buf, R_A1, ag);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma16x(acc[0][1], af, bf1);
+        bar();
+        // ph2: (A1, B1)
+        if (t + 2 < nt) stage(t + 2, 2);
+        bar_wait_lgkm();
+        mfma16x(acc[1][1], ag, bf1);
+        bar();
+        // ph3: (A1, B0); retire tile t+1, then prefetch its A0 and B0
+        if (t + 2 < nt) {
+            stage(t + 2, 3);
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else if (t + 1 < nt) {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        bar_wait_lgkm();
+        if (t + 1 < nt) {
+            read_a_to(nbuf, R_A0, af);
+            read_b(nbuf, R_B0, b0n);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma16x(acc[1][0], ag, b0);
+        bar();
+    };
+    // SCHED 2: ONE barrier per phase.  Phase p = [lgkmcnt(0): my phase p-1 reads landed; (ph3:
+    // vmcnt(6): tile t+1 landed); s_barrier; DMA; reads for phase p+1; 16 MFMAs].  Passing the
+    // barrier proves every wave's phase p-1 reads complete (so the half-tile they last touched may be
+    // restaged) and, in ph3, tile t+1 visible.  Last reads of tile t's half-tiles: A0, B0 in ph3 of
+    // tile t-1, B1 in ph0, A1 in ph1 -> tile t+2 restaged ph0: A0, ph1: B0, ph2: B1, ph3: A1 (each
+    // at least one phase, i.e. one barrier, after the last read).  The ph3 wait leaves the three
+    // half-tiles of t+2 issued in ph0-ph2 in flight.  The waves run a phase's MFMAs straight into
+    // the next phase's barrier: the pipe is not drained by a second barrier behind them.
+    auto tile4b = [&](int t, const char* buf, const char* nbuf, bf16x8_t (&b0)[2][2],
+                      bf16x8_t (&b0n)[2][2]) __attribute__((always_inline)) {
+#ifdef VS_G8_DIAG_NODMA     // timing diagnostics only (wrong results): no in-loop DMA / waits
+        const bool more = false;
+        if (nt < 0) t = 0;
+#else
+        const bool more = t + 2 < nt;
+#endif
+        // ph0: (A0, B0); restage A0 of t+2; prefetch B1
+        bar_wait_lgkm_pre();
+        if (more) stage(t + 2, 0);
+        read_b(buf, R_B1, bf1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma16x(acc[0][0], af, b0);
+        // ph1: (A0, B1); restage B0 of t+2; prefetch A1
+        bar_wait_lgkm_pre();
+        if (more) stage(t + 2, 2);
+        read_a_to(buf, R_A1, ag);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma16x(acc[0][1], af, bf1);
+        // ph2: (A1, B1); restage B1 of t+2
+        bar_wait_lgkm_pre();
+        if (more) stage(t + 2, 3);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma16x(acc[1][1], ag, bf1);
+        // ph3: (A1, B0); retire tile t+1, restage A1 of t+2, prefetch A0 / B0 of t+1
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);                       // lgkmcnt(0)
+        if (more)
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+#ifndef VS_G8_DIAG_NODMA
+        else if (t + 1 < nt)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+        bar_wait_lgkm_pre();
+        if (more) stage(t + 2, 1);
+        if (t + 1 < nt) {
+            read_a_to(nbuf, R_A0, af);
+            read_b(nbuf, R_B0, b0n);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma16x(acc[1][0], ag, b0);
+    };
+    if constexpr (SCHED == 2) {
+        read_a_to(smem, R_A0, af);
+        read_b(smem, R_B0, bf0);
 #pragma nounroll
-    for (int t = 0; t < nt; t += 2) {
-        tile4(t, smem);
-        if (t + 1 < nt) tile4(t + 1, smem + BUF8);
+        for (int t = 0; t < nt; t += 2) {
+            tile4b(t, smem, smem + BUF8, bf0, bg0);
+            if (t + 1 < nt) tile4b(t + 1, smem + BUF8, smem, bg0, bf0);
+        }
+    } else if constexpr (PRE) {
+        read_a_to(smem, R_A0, af);
+        read_b(smem, R_B0, bf0);
+#pragma nounroll
+        for (int t = 0; t < nt; t += 2) {
+            tile4p(t, smem, smem + BUF8, bf0, bg0);
+            if (t + 1 < nt) tile4p(t + 1, smem + BUF8, smem, bg0, bf0);
+        }
+    } else {
+#pragma nounroll
+        for (int t = 0; t < nt; t += 2) {
+            tile4(t, smem);
+            if (t + 1 < nt) tile4(t + 1, smem + BUF8);
+        }
     }
 
     // output: acc[qa][qb][i][j][e] = C[m][n], m = m0 + 128 qa + 64 wr + 16 i + (lane & 15),
@@ -774,6 +961,230 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
                     const int n = n0 + 128 * b + 32 * wc + 16 * j + 4 * (lane >> 4);
                     if (n >= N) continue;
                     epilogue_store(acc[a][b][i][j], m, n, C, ldc, ep);
+                }
+        }
+}
+
+
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+
+// ---------------------------------------------------------------------------------------------
+// gemm_fp8_tn_8p: the 8-phase skeleton of gemm_bf16_tn_8p for the fp8 path (config 5;
+// AutoWrappedLinear.fp8_linear, diffsynth/vram_management/layers.py:115-151):
+// C = epilogue(scale_a[m] * (A8 . W8^T)), e4m3 (OCP) operands, activations quantised per row by
+// vs_quant_fp8_rows, unscaled weights.  A K-tile is 128 fp8 = the same 128-B LDS rows, half-tiles,
+// DMA pieces and phase schedule as the bf16 kernel; per phase a wave runs 4 MX-rate
+// v_mfma_scale_f32_32x32x64_f8f6f4 (unit E8M0 scales; two 64-deep k-steps x two 32-row m-tiles
+// x one 32-column n-tile) = twice the bf16 FLOPs in the same MFMA cycles.  Fragment (32x32x64 map,
+// as the r2 kernel): lane l holds row l & 31, k = 32 (l >> 5) .. +31 of the k-step, i.e. 16-B chunks
+// 4s + 2(l >> 5) + {0, 1}; chunk swizzle c ^ ((row & 7) ^ ((row >> 3) & 1)) makes these reads
+// conflict-free (the bf16 kernel's c ^ (row & 7) would be 2-way here).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int q8_off(int row, int ch) {
+    return row * 128 + 16 * (ch ^ (row & 7) ^ ((row >> 3) & 1));
+}
+
+__global__ __launch_bounds__(512, 2) void gemm_fp8_tn_8p(
+    const uint8_t* __restrict__ A, long long lda, const float* __restrict__ scale_a, const uint8_t* __restrict__ W,
+    long long ldw, bf16_t* C, long long ldc, int M, int N, int K, Epi ep, int ntm, int ntn, int nmain, int ksplit,
+    int piece_k, float* __restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    int pid, piece = -1;
+    if ((int)blockIdx.x < nmain) {
+        pid = xcd_remap(blockIdx.x, nmain);
+    } else {
+        const int t = blockIdx.x - nmain;
+        pid = nmain + t / ksplit;
+        piece = t % ksplit;
+    }
+    int tm, tn;
+    tile_of(pid, ntm, ntn, tm, tn);
+    const int m0 = tm * T8, n0 = tn * T8;
+    const int kb = piece < 0 ? 0 : piece * piece_k;
+    const int Kp = piece < 0 ? K : min(K - kb, piece_k);
+    const int nt = Kp / 128;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 2, wc = wave & 3;
+
+    f32x16_t acc[2][2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[a][b][i][r] = 0.f;
+
+    // DMA: as gemm_bf16_tn_8p; piece j of a wave covers rows 16w + 8j + L/8, whose (row >> 3) & 1 = j
+    const int prow = 16 * wave + (lane >> 3);
+    auto rsrc = [](const void* base) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t ra = rsrc(A + (long long)m0 * lda + kb);
+    const __amdgpu_buffer_rsrc_t rw = rsrc(W + (long long)n0 * ldw + kb);
+    const unsigned pcol = 16u * ((lane & 7) ^ (lane >> 3));
+    const int alim = M - 1 - m0, wlim = N - 1 - n0;
+    // row offsets formed per stage from two opaque VGPRs (see gemm_bf16_tn_8p)
+    auto stage = [&](int t, int which) {
+        char* dst = smem + hoff(which, t & 1) + wave * 2048;
+        const bool isw = which >= 2;
+        const int h = which & 1;
+        const unsigned ko = (unsigned)t * 128u;
+        int pr = prow;
+        unsigned pc = pcol;
+        asm volatile("" : "+v"(pr), "+v"(pc));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int r = h * 128 + pr + 8 * j;
+            const unsigned pcj = pc ^ (16u * j);
+            const unsigned vo = isw ? (unsigned)min(r, wlim) * (unsigned)ldw + pcj : (unsigned)min(r, alim) * (unsigned)lda + pcj;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(isw ? rw : ra, (LDS_AS void*)(dst + j * 1024), 16, vo, ko, 0, 0);
+        }
+    };
+
+    const int frow = lane & 31, fh = lane >> 5;
+    i32x8_t af[2][2], ag[2][2], bf0[2], bg0[2], bf1[2];
+    // fragment bases per (buffer, k-step): q8_off(row0 + 32 i + frow, c) = q8_off(row0 + frow, c) + 4096 i,
+    // and the second 16-B chunk of a lane's 32 bytes sits at (address ^ 16) (bit 4 of the address =
+    // bit 0 of the swizzled chunk; every other term is a multiple of 128)
+    int abase[2], bbase[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        abase[s] = (int)(uintptr_t)smem + q8_off(wr * 64 + frow, 4 * s + 2 * fh);
+        bbase[s] = (int)(uintptr_t)smem + hoff(R_B0, 0) + q8_off(wc * 32 + frow, 4 * s + 2 * fh);
+        asm volatile("" : "+v"(abase[s]), "+v"(bbase[s]));
+    }
+    auto frag = [&](int base, int imm) {
+        int base2;      // (asm: formed where it is used, not hoisted into a register live across the loop)
+        asm volatile("v_xor_b32 %0, 16, %1" : "=v"(base2) : "v"(base));
+        const u32x4_t lo = *reinterpret_cast<const LDS_AS u32x4_t*>((const LDS_AS char*)(uintptr_t)(unsigned)(base + imm));
+        const u32x4_t hi = *reinterpret_cast<const LDS_AS u32x4_t*>((const LDS_AS char*)(uintptr_t)(unsigned)(base2 + imm));
+        return i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    };
+    auto read_a = [&](int b, int region, i32x8_t (&a)[2][2]) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) a[i][s] = frag(abase[s], hoff(region, b) + 4096 * i);
+    };
+    auto read_b = [&](int b, int region, i32x8_t (&bf)[2]) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) bf[s] = frag(bbase[s], hoff(region, b) - hoff(R_B0, 0));
+    };
+    auto mfma4 = [&](f32x16_t (&c)[2], const i32x8_t (&a)[2][2], const i32x8_t (&bf)[2]) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                c[i] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(bf[s], a[i][s], c[i], 0, 0, 0, 0x7f, 0, 0x7f);
+        // pin the cluster inside its phase: the IR passes may otherwise sink these register-only
+        // MFMAs past the phase's barrier (and keep every fragment set live across phases)
+        asm volatile("" : "+v"(c[0]), "+v"(c[1]));
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar_wait_lgkm = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_barrier" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0), visible to the compiler's wait-count pass
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
+    if (nt > 1) {
+        stage(1, 0); stage(1, 2); stage(1, 3);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();
+    // the phase schedule and fragment prefetch of gemm_bf16_tn_8p<PRE>: each phase waits for the
+    // fragments the previous one read, reads the next phase's new ones and runs its 4 MX MFMAs
+    auto tile4p = [&](int t, int b, i32x8_t (&b0)[2], i32x8_t (&b0n)[2]) __attribute__((always_inline)) {
+        if (t + 1 < nt) stage(t + 1, 1);
+        bar_wait_lgkm();
+        read_b(b, R_B1, bf1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma4(acc[0][0], af, b0);
+        bar();
+        if (t + 2 < nt) stage(t + 2, 0);
+        bar_wait_lgkm();
+        read_a(b, R_A1, ag);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma4(acc[0][1], af, bf1);
+        bar();
+        if (t + 2 < nt) stage(t + 2, 2);
+        bar_wait_lgkm();
+        mfma4(acc[1][1], ag, bf1);
+        bar();
+        if (t + 2 < nt) {
+            stage(t + 2, 3);
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else if (t + 1 < nt) {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        bar_wait_lgkm();
+        if (t + 1 < nt) {
+            read_a(b ^ 1, R_A0, af);
+            read_b(b ^ 1, R_B0, b0n);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma4(acc[1][0], ag, b0);
+        bar();
+    };
+    read_a(0, R_A0, af);
+    read_b(0, R_B0, bf0);
+#pragma nounroll
+    for (int t = 0; t < nt; t += 2) {
+        tile4p(t, 0, bf0, bg0);
+        if (t + 1 < nt) tile4p(t + 1, 1, bg0, bf0);
+    }
+
+    // acc[qa][qb][i][4g + e] = D[n][m]: m = m0 + 128 qa + 64 wr + 32 i + (lane & 31),
+    // n = n0 + 128 qb + 32 wc + 8 g + 4 (lane >> 5) + e
+    if (piece >= 0) {
+        float* pp = part + ((long long)(pid - nmain) * ksplit + piece) * T8 * T8;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        *reinterpret_cast<f32x4_t*>(pp + (128 * a + 64 * wr + 32 * i + frow) * T8 + 128 * b + 32 * wc +
+                                                    8 * g + 4 * fh) =
+                            f32x4_t{acc[a][b][i][4 * g], acc[a][b][i][4 * g + 1], acc[a][b][i][4 * g + 2],
+                                    acc[a][b][i][4 * g + 3]};
+        return;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int m = m0 + 128 * a + 64 * wr + 32 * i + frow;
+            if (m >= M) continue;
+            const float sa = scale_a[m];
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int n = n0 + 128 * b + 32 * wc + 8 * g + 4 * fh;
+                    if (n >= N) continue;
+                    epilogue_store(f32x4_t{acc[a][b][i][4 * g] * sa, acc[a][b][i][4 * g + 1] * sa,
+                                           acc[a][b][i][4 * g + 2] * sa, acc[a][b][i][4 * g + 3] * sa},
+                                   m, n, C, ldc, ep);
                 }
         }
 }
@@ -965,7 +1376,6 @@ __global__ __launch_bounds__(NTHR4, 1) void gemm_bf16_tn_w4(
 // MFMA cycles.  The product is formed transposed (D[n][m] = W8 . A8^T) so each lane owns 4
 // consecutive output columns per register group and the bf16 epilogue is reused unchanged.
 // ---------------------------------------------------------------------------------------------
-typedef int i32x8_t __attribute__((ext_vector_type(8)));
 
 template <bool BUF>
 __global__ __launch_bounds__(NTHR8, 2) void gemm_fp8_tn_256(
@@ -1300,9 +1710,10 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
     // acc + bias, one bf16 rounding) instead of bf16(acc + bias) + the gemm_epi_apply8 GELU pass: the
     // 14B FFN-up 6.18 -> 5.79 ms (profiles/r2/lt_gelu_ab.log).  It drops the reference's bf16 rounding
     // of the linear output before F.gelu: 35 % of outputs move by one bf16 ulp, closer to the exact
-    // GELU (0.8 % off its rounding vs 35 %).  VS_LT_GELU=0 keeps the two-pass rounding points.
+    // GELU (0.8 % off its rounding vs 35 %).  Off by default (r3): the default keeps the reference's
+    // rounding points (bf16 linear output, then the GELU pass); VS_LT_GELU=1 selects the fused epilogue.
     const char* lt_gelu = getenv("VS_LT_GELU");
-    if (k2 == 0 && epilogue == VS_EPI_GELU && !(lt_gelu && lt_gelu[0] == '0') && lt_route(m, n, k) &&
+    if (k2 == 0 && epilogue == VS_EPI_GELU && (lt_gelu && lt_gelu[0] == '1') && lt_route(m, n, k) &&
         vs_lt_gemm_bias_gelu(a, lda, w, ldw, c, ldc, m, n, k, ep.bias, (hipStream_t)stream) == VS_OK)
         return VS_OK;
     if (k2 == 0 && lt_route(m, n, k) &&
@@ -1337,14 +1748,17 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
         }
         static bool attr8 = false;
         if (!attr8) {
-            (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_8p<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      LDS8);
-            (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_8p<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      LDS8);
+            for (const void* f : {(const void*)gemm_bf16_tn_8p<false, 0>, (const void*)gemm_bf16_tn_8p<true, 0>,
+                                  (const void*)gemm_bf16_tn_8p<false, 1>, (const void*)gemm_bf16_tn_8p<false, 2>})
+                (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
             attr8 = true;
         }
-        const char* impl_env = getenv("VS_GEMM_IMPL");   // pp: the r2 ping-pong kernel (A/B only)
-        const bool pp = impl_env && impl_env[0] == 'p';
+        // VS_GEMM_IMPL (A/B only): pp = the r2 ping-pong kernel, 8p = the 8-phase kernel without the
+        // fragment prefetch; default: 8-phase with prefetch
+        const char* impl_env = getenv("VS_GEMM_IMPL");
+        const bool pp = impl_env && impl_env[0] == 'p' && impl_env[1] == 'p';
+        // 8p: reads at phase start; pre: fragment prefetch, two barriers per phase; default: 1b
+        const int sched = (impl_env && impl_env[0] == '8') ? 0 : (impl_env && impl_env[0] == 'p') ? 1 : 2;
         if (!pp) {
             KSplit sp = k2 ? KSplit{tm * tn, 0, 1, 0}
                            : plan_ksplit(tm * tn, k / 64, vs_cus_for_split("VS_GEMM_NO_SPLIT"), 64);
@@ -1353,8 +1767,11 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
                 part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
                 if (!part) sp = KSplit{tm * tn, 0, 1, 0};
             }
-            hipLaunchKernelGGL(k2 ? gemm_bf16_tn_8p<true> : gemm_bf16_tn_8p<false>,
-                               dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(512), LDS8, (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw, (bf16_t*)c, ldc, m,
+            // (the LoRA second phase needs a few more VGPRs than the prefetch leaves: no prefetch there)
+            auto kern = k2 ? gemm_bf16_tn_8p<true, 0>
+                           : sched == 2 ? gemm_bf16_tn_8p<false, 2>
+                                        : sched == 1 ? gemm_bf16_tn_8p<false, 1> : gemm_bf16_tn_8p<false, 0>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(512), LDS8, (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw, (bf16_t*)c, ldc, m,
                                n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2, k2, ep, tm, tn, sp.nmain,
                                sp.ksplit, sp.piece_k, part);
             VS_CHECK_LAUNCH();
@@ -1431,11 +1848,11 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
     // + the epilogue pass: 1.3-1.6x the fp8 MFMA kernel on every 14B block shape at SP=1 and SP=8
     // and bit-identical to it, epilogues included (profiles/r1/gemm_fp8_lt_r1j.log).
     // VS_FP8_BACKEND=vstyler forces the MFMA kernel, which also runs when no workspace is bound.
-    // GELU as in vs_gemm: hipBLASLt's fused GELU_BIAS epilogue unless VS_LT_GELU=0.
-    const char* fb = getenv("VS_FP8_BACKEND");
+    // GELU as in vs_gemm: hipBLASLt's fused GELU_BIAS epilogue only with VS_LT_GELU=1.
+    const char* fb = getenv("VS_FP8_BACKEND");      // lt | vstyler (8-phase MFMA kernel) | pp (r2 kernel, A/B)
     const char* lt_gelu = getenv("VS_LT_GELU");
-    const bool use_lt = !(fb && fb[0] == 'v');
-    if (use_lt && epilogue == VS_EPI_GELU && !(lt_gelu && lt_gelu[0] == '0') &&
+    const bool use_lt = !(fb && (fb[0] == 'v' || fb[0] == 'p'));
+    if (use_lt && epilogue == VS_EPI_GELU && (lt_gelu && lt_gelu[0] == '1') &&
         vs_lt_gemm_fp8(a8, lda, scale_a, w8, ldw, c, ldc, m, n, k, ep.bias, true, (hipStream_t)stream) == VS_OK)
         return VS_OK;
     if (use_lt &&
@@ -1444,6 +1861,31 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
         }))
         return VS_OK;
     const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
+    if (k % 128 == 0 && !(fb && fb[0] == 'p')) {
+        static bool attr8 = false;
+        if (!attr8) {
+            (void)hipFuncSetAttribute((const void*)gemm_fp8_tn_8p, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
+            attr8 = true;
+        }
+        KSplit sp = plan_ksplit(tm * tn, k / 128, vs_cus_for_split("VS_GEMM_NO_SPLIT"), 128);
+        float* part = nullptr;
+        if (sp.ntail) {
+            part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
+            if (!part) sp = KSplit{tm * tn, 0, 1, 0};
+        }
+        hipLaunchKernelGGL(gemm_fp8_tn_8p, dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(512), LDS8,
+                           (hipStream_t)stream, (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c,
+                           ldc, m, n, k, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part);
+        VS_CHECK_LAUNCH();
+        if (sp.ntail) {
+            const long long threads = (long long)sp.ntail * BT * (BT / 4);
+            hipLaunchKernelGGL(gemm_split_combine, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                               (hipStream_t)stream, part, (bf16_t*)c, ldc, m, n, ep, tm, tn, sp.nmain, sp.ntail,
+                               sp.ksplit, scale_a);
+            VS_CHECK_LAUNCH();
+        }
+        return VS_OK;
+    }
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)gemm_fp8_tn_256<true>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -212,8 +212,13 @@ class Workspace:
         t = self.bufs.get(name)
         if t is None or t.shape != shape or t.dtype != dtype:
             t = torch.empty(shape, device=self.device, dtype=dtype)
+            if _POISON:                 # debugging aid: NaN-fill so a read-before-write shows up
+                t.view(torch.uint8).fill_(0xFF)
             self.bufs[name] = t
         return t
+
+
+_POISON = os.environ.get("VSTYLER_WS_POISON", "0") == "1"
 
 
 class KernelTimer:
