@@ -385,7 +385,7 @@ def denoise(W, cfg, latents, context_pos, context_neg, vace_context=None, num_in
     sigmas, timesteps = set_timesteps(num_inference_steps, 1.0, sigma_shift)
     tp, tn = tea_caches if tea_caches is not None else (None, None)
     for i, ts in enumerate(timesteps):
-        t = ts.unsqueeze(0).to(BF16)                                 # :526
+        t = ts.unsqueeze(0).to(BF16).to(latents.device)              # :526
         vp = model_fn(W, cfg, latents, t, context_pos, vace_context, vace_scale, num_layers, tea_cache=tp)
         if cfg_scale != 1.0:
             vn = model_fn(W, cfg, latents, t, context_neg, vace_context, vace_scale, num_layers, tea_cache=tn)

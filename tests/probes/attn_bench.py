@@ -1,4 +1,6 @@
-"""Attention microbenchmark at the 14B 832x480x73 shapes (random data), + spot parity vs fp32."""
+"""Attention microbenchmark at the 14B 832x480x73 shapes (random data), + spot parity vs fp32.
+ATTN_AB="8,4": interleaved rounds of VS_ATTN_IMPL values in one process (8: the 8-wave kernel,
+4: attn_fwd_w4)."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "video-styler_amd"))
 import torch
@@ -12,7 +14,12 @@ v = torch.randn(B * S, D, device="cuda", generator=g).to(torch.bfloat16)
 o = torch.empty_like(q)
 kc = torch.randn(B * L, D, device="cuda", generator=g).to(torch.bfloat16)
 vc = torch.randn(B * L, D, device="cuda", generator=g).to(torch.bfloat16)
-for name, kk, vv, skv in (("self", k, v, S), ("cross", kc, vc, L)):
+impls = os.environ.get("ATTN_AB", "").split(",") if os.environ.get("ATTN_AB") else [None]
+cases = [(name, kk, vv, skv, impl) for _ in range(2 if impls[0] is not None else 1) for impl in impls
+         for name, kk, vv, skv in (("self", k, v, S), ("cross", kc, vc, L))]
+for name, kk, vv, skv, impl in cases:
+    if impl is not None:
+        os.environ["VS_ATTN_IMPL"] = impl
     fn = lambda: K.attention(q, kk, vv, o, H, B)
     fn(); torch.cuda.synchronize()
     ts = []
@@ -31,4 +38,4 @@ for name, kk, vv, skv in (("self", k, v, S), ("cross", kc, vc, L)):
         ref = torch.softmax(qs @ ks.t() / 128 ** 0.5, -1) @ vs
         got = o.view(B, S, H, 128)[1, rows, hh].float()
         worst = max(worst, (got - ref).abs().max().item())
-    print(f"{name}: {t:.3f} ms  {fl / t / 1e9:.1f} TF/s  spot max-abs {worst:.3e}", flush=True)
+    print(f"{name}{'' if impl is None else ' impl ' + impl}: {t:.3f} ms  {fl / t / 1e9:.1f} TF/s  spot max-abs {worst:.3e}", flush=True)

@@ -2,7 +2,9 @@
 product UlyssesGroup with its RCCL collectives replaced by same-size device copies (rank 0's
 data stands in for every peer, so the numbers are garbage; the work and the bytes moved per rank
 are the real ones).  Bounds the SP speedup the 8-GPU run can reach: t(SP=1) / t(rank, SP=P).
-  python tests/probes/sp_rank_compute.py [P ...]"""
+  python tests/probes/sp_rank_compute.py [P ...]
+SPC_SIZE=720p: BASELINE C4's 1280x720x121 (latent 31 x 90 x 160, S = 111 600) instead of 832x480x73;
+SPC_REPS: timed repetitions (default 3)."""
 import os, sys, time
 ROOT = os.path.join(os.path.dirname(__file__), "..", "..")
 sys.path.insert(0, os.path.join(ROOT, "video-styler_amd"))
@@ -29,7 +31,8 @@ class LocalUlysses(UlyssesGroup):
 
 dev = torch.device("cuda:0")
 m = MODELS["14B"]
-T, Hl, Wl = 19, 60, 104
+T, Hl, Wl = (31, 90, 160) if os.environ.get("SPC_SIZE") == "720p" else (19, 60, 104)
+REPS = int(os.environ.get("SPC_REPS", "3"))
 dit = WanModel(dim=m["dim"], in_dim=16, ffn_dim=m["ffn_dim"], out_dim=16, text_dim=4096, freq_dim=256, eps=1e-6,
                patch_size=(1, 2, 2), num_heads=m["num_heads"], num_layers=m["num_layers"], device=dev)
 vace = VaceWanModel(vace_layers=m["vace_layers"], dim=m["dim"], num_heads=m["num_heads"], ffn_dim=m["ffn_dim"],
@@ -73,7 +76,7 @@ for a in sys.argv[1:] or ["1", "8"]:
                                     use_unified_sequence_parallel=sp is not None, sp_group=sp)
     fn(); torch.cuda.synchronize()
     ts = []
-    for _ in range(3):
+    for _ in range(REPS):
         t0 = time.perf_counter(); fn(); torch.cuda.synchronize(); ts.append(time.perf_counter() - t0)
     label = f"CFG2 x SP={P} (world {2 * P})" if cfgp else f"SP={P} overlap={OVL}"
-    print(f"{label}: per-rank CFG step (eager) {1000 * min(ts):.1f} ms", flush=True)
+    print(f"{label} S={T * Hl * Wl // 4}: per-rank CFG step (eager) {1000 * min(ts):.1f} ms", flush=True)

@@ -108,3 +108,32 @@ def test_loader_normalizes_comfyui_kijai_layouts():
     assert hash_state_dict_keys(n) == hash_state_dict_keys(plain)
     assert torch.equal(n["blocks.0.self_attn.q.weight"].float(), w8.float() * 0.5)
     assert set(normalize_keys({"diffusion_model.x.weight": torch.zeros(1)})) == {"x.weight"}
+
+
+def test_loader_configs_from_shapes_and_shards(tmp_path):
+    """loader.dit/vace_config_from_shapes (the extension for key hashes outside the reference's
+    table) reproduce the published configs from the 1.3B / 14B layouts, and a tiny checkpoint split
+    over two safetensors shards reads back as one state dict with the tiny config."""
+    from safetensors.torch import save_file
+    from vstyler.loader import (WAN_DIT_CONFIGS, dit_config_from_shapes, load_state_dict,
+                                vace_config_from_shapes)
+
+    def meta(shapes):
+        return {k: torch.empty(s, device="meta") for k, s in shapes.items()}
+    for name in ("1.3B", "14B", "tiny"):
+        cfg = O.WAN_CONFIGS[name]
+        d = dit_config_from_shapes(meta(O.dit_param_shapes(cfg)))
+        for k in ("dim", "ffn_dim", "num_heads", "num_layers", "in_dim", "out_dim", "text_dim", "freq_dim"):
+            assert d[k] == cfg[k], (name, k)
+        v = vace_config_from_shapes(meta(O.vace_param_shapes(cfg)), cfg["num_layers"])
+        assert v["vace_layers"] == tuple(cfg["vace_layers"]) and v["dim"] == cfg["dim"], name
+        assert v["ffn_dim"] == cfg["ffn_dim"] and v["vace_in_dim"] == cfg["vace_in_dim"], name
+    assert dit_config_from_shapes({"head.head.weight": torch.zeros(64, 8)}) is None
+    assert len(WAN_DIT_CONFIGS) == 2
+    W = O.random_weights(O.WAN_CONFIGS["tiny"], seed=3)
+    keys = sorted(W)
+    save_file({k: W[k] for k in keys[0::2]}, str(tmp_path / "a-00001-of-00002.safetensors"))
+    save_file({k: W[k] for k in keys[1::2]}, str(tmp_path / "a-00002-of-00002.safetensors"))
+    sd = load_state_dict([str(tmp_path / "a-00001-of-00002.safetensors"),
+                          str(tmp_path / "a-00002-of-00002.safetensors")])
+    assert set(sd) == set(W) and all(torch.equal(sd[k], W[k]) for k in W)

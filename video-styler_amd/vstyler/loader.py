@@ -84,22 +84,67 @@ def normalize_keys(state_dict):
     return sd
 
 
+def _n_blocks(sd, prefix):
+    ids = {int(k.split(".")[1]) for k in sd if k.startswith(prefix + ".") and k.split(".")[1].isdigit()}
+    return len(ids)
+
+
+def dit_config_from_shapes(sd):
+    """Extension for checkpoints whose key hash the reference's table does not list (fine-tunes of
+    another width, the tiny test checkpoints): the WanModel config read off the tensor shapes of the
+    Wan key layout (wan_video_dit.py:272-308; head_dim 128 as every Wan2.1 model, patch 1x2x2).
+    None when the layout is not a Wan DiT."""
+    need = ("patch_embedding.weight", "blocks.0.ffn.0.weight", "text_embedding.0.weight",
+            "time_embedding.0.weight", "head.head.weight")
+    if not all(k in sd for k in need):
+        return None
+    pe = sd["patch_embedding.weight"]
+    if tuple(pe.shape[2:]) != (1, 2, 2):
+        return None
+    dim = pe.shape[0]
+    return dict(WAN_COMMON, dim=dim, in_dim=pe.shape[1], ffn_dim=sd["blocks.0.ffn.0.weight"].shape[0],
+                num_heads=dim // 128, num_layers=_n_blocks(sd, "blocks"),
+                text_dim=sd["text_embedding.0.weight"].shape[1], freq_dim=sd["time_embedding.0.weight"].shape[1],
+                out_dim=sd["head.head.weight"].shape[0] // 4)
+
+
+def vace_config_from_shapes(sd, num_layers):
+    """The VaceWanModel config of a VACE key set outside the hash table: widths off the shapes, the
+    n VACE blocks spread evenly over the main blocks (range(0, L, L // n): (0,2,..,28) for 1.3B,
+    (0,5,..,35) for 14B, the two published layouts, wan_video_vace.py:98-113)."""
+    pe = sd["vace_patch_embedding.weight"]
+    dim, n = pe.shape[0], _n_blocks(sd, "vace_blocks")
+    step = max(1, num_layers // n) if num_layers else 2
+    return dict(vace_layers=tuple(range(0, n * step, step)), vace_in_dim=pe.shape[1], patch_size=(1, 2, 2),
+                dim=dim, num_heads=dim // 128, ffn_dim=sd["vace_blocks.0.ffn.0.weight"].shape[0], eps=1e-6)
+
+
 def build_dit(state_dict, device):
     sd = {k: v for k, v in state_dict.items() if not k.startswith("vace")}
     h = hash_state_dict_keys(sd)
-    if h not in WAN_DIT_CONFIGS:
-        return None
-    cfg = dict(WAN_COMMON, **WAN_DIT_CONFIGS[h])
+    if h in WAN_DIT_CONFIGS:
+        cfg = dict(WAN_COMMON, **WAN_DIT_CONFIGS[h])
+    else:
+        cfg = dit_config_from_shapes(sd)
+        if cfg is None:
+            return None
     model = WanModel(device=device, **cfg)
     model.load_state_dict({k: v.to(torch.bfloat16) for k, v in sd.items()}, strict=True)
     return model
 
 
-def build_vace(state_dict, device):
+def build_vace(state_dict, device, num_layers=None):
     sd = {k: v for k, v in state_dict.items() if k.startswith("vace")}
     if not sd:
         return None
-    cfg = VACE_14B if hash_state_dict_keys(sd) == VACE_14B_HASH else VACE_DEFAULT
+    h = hash_state_dict_keys(sd)
+    if h == VACE_14B_HASH:
+        cfg = VACE_14B
+    elif sd["vace_patch_embedding.weight"].shape[0] == VACE_DEFAULT["dim"] and \
+            _n_blocks(sd, "vace_blocks") == len(VACE_DEFAULT["vace_layers"]):
+        cfg = VACE_DEFAULT
+    else:
+        cfg = vace_config_from_shapes(sd, num_layers)
     model = VaceWanModel(device=device, **cfg)
     model.load_state_dict({k: v.to(torch.bfloat16) for k, v in sd.items()}, strict=True)
     return model
@@ -152,7 +197,7 @@ def load_models(paths, device="cuda"):
         dit = build_dit(sd, device)
         if dit is not None:
             out["wan_video_dit"] = dit
-            vace = build_vace(sd, device)
+            vace = build_vace(sd, device, num_layers=len(dit.blocks))
             if vace is not None:
                 out["wan_video_vace"] = vace
             continue
