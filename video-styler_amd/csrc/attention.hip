@@ -22,14 +22,13 @@
 //    inside the phase that completes it -- no per-item prologue or drain (worth most on the
 //    cross-attention, whose 512 keys are only 8 tiles per item).
 #include "common.h"
+#include "attention.h"
 #include <algorithm>
 #include <set>
 
 namespace {
+using namespace vs_attn;
 
-constexpr int HD = 128;          // head dim
-constexpr int BQ = 256;          // query rows per workgroup
-constexpr int BKV = 64;          // keys per tile
 constexpr int NTHR = 512;
 constexpr int KROW = 272;        // LDS row pitch of the K tile (256 B + 16): row reads conflict-free
 constexpr int VROW = 320;        // LDS row pitch of the V tile (256 B + 64): transposed reads conflict-free
@@ -37,7 +36,6 @@ constexpr int KT = BKV * KROW;   // 17408
 constexpr int VT = BKV * VROW;   // 20480
 constexpr int LDS_BYTES = 2 * (KT + VT);   // K ring 2 x 17408 + V ring 2 x 20480
 constexpr int QPRE_BYTES = 9 * NTHR * 16;  // persistent mode: next item's Q / previous item's O, lane-private
-constexpr int PROW = HD + 4;     // split-tail partial row: 128 fp32 O, m, l, 2 pad (16-B aligned)
 constexpr int PERSIST_MIN_TILES = 8;
 // items of fewer key tiles prefetch Q / drain O inside the tile loop.  0: never -- measured on the
 // 14B shapes the synchronous item switch wins for long items (self-attention 31.0 -> 29.1 ms) and
@@ -47,13 +45,7 @@ constexpr int PF_MAX_TILES = 0;
 #define VS_ATTN_MFMA16_DEFAULT true
 #endif       // the Q prefetch spreads its 8 chunks over the first 8 tiles
 
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
-    // raw buffer descriptor; out-of-range loads return 0 (rows past Skv, masked anyway)
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
-}
 
 // ---------------------------------------------------------------------------------------------
 // Two phases per 64-key tile, the two wave halves one barrier apart, one S tile live:
@@ -92,8 +84,6 @@ constexpr float SUM_MIN = 0x1p-60f;
 // and recomputed by the checked kernel (the redo launch), so the result is either the optimistic
 // one -- which sums the P actually multiplied with V -- or bit for bit the checked one.  With
 // l <= 2^64 the fp32 O accumulators stay finite for |v| < 2^64.
-constexpr float NC_LMIN = 0x1p-64f;
-constexpr float NC_LMAX = 0x1p64f;
 
 // v_mfma_f32_32x32x16_bf16.  VS_ATTN_DIAG_MFMA16 (timing diagnostic only, wrong results): the same
 // FLOPs as two v_mfma_f32_16x16x32_bf16 on the same operands, to measure the clock / issue effect
@@ -160,30 +150,6 @@ constexpr int STAMP_LDS = 8 * 4 * 32 * 8;
 #define ATTN_STAMP(slot) do {} while (0)
 #endif
 
-// Kernel arguments.  The fields an item switch needs (bases, batch strides, nqb, H) are read
-// through a volatile view of the argument block at each switch, so they do not stay live in SGPRs
-// across the tile loop (they pushed it past the SGPR file).
-struct AttnArgs {
-    const bf16_t *Q, *K, *V;
-    bf16_t* O;
-    long long bsq, bsk, bsv, bso;
-    long long ldq, ldk, ldv, ldo;
-    float* part;
-    int* flags;      // item-flag workspace (layout at NcWs): written by the NC kernel / the combine,
-                     // consumed and cleared by the redo launch
-    float c;
-    int Sq, Skv, H, nqb, nmain, npers, nsplit, piece_tiles;
-    int nc_cap;      // items the flag workspace holds (its list and its flags)
-};
-
-// Item-flag workspace (kind 4, ints; count, done and flags zero between launches): [0] count of
-// listed items, [1] redo blocks done reading the count, [2, 2 + cap) one flag per item,
-// [2 + cap, 2 + 2 cap) the list of flagged items (an item is listed once: the first flagger's
-// atomicExch sees 0).  cap follows from the bound size, so the regions never move.
-__device__ __forceinline__ void nc_list_item(int* ws, int cap, int gi) {
-    if (atomicExch(ws + 2 + gi, 1) == 0) ws[2 + cap + atomicAdd(ws, 1)] = gi;
-}
-constexpr int MODE_CHK = 0, MODE_NC = 1, MODE_REDO = 2;
 
 template <bool REBASE, bool M16, bool PF, int MODE>
 __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
@@ -1056,7 +1022,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
 __global__ __launch_bounds__(256) void attn_combine(const float* __restrict__ part, bf16_t* __restrict__ O,
                                                     int ntail, int nmain, int nsplit, int Sq, int H, int nqb,
                                                     long long ldo, long long bso, int* __restrict__ flags,
-                                                    int nc_cap) {
+                                                    int nc_cap, float lmin) {
     const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
     const int c4 = (int)(idx & 31);
     const long long rowid = idx >> 5;              // item * BQ + row
@@ -1078,7 +1044,7 @@ __global__ __launch_bounds__(256) void attn_combine(const float* __restrict__ pa
         acc += w * *reinterpret_cast<const f32x4_t*>(pj + 4 * c4);
     }
     // NC pieces (all m_j = 0): a row sum outside [NC_LMIN, NC_LMAX] sends the item to the redo launch
-    if (flags && !(lsum >= NC_LMIN && lsum <= NC_LMAX)) nc_list_item(flags, nc_cap, g);
+    if (flags && !(lsum >= lmin && lsum <= NC_LMAX)) nc_list_item(flags, nc_cap, g);
     const float inv = 1.f / lsum;
     bf16_t* op = O + (long long)b * bso + (long long)q * ldo + h * HD + 4 * c4;
     const unsigned lo = pack2(acc[0] * inv, acc[1] * inv), hi = pack2(acc[2] * inv, acc[3] * inv);
@@ -1225,11 +1191,21 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
         hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(NTHR), lds, (hipStream_t)stream, a);
         return hipGetLastError() == hipSuccess;
     };
-    if (!launch(pick(flags ? MODE_NC : MODE_CHK, pf), grid, args)) return VS_E_LAUNCH;
+    // the NC pass: attn_fwd_w4 (4 waves x 64 rows); VS_ATTN_IMPL=8 / =4 force the 8-wave / 4-wave kernel
+    // (items of fewer than 16 key tiles -- the 512-key cross-attention -- stay on the 8-wave kernel:
+    // the 4-wave pipeline's per-item fill and drain are a large share of an 8-tile item)
+    const char* impl_env = getenv("VS_ATTN_IMPL");
+    const bool w4 = flags && (impl_env ? impl_env[0] == '4' : nkv >= 16);
+    if (w4) {
+        if (attn_w4_launch(args, rebase, (unsigned)grid, (hipStream_t)stream) != hipSuccess) return VS_E_LAUNCH;
+    } else if (!launch(pick(flags ? MODE_NC : MODE_CHK, pf), grid, args)) {
+        return VS_E_LAUNCH;
+    }
     if (sp.ntail) {
         const long long threads = (long long)sp.ntail * BQ * 32;
         hipLaunchKernelGGL(attn_combine, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                           part, (bf16_t*)o, sp.ntail, sp.nmain, sp.nsplit, sq, heads, nqb, ldo, bso, flags, nc_cap);
+                           part, (bf16_t*)o, sp.ntail, sp.nmain, sp.nsplit, sq, heads, nqb, ldo, bso, flags, nc_cap,
+                           w4 ? W4_LMIN : NC_LMIN);
         VS_CHECK_LAUNCH();
     }
     if (flags) {

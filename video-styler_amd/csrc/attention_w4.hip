@@ -1,0 +1,627 @@
+// attn_fwd_w4: the 4-wave x 64-row flash-attention forward (NC pass), gfx950.  Built with its own
+// code-generation flags (Makefile): the MFMA results in VGPRs (-amdgpu-mfma-vgpr-form), so the
+// softmax reads S without AGPR copies.
+#include <cstdlib>
+#include <mutex>
+#include <set>
+#include <type_traits>
+
+#include "attention.h"
+
+namespace vs_attn {
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// attn_fwd_w4 (r3): one wave per SIMD, 64 query rows per wave.  A workgroup is 4 waves = the same
+// 256-row item of one (batch, head) as attn_fwd_d128, so the item list, the persistent grid, the
+// split-tail pieces, the combine and the NC redo launch are shared with it.  What changes is the
+// per-wave tile: every K / V^T fragment read from LDS feeds TWO 32-row MFMA blocks, which halves
+// the LDS read traffic per FLOP of the 8-wave kernel (8 waves x 32 rows all re-reading the same
+// fragments: SQ_WAIT_INST_LDS 15.6 %, profiles/r2/pmc_attn_ilp), and the matrix pipe of a SIMD is
+// fed by one instruction stream with the softmax interleaved into its MFMA gaps (MI355X_MICROARCH
+// 'one wave per SIMD': <= 5 single-issue fillers per v_mfma_f32_32x32x16_bf16 gap hide).
+//
+// Per 64-key tile T and wave (v_mfma_f32_32x32x16_bf16, the swapped products of the M32 layout):
+//   QK(T):   S^T[kb][rb] = K(T)[32kb..] Q[32rb..]^T        16 K fragments -> 32 MFMAs
+//   softmax: p = exp2(S) (Q pre-scaled by log2(e)/sqrt(d); optimistic, no reference max -- the NC
+//            rule of attn_fwd_d128), row sums in fp32, P packed to bf16 as the PV B operands
+//   PV(T-1): O^T[rb][dt] += V(T-1)^T[32dt..] P(T-1)[rb]     16 V^T fragments (32 tr reads) -> 32 MFMAs
+// all in one basic block, so the machine scheduler spreads the softmax of tile T over the MFMAs of
+// QK(T) and PV(T-1).  O^T (8 x 16 fp32 per lane) lives in AGPRs (512-register wave).
+//
+// LDS: 4 slots x (K 16 KB | V 16 KB), filled by LDS-DMA (buffer_load ... lds, 1 KB = 4 rows per
+// wave-instruction, 8 per wave per tile) two tiles ahead; unpadded 256-B rows with the 16-B chunk
+// swizzled on the SOURCE address: K chunk c of row R at c ^ (R & 15) (conflict-free 32-row
+// ds_read_b128), V at c ^ 4 (R & 3) (the 4 rows x 64 B of a ds_read_b64_tr_b16 half-wave in 4
+// distinct bank quarters).  One s_barrier per tile: at the top of iteration T each wave retires its
+// own DMA of tile T (counted vmcnt, tile T+1 stays in flight), the barrier makes every wave's part
+// visible and proves every wave finished iteration T-1 -- the last reader of the slot tile T+2 is
+// then staged into (QK(T-2) in iteration T-2, PV(T-2) in iteration T-1).
+//
+// Key masking without a branch: rows past Skv are outside the buffer range and load as 0, so a
+// padded key scores exactly 0, contributes P = exp2(0) = 1 against a zero V row (O unchanged) and
+// exactly 1 to every row sum; the item's (nkv * 64 - Skv) padded keys are subtracted from l at the
+// end.  That subtraction cancels when the true l is tiny, so an item with a row sum below
+// W4_LMIN (2^-4, a row whose scores all lie below -4 in the exp2 domain) goes to the redo launch
+// with the overflow / underflow cases of the NC rule.
+constexpr int W4_THR = 256;
+constexpr int W4_TILE = BKV * HD * 2;      // 16 KB: one K or V tile
+constexpr int W4_SLOT = 2 * W4_TILE;
+constexpr int W4_LDS = 4 * W4_SLOT;        // 128 KB
+
+template <bool REBASE, bool PIPE>
+__global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    typedef const volatile AttnArgs __attribute__((address_space(4))) ColdArgs;
+    ColdArgs* cold = (ColdArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    const int Sq = args.Sq, Skv_all = args.Skv, nmain = args.nmain, npers = args.npers;
+    const int nsplit = args.nsplit, piece_tiles = args.piece_tiles;
+    const long long ldq = args.ldq, ldk = args.ldk, ldv = args.ldv, ldo = args.ldo;
+    const float c = args.c;
+
+    // item list: identical to attn_fwd_d128 (persistent blocks stride over XCD-contiguous ranges,
+    // the blocks after npers run the split-tail pieces)
+    int piece = -1, kv_begin = 0, Skv = Skv_all;
+    int g0, gstride, n_items;
+    if ((int)blockIdx.x < npers) {
+        const int x = blockIdx.x & 7, lb = blockIdx.x >> 3;
+        const int qx = nmain >> 3, rx = nmain & 7, qbk = npers >> 3, rbk = npers & 7;
+        const int cs = x < rx ? x * (qx + 1) : rx * (qx + 1) + (x - rx) * qx;
+        const int csz = qx + (x < rx ? 1 : 0);
+        gstride = qbk + (x < rbk ? 1 : 0);
+        g0 = cs + lb;
+        n_items = lb < csz ? (csz - lb + gstride - 1) / gstride : 0;
+    } else {
+        const int t = blockIdx.x - npers;
+        g0 = nmain + t / nsplit;
+        gstride = 0;
+        n_items = 1;
+        piece = t % nsplit;
+        kv_begin = piece * piece_tiles * BKV;
+        Skv = min(Skv_all - kv_begin, piece_tiles * BKV);
+    }
+    if (n_items == 0) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, hh = lane >> 5;
+
+    auto item_bh = [&](int j, int& qrow0) {
+        const int nqb = cold->nqb;
+        const int g = g0 + j * gstride;
+        qrow0 = (g % nqb) * BQ;
+        return g / nqb;
+    };
+    auto q_base = [&](int bh) { const int H = cold->H; return cold->Q + (long long)(bh / H) * cold->bsq + (bh % H) * HD; };
+    auto k_base = [&](int bh) {
+        const int H = cold->H;
+        return cold->K + (long long)(bh / H) * cold->bsk + (long long)kv_begin * ldk + (bh % H) * HD;
+    };
+    auto v_base = [&](int bh) {
+        const int H = cold->H;
+        return cold->V + (long long)(bh / H) * cold->bsv + (long long)kv_begin * ldv + (bh % H) * HD;
+    };
+    auto o_base = [&](int bh) { const int H = cold->H; return cold->O + (long long)(bh / H) * cold->bso + (bh % H) * HD; };
+
+    const int nkv = (Skv + BKV - 1) / BKV;
+    const int Ttot = n_items * nkv;
+    const float npad = (float)(nkv * BKV - Skv);
+
+    // ---- LDS-DMA loader: tile T of the flattened sequence into slot T & 3, two tiles ahead of QK.
+    // Wave w fills rows 16w .. 16w+15 of both tiles, 4 rows per instruction; lane L lands in chunk
+    // L & 15 of row 16w + 4i + (L >> 4) and fetches the logical chunk the swizzle puts there.
+    const int ldk32 = (int)ldk, ldv32 = (int)ldv;       // host: 64 * ld * 2 < 2^31
+    unsigned kvo[4], vvo[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int R = 16 * wave + 4 * i + (lane >> 4), p = lane & 15;
+        kvo[i] = (unsigned)(R * ldk32 * 2 + ((p ^ (R & 15)) << 4));
+        vvo[i] = (unsigned)(R * ldv32 * 2 + ((p ^ ((R & 3) << 2)) << 4));
+    }
+    // The DMA is issued from inline asm: the compiler, which sees an LDS-DMA as a write to all of
+    // LDS, would otherwise put vmcnt(0) before the first fragment read of every iteration and drain
+    // the two-tile lead.  Ordering is the protocol above (counted vmcnt + s_barrier); the compiler's
+    // own vmcnt waits (Q loads) only grow more conservative with the uncounted DMA.
+    auto rsrc4 = [&](const bf16_t* base, unsigned bytes) {
+        const unsigned long long a = (unsigned long long)(uintptr_t)base;
+        return i32x4_t{(int)(unsigned)a, (int)((unsigned)(a >> 32) & 0xffffu), (int)bytes, 0x00020000};
+    };
+    auto slab_rsrc = [&](const bf16_t* base, int ld) {
+        return rsrc4(base, REBASE ? 0u : (unsigned)((Skv - 1) * ld * 2 + HD * 2));
+    };
+    auto dma16 = [](unsigned lds, unsigned voff, i32x4_t rs, int soff) __attribute__((always_inline)) {
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :: "s"(lds), "v"(voff), "s"(rs), "s"(soff) : "m0");
+    };
+    int lj = 0, li = 0;
+    int qrow_unused;
+    const bf16_t* Kl = k_base(item_bh(0, qrow_unused));
+    const bf16_t* Vl = v_base(item_bh(0, qrow_unused));
+    i32x4_t krs = slab_rsrc(Kl, ldk32), vrs = slab_rsrc(Vl, ldv32);
+    const unsigned lds0 = (unsigned)(uintptr_t)smem + wave * 16 * 256;
+    // stage(T) = stage_piece(T, 0..7) (K rows, then V rows, 4 rows per piece) + stage_next()
+    struct StageCtx { unsigned kdst, vdst; i32x4_t kr, vr; int ks, vs; } sc;
+    auto stage_begin = [&](int T) __attribute__((always_inline)) {
+        sc.kdst = lds0 + (T & 3) * W4_SLOT;
+        sc.vdst = sc.kdst + W4_TILE;
+        const int kv0 = li * BKV;
+        sc.kr = krs;
+        sc.vr = vrs;
+        sc.ks = kv0 * ldk32 * 2;
+        sc.vs = kv0 * ldv32 * 2;
+        if constexpr (REBASE) {
+            const int rows = min(BKV, Skv - kv0);
+            sc.kr = rsrc4(Kl + (long long)kv0 * ldk, (unsigned)((rows - 1) * ldk32 * 2 + HD * 2));
+            sc.vr = rsrc4(Vl + (long long)kv0 * ldv, (unsigned)((rows - 1) * ldv32 * 2 + HD * 2));
+            sc.ks = 0;
+            sc.vs = 0;
+        }
+    };
+    auto stage_piece = [&](int i) __attribute__((always_inline)) {
+        if (i < 4)
+            dma16(sc.kdst + i * 1024, kvo[i], sc.kr, sc.ks);
+        else
+            dma16(sc.vdst + (i - 4) * 1024, vvo[i - 4], sc.vr, sc.vs);
+    };
+    auto stage_next = [&]() __attribute__((always_inline)) {
+        if (++li == nkv) {
+            li = 0;
+            if (++lj < n_items) {
+                const int bh = item_bh(lj, qrow_unused);
+                Kl = k_base(bh);
+                Vl = v_base(bh);
+                krs = slab_rsrc(Kl, ldk32);
+                vrs = slab_rsrc(Vl, ldv32);
+            }
+        }
+    };
+    auto stage = [&](int T) __attribute__((always_inline)) {
+        stage_begin(T);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) stage_piece(i);
+        stage_next();
+    };
+
+    // ---- Q fragments (B operand of S^T = K Q^T), pre-scaled by c: qf[rb][j] = row q0 + 32rb + r,
+    // columns 16j + 8hh .. +7 (rows past Sq read row Sq - 1; their outputs are dropped)
+    bf16x8_t qf[2][8];
+    auto load_q = [&](const bf16_t* qb0, int q0v) __attribute__((always_inline)) {
+        bf16x8_t raw[2][8];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+            const int qrow = min(q0v + 32 * rb + r, Sq - 1);
+            const bf16_t* src = qb0 + (long long)qrow * ldq + 8 * hh;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) raw[rb][j] = *reinterpret_cast<const bf16x8_t*>(src + 16 * j);
+        }
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) qf[rb][j][e] = (__bf16)((float)raw[rb][j][e] * c);
+                asm volatile("" : "+a"(qf[rb][j]));    // the B operands live in AGPRs
+            }
+    };
+
+    // ---- fragment addresses (bytes from the slot base).  K (kb, j): row 32kb + r, chunk
+    // (2j + hh) ^ (r & 15).  V^T (ks, dt): the M32 transposed-read pattern of attn_fwd_d128 (rows
+    // 16ks + 4(g4 >> 1) + q4 and +8, bytes 64dt + 32(g4 & 1) + 8p4) through the V swizzle, which
+    // turns the 64-B block dt into dt ^ q4 (rows = q4 mod 4)
+    int koff[8], voff[4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        koff[j] = r * 256 + (((2 * j + hh) ^ (r & 15)) << 4);
+        asm volatile("" : "+v"(koff[j]));
+    }
+    {
+        const int g4 = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            voff[dt] = W4_TILE + (4 * (g4 >> 1) + q4) * 256 + ((dt ^ q4) << 6) + 32 * (g4 & 1) + 8 * p4;
+            asm volatile("" : "+v"(voff[dt]));
+        }
+    }
+    const unsigned smem_base = (unsigned)(uintptr_t)smem;
+    auto lds16 = [&](unsigned addr) {
+        return *reinterpret_cast<const LDS_AS bf16x8_t*>((const LDS_AS char*)(uintptr_t)addr);
+    };
+    auto tr8 = [&](unsigned addr) {
+        return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_t*)(uintptr_t)addr);
+    };
+
+    f32x16_t o[2][4];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[rb][dt][i] = 0.f;
+    float lsum[2] = {0.f, 0.f};
+    f32x16_t zero;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) zero[i] = 0.f;
+
+    // QK(T) + softmax -> pk (P(T) as PV B operands: pk[rb][ks] = keys 16ks.. of rows 32rb + r, the
+    // M32 packing), rs (the tile's row-sum partials)
+    auto qk_softmax = [&](int T, u32x4_t (&pk)[2][4], float (&rs)[2]) __attribute__((always_inline)) {
+        const unsigned kb0 = smem_base + (T & 3) * W4_SLOT;
+        f32x16_t s[2][2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const bf16x8_t kf = lds16(kb0 + koff[j] + kb * 32 * 256);
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb)
+                    s[kb][rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[rb][j], j == 0 ? zero : s[kb][rb], 0, 0, 0);
+            }
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+            float acc = 0.f;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int i0 = 4 * q;
+                    const float p0 = __builtin_amdgcn_exp2f(s[kb][rb][i0]);
+                    const float p1 = __builtin_amdgcn_exp2f(s[kb][rb][i0 + 1]);
+                    const float p2 = __builtin_amdgcn_exp2f(s[kb][rb][i0 + 2]);
+                    const float p3 = __builtin_amdgcn_exp2f(s[kb][rb][i0 + 3]);
+                    acc += (p0 + p1) + (p2 + p3);
+                    const bf16x2_t w0 = {(__bf16)p0, (__bf16)p1}, w1 = {(__bf16)p2, (__bf16)p3};
+                    const int ks = 2 * kb + (q >> 1), jj = 2 * (q & 1);
+                    pk[rb][ks][jj] = __builtin_bit_cast(unsigned, w0);
+                    pk[rb][ks][jj + 1] = __builtin_bit_cast(unsigned, w1);
+                }
+            rs[rb] = acc;
+        }
+    };
+    // PV(T) with P(T) = pk
+    auto pv = [&](int T, const u32x4_t (&pk)[2][4]) __attribute__((always_inline)) {
+        const unsigned vb0 = smem_base + (T & 3) * W4_SLOT;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const unsigned a0 = vb0 + voff[dt] + ks * 16 * 256;
+                const i16x4_t v0 = tr8(a0), v1 = tr8(a0 + 8 * 256);
+                const bf16x8_t vf = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, v0),
+                                                            __builtin_bit_cast(bf16x4_t, v1), 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb)
+                    o[rb][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, __builtin_bit_cast(bf16x8_t, pk[rb][ks]),
+                                                                         o[rb][dt], 0, 0, 0);
+            }
+    };
+
+    // ---- items run one after the other (the K/V DMA pipeline runs on across item boundaries);
+    // within an item the tile loop is unrolled by two over the two P buffers, and its body --
+    // barrier, QK(T) + softmax, PV(T - 1), the DMA of tile T + 2 -- has no branch before the DMA
+    // cursor's item switch at its end, so the scheduler sees QK, softmax and PV as one region
+    // finished item: row sums (both lane halves, padded keys removed), NC flag, normalised store
+    // or (split-tail piece) the fp32 partial with m = 0
+    auto finish = [&](bf16_t* ob, int qrow0, int gi) __attribute__((always_inline)) {
+        float lt[2];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) lt[rb] = lsum[rb] + __shfl_xor(lsum[rb], 32) - npad;
+        if (piece >= 0) {
+            float* pp = args.part + ((long long)(gi - nmain) * nsplit + piece) * BQ * PROW + wave * 64 * PROW;
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+                float* pr = pp + (32 * rb + r) * PROW;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int gi4 = 0; gi4 < 4; ++gi4)
+                        *reinterpret_cast<f32x4_t*>(pr + 32 * dt + 8 * gi4 + 4 * hh) =
+                            f32x4_t{o[rb][dt][4 * gi4], o[rb][dt][4 * gi4 + 1], o[rb][dt][4 * gi4 + 2],
+                                    o[rb][dt][4 * gi4 + 3]};
+                if (hh == 0) *reinterpret_cast<f32x2_t*>(pr + HD) = f32x2_t{0.f, lt[rb]};
+            }
+            return;
+        }
+        const bool ok = lt[0] >= W4_LMIN && lt[0] <= NC_LMAX && lt[1] >= W4_LMIN && lt[1] <= NC_LMAX;
+        if (__any(!ok) && lane == 0) nc_list_item(cold->flags, cold->nc_cap, gi);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+            const float inv = 1.f / lt[rb];
+            const int row = qrow0 + 32 * rb + r;
+            bf16_t* op = ob + (long long)row * ldo + 8 * hh;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int gp = 0; gp < 2; ++gp) {
+                    // lane (r, hh) holds columns 32dt + 8gi + 4hh .. +3; one permlane32_swap per
+                    // dword pairs groups (2gp, 2gp+1) into columns 16(2dt + gp) + 8hh .. +7
+                    const int gi = 2 * gp;
+                    const unsigned ax = pack2(o[rb][dt][4 * gi] * inv, o[rb][dt][4 * gi + 1] * inv);
+                    const unsigned ay = pack2(o[rb][dt][4 * gi + 2] * inv, o[rb][dt][4 * gi + 3] * inv);
+                    const unsigned bx = pack2(o[rb][dt][4 * gi + 4] * inv, o[rb][dt][4 * gi + 5] * inv);
+                    const unsigned by = pack2(o[rb][dt][4 * gi + 6] * inv, o[rb][dt][4 * gi + 7] * inv);
+                    const auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+                    const auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+                    if (row < Sq)
+                        *reinterpret_cast<u32x4_t*>(op + 16 * (2 * dt + gp)) = u32x4_t{sx[0], sy[0], sx[1], sy[1]};
+                }
+        }
+    };
+
+    // Every iteration stages a tile -- past the end of the sequence the cursor stays on the last
+    // item and re-reads one of its tiles into the free slot -- so the wait at the top is always
+    // vmcnt(8) (no branch) and the kernel drains the DMA before it exits.
+    auto top = [&]() __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // end of an iteration: P(T) and the row sums are formed here (LLVM would otherwise sink the
+    // softmax into the next iteration, past its barrier), then the DMA of tile T + 2
+    auto tail = [&](int T, const u32x4_t (&pk)[2][4]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) asm volatile("" :: "v"(pk[rb][ks]));
+        asm volatile("" :: "v"(lsum[0]), "v"(lsum[1]));
+        stage(T + 2);
+    };
+    if constexpr (PIPE) {
+        // ---- hand-pipelined schedule (PIPE): each iteration is four phases of 16 MFMAs, every
+        // phase a sequence of 8 fenced steps (2 MFMAs of the two row blocks + fillers), so the
+        // program order is the issue order and the softmax VALU sits in the MFMA gaps:
+        //   A  QK(T) kb0              | exp/sum/pack of S(T-1) kb1 rb0 -> P(T-1) ks2,3 | K(T) kb1 reads
+        //   B  QK(T) kb1              | S(T-1) kb1 rb1                                  | V(T-1) ks0,1 reads
+        //   C  PV(T-1) ks0,1          | S(T) kb0 rb0 -> P(T) ks0,1                       | V(T-1) ks2,3 reads
+        //   [lgkmcnt(0), vmcnt(8), s_barrier B(T+1), DMA of tile T+3]
+        //   D  PV(T-1) ks2,3          | S(T) kb0 rb1                                    | K(T+1) kb0 reads
+        // Barrier B(T+1) sits between C and D: it retires tile T+1 (so D can read K(T+1) for the
+        // next A) and proves every wave has read V(T-1) (the slot tile T+3 is staged into, with its
+        // K(T-1), read in iteration T-1).  Tile X is staged right after B(X-2); the wait is always
+        // vmcnt(8) (tiles X, X+1 outstanding).  An item's first tile runs the phases without PV
+        // and without the previous tile's softmax; after its last tile a drain finishes S kb1 and
+        // runs PV(last) (no barrier), while the next item's Q loads.
+        bf16x8_t kf0[8], kf1[8], vfa[8], vfb[8];
+        f32x16_t s0[2], s1a[2], s1b[2];
+        u32x4_t p0a[2][2], p0b[2][2], p1[2][2];
+        auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
+        auto rdK = [&](bf16x8_t& d, int T, int kb, int j) __attribute__((always_inline)) {
+            d = lds16(smem_base + (T & 3) * W4_SLOT + koff[j] + kb * 32 * 256);
+        };
+        auto rdV = [&](bf16x8_t& d, int T, int ks, int dt) __attribute__((always_inline)) {
+            const unsigned a0 = smem_base + (T & 3) * W4_SLOT + voff[dt] + ks * 16 * 256;
+            const i16x4_t v0 = tr8(a0), v1 = tr8(a0 + 8 * 256);
+            d = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, v0), __builtin_bit_cast(bf16x4_t, v1), 0, 1, 2,
+                                        3, 4, 5, 6, 7);
+        };
+        // QK MFMAs in inline asm: S is written straight to VGPRs (the builtin's result lands in AGPRs
+        // next to O and then costs a v_accvgpr_read per value before the exps), the Q operand is read
+        // from AGPRs.  Hazards the compiler cannot see inside asm are covered by the schedule: an S
+        // block's first VALU read comes >= 16 MFMAs after its chain's last MFMA (XDL write -> VALU
+        // read needs ~18 wait states); the chain itself accumulates in place (srcC == vdst, the
+        // same opcode: forwarded); the K operand's lgkmcnt wait is inserted by the compiler (it
+        // tracks the asm's register uses).
+        auto mfK = [&](const bf16x8_t& kf, int j, f32x16_t (&sv)[2]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+                if (j == 0)
+                    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(sv[rb]) : "v"(kf), "a"(qf[rb][j]));
+                else
+                    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(sv[rb]) : "v"(kf), "a"(qf[rb][j]));
+            }
+        };
+        auto mfV = [&](const bf16x8_t& vf, const u32x4_t (&pkv)[2][2], int ksl, int dt) __attribute__((always_inline)) {
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+            {
+                o[rb][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, __builtin_bit_cast(bf16x8_t, pkv[rb][ksl]),
+                                                                     o[rb][dt], 0, 0, 0);
+                asm volatile("" : "+a"(o[rb][dt]));
+            }
+        };
+        // softmax of elements e, e+1 of one 16-value S block of row block rb: P pair -> dword
+        // (e >> 1) & 3 of k-step (e >> 3) of pkd, the two p into rb's row sum
+        auto smp = [&](const f32x16_t& sv, int e, u32x4_t (&pkd)[2], int rb) __attribute__((always_inline)) {
+            const float pa = __builtin_amdgcn_exp2f(sv[e]), pb = __builtin_amdgcn_exp2f(sv[e + 1]);
+            lsum[rb] += pa + pb;
+            const bf16x2_t w = {(__bf16)pa, (__bf16)pb};
+            unsigned wu = __builtin_bit_cast(unsigned, w);
+            // pure VALU floats freely in the IR: tie it to this step
+            asm volatile("" : "+v"(lsum[rb]), "+v"(wu));
+            pkd[e >> 3][(e >> 1) & 3] = wu;
+        };
+        // B(T+1); the DMA of tile T+3 is issued one piece per step of phase D
+        auto sync = [&](int T) __attribute__((always_inline)) {
+            fence();
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+            fence();
+            stage_begin(T + 3);
+        };
+        // one iteration on tile T; FIRST: the item's first tile (no PV, no previous softmax)
+        auto iteration = [&](int T, f32x16_t (&s1c)[2], const f32x16_t (&s1p)[2], u32x4_t (&p0c)[2][2],
+                             const u32x4_t (&p0p)[2][2], auto first_c) __attribute__((always_inline)) {
+            constexpr bool FIRST = decltype(first_c)::value;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {                                   // A
+                rdK(kf1[j], T, 1, j);
+                mfK(kf0[j], j, s0);
+                if (!FIRST) smp(s1p[0], 2 * j, p1[0], 0);
+                fence();
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {                                   // B
+                if (!FIRST) rdV(vfa[j], T - 1, j >> 2, j & 3);
+                mfK(kf1[j], j, s1c);
+                if (!FIRST) smp(s1p[1], 2 * j, p1[1], 1);
+                fence();
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {                                   // C
+                if (!FIRST) {
+                    // V ks2,3 fragments in the first half of C: the lgkmcnt(0) before the barrier
+                    // then finds them landed
+                    if (i < 4) {
+                        rdV(vfb[2 * i], T - 1, 2 + (i >> 1), (2 * i) & 3);
+                        rdV(vfb[2 * i + 1], T - 1, 2 + (i >> 1), (2 * i + 1) & 3);
+                    }
+                    mfV(vfa[i], p0p, i >> 2, i & 3);
+                }
+                smp(s0[0], 2 * i, p0c[0], 0);
+                fence();
+            }
+            sync(T);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {                                   // D
+                stage_piece(i);
+                rdK(kf0[i], T + 1, 0, i);
+                if (!FIRST) mfV(vfb[i], p1, i >> 2, i & 3);
+                smp(s0[1], 2 * i, p0c[1], 1);
+                fence();
+            }
+            stage_next();
+        };
+        // after the item's last tile TL: S(TL) kb1 -> P ks2,3, PV(TL)
+        auto drain = [&](int TL, const f32x16_t (&s1l)[2], const u32x4_t (&p0l)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                rdV(vfa[j], TL, j >> 2, j & 3);
+                smp(s1l[0], 2 * j, p1[0], 0);
+                fence();
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                rdV(vfb[j], TL, 2 + (j >> 2), j & 3);
+                smp(s1l[1], 2 * j, p1[1], 1);
+                fence();
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) mfV(vfa[i], p0l, i >> 2, i & 3);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) mfV(vfb[i], p1, i >> 2, i & 3);
+        };
+        // prologue: tiles 0, 1 staged, B(0), tile 2 staged, K(0) kb0 fragments, the first Q
+        stage(0);
+        stage(1);
+        fence();
+        asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+        fence();
+        stage(2);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) rdK(kf0[i], 0, 0, i);
+        int T = 0, q0 = 0;
+        int bh = item_bh(0, q0);
+        q0 += 64 * wave;
+        load_q(q_base(bh), q0);
+        for (int jt = 0; jt < n_items; ++jt) {
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+                lsum[rb] = 0.f;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) o[rb][dt][i] = 0.f;
+            }
+            iteration(T, s1a, s1b, p0a, p0b, std::true_type{});
+            ++T;
+            int t = 1;
+            for (; t + 1 < nkv; t += 2) {
+                iteration(T, s1b, s1a, p0b, p0a, std::false_type{});
+                ++T;
+                iteration(T, s1a, s1b, p0a, p0b, std::false_type{});
+                ++T;
+            }
+            const int bh_done = bh, q0_done = q0;
+            if (jt + 1 < n_items) {          // the next item's Q (its QK starts after the drain)
+                bh = item_bh(jt + 1, q0);
+                q0 += 64 * wave;
+            }
+            if (t < nkv) {
+                iteration(T, s1b, s1a, p0b, p0a, std::false_type{});
+                ++T;
+                if (jt + 1 < n_items) load_q(q_base(bh), q0);
+                drain(T - 1, s1b, p0b);
+            } else {
+                if (jt + 1 < n_items) load_q(q_base(bh), q0);
+                drain(T - 1, s1a, p0a);
+            }
+            finish(o_base(bh_done), q0_done, g0 + jt * gstride);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+    }
+    u32x4_t pkA[2][4], pkB[2][4];
+    float rs[2];
+    stage(0);
+    stage(1);
+    int T = 0;
+    for (int j = 0; j < n_items; ++j) {
+        int q0;
+        const int bh = item_bh(j, q0);
+        q0 += 64 * wave;
+        load_q(q_base(bh), q0);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+            lsum[rb] = 0.f;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) o[rb][dt][i] = 0.f;
+        }
+        top();
+        qk_softmax(T, pkA, rs);
+        lsum[0] += rs[0];
+        lsum[1] += rs[1];
+        tail(T, pkA);
+        ++T;
+        int t = 1;
+        for (; t + 1 < nkv; t += 2) {
+            top();
+            qk_softmax(T, pkB, rs);
+            pv(T - 1, pkA);
+            lsum[0] += rs[0];
+            lsum[1] += rs[1];
+            tail(T, pkB);
+            ++T;
+            top();
+            qk_softmax(T, pkA, rs);
+            pv(T - 1, pkB);
+            lsum[0] += rs[0];
+            lsum[1] += rs[1];
+            tail(T, pkA);
+            ++T;
+        }
+        if (t < nkv) {
+            top();
+            qk_softmax(T, pkB, rs);
+            pv(T - 1, pkA);
+            lsum[0] += rs[0];
+            lsum[1] += rs[1];
+            tail(T, pkB);
+            ++T;
+            pv(T - 1, pkB);
+        } else {
+            pv(T - 1, pkA);
+        }
+        finish(o_base(bh), q0, g0 + j * gstride);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
+}
+
+}  // namespace
+
+hipError_t attn_w4_launch(const AttnArgs& args, bool rebase, unsigned grid, hipStream_t stream) {
+    // VS_ATTN_W4_PIPE=0: the compiler-scheduled loop body (A/B reference)
+    const char* pe = getenv("VS_ATTN_W4_PIPE");
+    const bool pipe = !(pe && pe[0] == '0');
+    void (*kern)(AttnArgs) = rebase ? (pipe ? attn_fwd_w4<true, true> : attn_fwd_w4<true, false>)
+                                    : (pipe ? attn_fwd_w4<false, true> : attn_fwd_w4<false, false>);
+    static std::mutex mu;
+    static std::set<const void*> done;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        if (done.insert((const void*)kern).second)
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS);
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(W4_THR), W4_LDS, stream, args);
+    return hipGetLastError();
+}
+
+}  // namespace vs_attn
