@@ -7,6 +7,8 @@ K-tile counts 1..6 (both buffer parities and every prefetch-tail branch of the p
 partial last row / column tiles, the un-merged LoRA second K phase (layers.py:180-182) and the
 split tail (grid larger than the CU count).  Reference linears: wan_video_dit.py:131-134,157-160,
 209-210 through AutoWrappedLinear (vram_management/layers.py:173-188)."""
+import os
+
 import pytest
 import torch
 
@@ -124,7 +126,7 @@ def test_gemm_fp8_8p_integer_exact(M, N, Kd, monkeypatch):
     must reproduce oracle.fp8_linear (layers.py:115-151) bit for bit: pins the MX 32x32x64 operand
     maps, the fp8 chunk swizzle and the per-row scale."""
     from vstyler import kernels as K
-    monkeypatch.setenv("VS_FP8_BACKEND", "vstyler")
+    monkeypatch.setenv("VS_FP8_BACKEND", os.environ.get("VS_FP8_BACKEND", "vstyler"))
     g = torch.Generator().manual_seed(M + N + Kd)
     x = torch.randint(-4, 5, (M, Kd), generator=g).to(BF16)
     x[::5] *= 512          # rows whose max exceeds 448: scale 2**k > 1
@@ -144,7 +146,7 @@ def test_gemm_fp8_8p_split_tail_and_epilogue(monkeypatch):
     """272 tiles: the split-tail pieces + combine (per-row scale applied after the sum) equal the
     unsplit kernel on integer data; gate-residual + hint epilogue bit-exact vs the oracle."""
     from vstyler import kernels as K
-    monkeypatch.setenv("VS_FP8_BACKEND", "vstyler")
+    monkeypatch.setenv("VS_FP8_BACKEND", os.environ.get("VS_FP8_BACKEND", "vstyler"))
     M, N, Kd, S = 4352, 4096, 1024, 2176
     g = torch.Generator().manual_seed(21)
     x = torch.randint(-4, 5, (M, Kd), generator=g).to(BF16)

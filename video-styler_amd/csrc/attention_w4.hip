@@ -246,6 +246,7 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) o[rb][dt][i] = 0.f;
     float lsum[2] = {0.f, 0.f};
+    auto row_sum = [&](int rb) { return lsum[rb] + __shfl_xor(lsum[rb], 32); };
     f32x16_t zero;
 #pragma unroll
     for (int i = 0; i < 16; ++i) zero[i] = 0.f;
@@ -312,7 +313,7 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
     auto finish = [&](bf16_t* ob, int qrow0, int gi) __attribute__((always_inline)) {
         float lt[2];
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb) lt[rb] = lsum[rb] + __shfl_xor(lsum[rb], 32) - npad;
+        for (int rb = 0; rb < 2; ++rb) lt[rb] = row_sum(rb) - npad;
         if (piece >= 0) {
             float* pp = args.part + ((long long)(gi - nmain) * nsplit + piece) * BQ * PROW + wave * 64 * PROW;
 #pragma unroll
@@ -460,6 +461,26 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
             asm volatile("" : "+v"(lsum[rb]), "+v"(wu));
             pkd[e >> 3][(e >> 1) & 3] = wu;
         };
+        // the same softmax step in two halves for the split-gap placement: the two exps (8 issue
+        // cycles each) in one MFMA gap, the row-sum adds and the pack in the next
+        auto smp_e = [&](const f32x16_t& sv, int e, float& pa, float& pb) __attribute__((always_inline)) {
+            pa = __builtin_amdgcn_exp2f(sv[e]);
+            pb = __builtin_amdgcn_exp2f(sv[e + 1]);
+            asm volatile("" : "+v"(pa), "+v"(pb));
+        };
+        auto smp_f = [&](float pa, float pb, int e, u32x4_t (&pkd)[2], int rb) __attribute__((always_inline)) {
+            lsum[rb] += pa + pb;
+            const bf16x2_t w = {(__bf16)pa, (__bf16)pb};
+            unsigned wu = __builtin_bit_cast(unsigned, w);
+            asm volatile("" : "+v"(lsum[rb]), "+v"(wu));
+            pkd[e >> 3][(e >> 1) & 3] = wu;
+        };
+        auto mfK1 = [&](const bf16x8_t& kf, int j, f32x16_t (&sv)[2], int rb) __attribute__((always_inline)) {
+            if (j == 0)
+                asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(sv[rb]) : "v"(kf), "a"(qf[rb][j]));
+            else
+                asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(sv[rb]) : "v"(kf), "a"(qf[rb][j]));
+        };
         // B(T+1); the DMA of tile T+3 is issued one piece per step of phase D
         auto sync = [&](int T) __attribute__((always_inline)) {
             fence();
@@ -484,6 +505,37 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
             st_it = (blockIdx.x == 0 && !FIRST && T >= 8 && T < 40) ? T - 8 : -1;
 #endif
             stamp(0);
+#ifdef VS_W4_SPLITGAP
+            // A/B with the step's fillers split over its two MFMA gaps (program order pinned):
+            // [read, MFMA rb0] [exp, exp] [MFMA rb1] [add, add, pack]
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {                                   // A
+                float pa = 0.f, pb = 0.f;
+                rdK(kf1[j], T, 1, j);
+                mfK1(kf0[j], j, s0, 0);
+                fence();
+                if (!FIRST) smp_e(s1p[0], 2 * j, pa, pb);
+                fence();
+                mfK1(kf0[j], j, s0, 1);
+                fence();
+                if (!FIRST) smp_f(pa, pb, 2 * j, p1[0], 0);
+                fence();
+            }
+            stamp(1);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {                                   // B
+                float pa = 0.f, pb = 0.f;
+                if (!FIRST) rdV(vfa[j], T - 1, j >> 2, j & 3);
+                mfK1(kf1[j], j, s1c, 0);
+                fence();
+                if (!FIRST) smp_e(s1p[1], 2 * j, pa, pb);
+                fence();
+                mfK1(kf1[j], j, s1c, 1);
+                fence();
+                if (!FIRST) smp_f(pa, pb, 2 * j, p1[1], 1);
+                fence();
+            }
+#else
 #pragma unroll
             for (int j = 0; j < 8; ++j) {                                   // A
                 rdK(kf1[j], T, 1, j);
@@ -499,7 +551,38 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
                 if (!FIRST) smp(s1p[1], 2 * j, p1[1], 1);
                 fence();
             }
+#endif
             stamp(2);
+#ifdef VS_W4_SPLITC
+            // C split the same way: [V reads, PV rb0] [4 exps] [PV rb1] [4 adds, 2 packs]
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {                                   // C
+                float pa0, pb0, pa1, pb1;
+                if (!FIRST) {
+                    if (i < 4) {
+                        rdV(vfb[2 * i], T - 1, 2 + (i >> 1), (2 * i) & 3);
+                        rdV(vfb[2 * i + 1], T - 1, 2 + (i >> 1), (2 * i + 1) & 3);
+                    }
+                    o[0][i & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                        vfa[i], __builtin_bit_cast(bf16x8_t, p0p[0][i >> 2]), o[0][i & 3], 0, 0, 0);
+                    asm volatile("" : "+a"(o[0][i & 3]));
+                }
+                fence();
+                smp_e(s0[0], 2 * i, pa0, pb0);
+                smp_e(s0[1], 2 * i, pa1, pb1);
+                fence();
+                if (!FIRST) {
+                    o[1][i & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                        vfa[i], __builtin_bit_cast(bf16x8_t, p0p[1][i >> 2]), o[1][i & 3], 0, 0, 0);
+                    asm volatile("" : "+a"(o[1][i & 3]));
+                }
+                fence();
+                smp_f(pa0, pb0, 2 * i, p0c[0], 0);
+                smp_f(pa1, pb1, 2 * i, p0c[1], 1);
+                fence();
+            }
+            if (false)
+#endif
 #pragma unroll
             for (int i = 0; i < 8; ++i) {                                   // C
                 if (!FIRST) {

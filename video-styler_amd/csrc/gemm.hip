@@ -754,7 +754,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
         __builtin_amdgcn_sched_barrier(0);
     };
 
-    constexpr bool PRE = SCHED >= 1;
+    constexpr bool PRE = SCHED == 1 || SCHED == 2;
     if constexpr (SCHED == 2) {
         // prologue: tiles 0 and 1 in flight (A0 B0 B1 A1 each), wait for tile 0
         stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
@@ -776,12 +776,23 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
     }
     bar();
 
+    // SCHED 3 (the template's stagger): waves 4-7 run one barrier behind waves 0-3, so on every SIMD
+    // one wave's 16 MFMAs pair with its partner's fragment reads + DMA issue (matrix beside memory)
+    // instead of all 8 waves reading, then all 8 computing.  A0 is restaged one phase after its ph0
+    // reads; with the groups a barrier apart the other group's reads are retired by a counted
+    // lgkmcnt(4) (the 8 A reads, issued first) before ph0's first barrier.
+    constexpr bool STAG = SCHED == 3;
     // one K-tile = 4 phases; the body is written for a pair of tiles so the buffer is a constant
     auto tile4 = [&](int t, const char* buf) __attribute__((always_inline)) {
         // ph0: quadrant (A0, B0)
         read_a(buf, R_A0);
+        if constexpr (STAG) __builtin_amdgcn_sched_barrier(0);
         read_b(buf, R_B0, bf0);
         if (t + 1 < nt) stage(t + 1, 1);
+        if constexpr (STAG) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_waitcnt(0xC47F);     // lgkmcnt(4): this wave's A0 reads landed
+        }
         bar_wait_lgkm();
         mfma16(acc[0][0], bf0);
         bar();
@@ -925,11 +936,13 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
             if (t + 1 < nt) tile4p(t + 1, smem + BUF8, smem, bg0, bf0);
         }
     } else {
+        if (STAG && wr == 1) bar();
 #pragma nounroll
         for (int t = 0; t < nt; t += 2) {
             tile4(t, smem);
             if (t + 1 < nt) tile4(t + 1, smem + BUF8);
         }
+        if (STAG && wr == 0) bar();
     }
 
     // output: acc[qa][qb][i][j][e] = C[m][n], m = m0 + 128 qa + 64 wr + 16 i + (lane & 15),
@@ -984,6 +997,7 @@ __device__ __forceinline__ int q8_off(int row, int ch) {
     return row * 128 + 16 * (ch ^ (row & 7) ^ ((row >> 3) & 1));
 }
 
+template <bool STAG>     // STAG: the staggered schedule of gemm_bf16_tn_8p<false, 3>
 __global__ __launch_bounds__(512, 2) void gemm_fp8_tn_8p(
     const uint8_t* __restrict__ A, long long lda, const float* __restrict__ scale_a, const uint8_t* __restrict__ W,
     long long ldw, bf16_t* C, long long ldc, int M, int N, int K, Epi ep, int ntm, int ntn, int nmain, int ksplit,
@@ -1143,12 +1157,57 @@ __global__ __launch_bounds__(512, 2) void gemm_fp8_tn_8p(
         mfma4(acc[1][0], ag, b0);
         bar();
     };
-    read_a(0, R_A0, af);
-    read_b(0, R_B0, bf0);
+    // STAG: reads at phase start, waves 4-7 one barrier behind waves 0-3 (see gemm_bf16_tn_8p
+    // SCHED 3; A0 is restaged one phase after its ph0 reads, retired by lgkmcnt(4) before ph0's
+    // first barrier: read_a issues its 8 reads before read_b's 4)
+    auto tile4s = [&](int t, int b) __attribute__((always_inline)) {
+        read_a(b, R_A0, af);
+        __builtin_amdgcn_sched_barrier(0);
+        read_b(b, R_B0, bf0);
+        if (t + 1 < nt) stage(t + 1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0xC47F);     // lgkmcnt(4)
+        bar_wait_lgkm();
+        mfma4(acc[0][0], af, bf0);
+        bar();
+        read_b(b, R_B1, bf1);
+        if (t + 2 < nt) stage(t + 2, 0);
+        bar_wait_lgkm();
+        mfma4(acc[0][1], af, bf1);
+        bar();
+        read_a(b, R_A1, af);
+        if (t + 2 < nt) stage(t + 2, 2);
+        bar_wait_lgkm();
+        mfma4(acc[1][1], af, bf1);
+        bar();
+        if (t + 2 < nt) {
+            stage(t + 2, 3);
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else if (t + 1 < nt) {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        bar_wait_lgkm();
+        mfma4(acc[1][0], af, bf0);
+        bar();
+    };
+    if constexpr (STAG) {
+        if (wr == 1) bar();
 #pragma nounroll
-    for (int t = 0; t < nt; t += 2) {
-        tile4p(t, 0, bf0, bg0);
-        if (t + 1 < nt) tile4p(t + 1, 1, bg0, bf0);
+        for (int t = 0; t < nt; t += 2) {
+            tile4s(t, 0);
+            if (t + 1 < nt) tile4s(t + 1, 1);
+        }
+        if (wr == 0) bar();
+    } else {
+        read_a(0, R_A0, af);
+        read_b(0, R_B0, bf0);
+#pragma nounroll
+        for (int t = 0; t < nt; t += 2) {
+            tile4p(t, 0, bf0, bg0);
+            if (t + 1 < nt) tile4p(t + 1, 1, bg0, bf0);
+        }
     }
 
     // acc[qa][qb][i][4g + e] = D[n][m]: m = m0 + 128 qa + 64 wr + 32 i + (lane & 31),
@@ -1749,7 +1808,8 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
         static bool attr8 = false;
         if (!attr8) {
             for (const void* f : {(const void*)gemm_bf16_tn_8p<false, 0>, (const void*)gemm_bf16_tn_8p<true, 0>,
-                                  (const void*)gemm_bf16_tn_8p<false, 1>, (const void*)gemm_bf16_tn_8p<false, 2>})
+                                  (const void*)gemm_bf16_tn_8p<false, 1>, (const void*)gemm_bf16_tn_8p<false, 2>,
+                                  (const void*)gemm_bf16_tn_8p<false, 3>})
                 (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
             attr8 = true;
         }
@@ -1758,7 +1818,8 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
         const char* impl_env = getenv("VS_GEMM_IMPL");
         const bool pp = impl_env && impl_env[0] == 'p' && impl_env[1] == 'p';
         // 8p: reads at phase start; pre: fragment prefetch, two barriers per phase; default: 1b
-        const int sched = (impl_env && impl_env[0] == '8') ? 0 : (impl_env && impl_env[0] == 'p') ? 1 : 2;
+        const int sched = (impl_env && impl_env[0] == '8') ? 0 : (impl_env && impl_env[0] == 'p') ? 1
+                        : (impl_env && impl_env[0] == 's') ? 3 : 2;
         if (!pp) {
             KSplit sp = k2 ? KSplit{tm * tn, 0, 1, 0}
                            : plan_ksplit(tm * tn, k / 64, vs_cus_for_split("VS_GEMM_NO_SPLIT"), 64);
@@ -1769,6 +1830,7 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
             }
             // (the LoRA second phase needs a few more VGPRs than the prefetch leaves: no prefetch there)
             auto kern = k2 ? gemm_bf16_tn_8p<true, 0>
+                           : sched == 3 ? gemm_bf16_tn_8p<false, 3>
                            : sched == 2 ? gemm_bf16_tn_8p<false, 2>
                                         : sched == 1 ? gemm_bf16_tn_8p<false, 1> : gemm_bf16_tn_8p<false, 0>;
             hipLaunchKernelGGL(kern, dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(512), LDS8, (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw, (bf16_t*)c, ldc, m,
@@ -1864,7 +1926,8 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
     if (k % 128 == 0 && !(fb && fb[0] == 'p')) {
         static bool attr8 = false;
         if (!attr8) {
-            (void)hipFuncSetAttribute((const void*)gemm_fp8_tn_8p, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
+            (void)hipFuncSetAttribute((const void*)gemm_fp8_tn_8p<false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
+            (void)hipFuncSetAttribute((const void*)gemm_fp8_tn_8p<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
             attr8 = true;
         }
         KSplit sp = plan_ksplit(tm * tn, k / 128, vs_cus_for_split("VS_GEMM_NO_SPLIT"), 128);
@@ -1873,7 +1936,8 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
             part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
             if (!part) sp = KSplit{tm * tn, 0, 1, 0};
         }
-        hipLaunchKernelGGL(gemm_fp8_tn_8p, dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(512), LDS8,
+        // VS_FP8_BACKEND=vs: the staggered schedule (A/B)
+        hipLaunchKernelGGL((fb && fb[0] == 'v' && fb[1] == 's') ? gemm_fp8_tn_8p<true> : gemm_fp8_tn_8p<false>, dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(512), LDS8,
                            (hipStream_t)stream, (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c,
                            ldc, m, n, k, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part);
         VS_CHECK_LAUNCH();
