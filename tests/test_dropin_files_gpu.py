@@ -39,8 +39,10 @@ def ditto_lora(cfg, n_vace, rank, seed):
     for b in range(n_vace):
         for t in TARGETS:
             out_f, in_f = {"ffn.0": (F, D), "ffn.2": (D, F)}.get(t, (D, D))
-            sd[f"vace_blocks.{b}.{t}.lora_A.default.weight"] = (0.05 * torch.randn(rank, in_f, generator=g)).to(BF16)
-            sd[f"vace_blocks.{b}.{t}.lora_B.default.weight"] = (0.05 * torch.randn(out_f, rank, generator=g)).to(BF16)
+            # 0.15: the merged delta B.A is ~2x the weights' own scale, so the LoRA moves the 2-step
+            # latents by rel-L2 ~0.14 (0.009 at 0.05, i.e. not above the GPU-vs-oracle error)
+            sd[f"vace_blocks.{b}.{t}.lora_A.default.weight"] = (0.15 * torch.randn(rank, in_f, generator=g)).to(BF16)
+            sd[f"vace_blocks.{b}.{t}.lora_B.default.weight"] = (0.15 * torch.randn(out_f, rank, generator=g)).to(BF16)
     return sd
 
 
@@ -97,4 +99,5 @@ def test_from_pretrained_shards_ditto_lora_pipe(tmp_path, hotload):
     # only if the LoRA term were negligible)
     base = O.denoise({k: v.cuda() for k, v in W.items()}, cfg, noise, cp.cuda(), cn.cuda(), vc.cuda(),
                      num_inference_steps=2)
-    assert (base.float() - r).abs().max().item() > 10 * (fmx + 1e-3)
+    eff = ((base.float() - r).norm() / r.norm()).item()
+    assert eff > 5 * max(frl, rl), (eff, frl, rl)

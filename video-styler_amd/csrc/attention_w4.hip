@@ -428,15 +428,6 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
         // read needs ~18 wait states); the chain itself accumulates in place (srcC == vdst, the
         // same opcode: forwarded); the K operand's lgkmcnt wait is inserted by the compiler (it
         // tracks the asm's register uses).
-        auto mfK = [&](const bf16x8_t& kf, int j, f32x16_t (&sv)[2]) __attribute__((always_inline)) {
-#pragma unroll
-            for (int rb = 0; rb < 2; ++rb) {
-                if (j == 0)
-                    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(sv[rb]) : "v"(kf), "a"(qf[rb][j]));
-                else
-                    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(sv[rb]) : "v"(kf), "a"(qf[rb][j]));
-            }
-        };
         auto mfV = [&](const bf16x8_t& vf, const u32x4_t (&pkv)[2][2], int ksl, int dt) __attribute__((always_inline)) {
 #pragma unroll
             for (int rb = 0; rb < 2; ++rb)
@@ -505,7 +496,6 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
             st_it = (blockIdx.x == 0 && !FIRST && T >= 8 && T < 40) ? T - 8 : -1;
 #endif
             stamp(0);
-#ifdef VS_W4_SPLITGAP
             // A/B with the step's fillers split over its two MFMA gaps (program order pinned):
             // [read, MFMA rb0] [exp, exp] [MFMA rb1] [add, add, pack]
 #pragma unroll
@@ -535,54 +525,7 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
                 if (!FIRST) smp_f(pa, pb, 2 * j, p1[1], 1);
                 fence();
             }
-#else
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {                                   // A
-                rdK(kf1[j], T, 1, j);
-                mfK(kf0[j], j, s0);
-                if (!FIRST) smp(s1p[0], 2 * j, p1[0], 0);
-                fence();
-            }
-            stamp(1);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {                                   // B
-                if (!FIRST) rdV(vfa[j], T - 1, j >> 2, j & 3);
-                mfK(kf1[j], j, s1c);
-                if (!FIRST) smp(s1p[1], 2 * j, p1[1], 1);
-                fence();
-            }
-#endif
             stamp(2);
-#ifdef VS_W4_SPLITC
-            // C split the same way: [V reads, PV rb0] [4 exps] [PV rb1] [4 adds, 2 packs]
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {                                   // C
-                float pa0, pb0, pa1, pb1;
-                if (!FIRST) {
-                    if (i < 4) {
-                        rdV(vfb[2 * i], T - 1, 2 + (i >> 1), (2 * i) & 3);
-                        rdV(vfb[2 * i + 1], T - 1, 2 + (i >> 1), (2 * i + 1) & 3);
-                    }
-                    o[0][i & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                        vfa[i], __builtin_bit_cast(bf16x8_t, p0p[0][i >> 2]), o[0][i & 3], 0, 0, 0);
-                    asm volatile("" : "+a"(o[0][i & 3]));
-                }
-                fence();
-                smp_e(s0[0], 2 * i, pa0, pb0);
-                smp_e(s0[1], 2 * i, pa1, pb1);
-                fence();
-                if (!FIRST) {
-                    o[1][i & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                        vfa[i], __builtin_bit_cast(bf16x8_t, p0p[1][i >> 2]), o[1][i & 3], 0, 0, 0);
-                    asm volatile("" : "+a"(o[1][i & 3]));
-                }
-                fence();
-                smp_f(pa0, pb0, 2 * i, p0c[0], 0);
-                smp_f(pa1, pb1, 2 * i, p0c[1], 1);
-                fence();
-            }
-            if (false)
-#endif
 #pragma unroll
             for (int i = 0; i < 8; ++i) {                                   // C
                 if (!FIRST) {
