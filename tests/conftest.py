@@ -22,3 +22,23 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _heartbeat():
+    """A line on stderr every 60 s while the GPU suite runs: some tests (the 14B production-shape
+    oracle checks, the RCCL world-1 worker) compute for minutes without output, and a GPU box
+    watchdog takes 3 silent minutes for a hang."""
+    import threading
+    import time
+    import torch
+    stop = threading.Event()
+    if torch.cuda.is_available():
+        t0 = time.time()
+
+        def beat():
+            while not stop.wait(60):
+                print(f"[heartbeat {time.time() - t0:.0f} s]", file=sys.__stderr__, flush=True)
+        threading.Thread(target=beat, daemon=True).start()
+    yield
+    stop.set()

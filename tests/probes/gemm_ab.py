@@ -1,12 +1,11 @@
-"""A/B: the fp8 8-phase MFMA GEMM (VS_FP8_BACKEND=vstyler) vs hipBLASLt fp8 (lt) vs the r2 fp8 kernel
-(pp), per 14B block GEMM with its real epilogue (GELU on the two-pass rounding route); interleaved
-rounds in one process.  usage: gemm_fp8_8p_ab.py [M ...]"""
+"""A/B: the hand-written staggered 8-phase GEMM (vstyler) vs the hipBLASLt route (lt, + its epilogue
+pass), per 14B block GEMM with its real epilogue; interleaved rounds, one process.  A third build
+can join with AB_VARIANTS=vstyler,lt,diag:<path to libvstyler.so> (not loaded here: run per build).
+usage: gemm_ab.py [M ...]"""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "video-styler_amd"))
 import torch
 from vstyler import kernels as K
-
-os.environ["VS_LT_GELU"] = "0"
 
 
 def timed(fn, reps=3):
@@ -19,15 +18,12 @@ def timed(fn, reps=3):
 
 SHAPES = (("qkv", 15360, 5120, K.VS_EPI_BIAS), ("o-proj", 5120, 5120, K.VS_EPI_GATE_RES),
           ("ffn-up", 13824, 5120, K.VS_EPI_GELU), ("ffn-down", 5120, 13824, K.VS_EPI_GATE_RES))
-VARIANTS = os.environ.get("AB_VARIANTS", "vstyler,lt,pp").split(",")
-for M in [int(v) for v in sys.argv[1:]] or (59280,):
+VARIANTS = [v for v in os.environ.get("AB_VARIANTS", "vstyler,lt").split(",")]
+for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
     for name, N, Kd, epi in SHAPES:
         g = torch.Generator(device="cuda").manual_seed(1)
         a = torch.randn(M, Kd, device="cuda", generator=g).to(torch.bfloat16)
-        w8 = (0.05 * torch.randn(N, Kd, device="cuda", generator=g)).to(torch.float8_e4m3fn).view(torch.uint8)
-        a8 = torch.empty(M, Kd, dtype=torch.uint8, device="cuda")
-        sc = torch.empty(M, dtype=torch.float32, device="cuda")
-        K.quant_fp8_rows(a, a8, sc)
+        w = (0.05 * torch.randn(N, Kd, device="cuda", generator=g)).to(torch.bfloat16)
         b = (0.1 * torch.randn(N, device="cuda", generator=g)).to(torch.bfloat16)
         gate = (0.1 * torch.randn(2, N, device="cuda", generator=g)).to(torch.bfloat16)
         x = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
@@ -35,16 +31,19 @@ for M in [int(v) for v in sys.argv[1:]] or (59280,):
         if epi == K.VS_EPI_GATE_RES:
             kw.update(residual=x, gate=gate, gate_bstride=N, rows_per_batch=(M + 1) // 2)
         out = x if epi == K.VS_EPI_GATE_RES else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+
+        def setv(v):
+            os.environ["VS_GEMM_BACKEND"] = "lt" if v == "lt" else "vstyler"
+            os.environ["VSTYLER_GEMM_TILE"] = "256"
         t = {v: [] for v in VARIANTS}
-        for v in VARIANTS:
-            os.environ["VS_FP8_BACKEND"] = v
-            K.gemm_fp8(a8, sc, w8, out, **kw); torch.cuda.synchronize()
+        for v in VARIANTS:             # warm (hipBLASLt autotune happens here)
+            setv(v); K.gemm(a, w, out, **kw); torch.cuda.synchronize()
         for r in range(4):
             for v in VARIANTS:
-                os.environ["VS_FP8_BACKEND"] = v
-                t[v].append(timed(lambda: K.gemm_fp8(a8, sc, w8, out, **kw)))
+                setv(v); t[v].append(timed(lambda: K.gemm(a, w, out, **kw)))
         fl = 2.0 * M * N * Kd
-        print(f"fp8 M={M} {name:8s} N={N} K={Kd}: " +
-              "  ".join(f"{v} {min(t[v]):.3f} ms ({fl / min(t[v]) / 1e9:.0f} TF/s)" for v in VARIANTS), flush=True)
-        del a, w8, a8, sc, b, gate, x, out
-os.environ.pop("VS_FP8_BACKEND", None)
+        s = "  ".join(f"{v} {min(t[v]):.3f} ms ({fl / min(t[v]) / 1e9:.0f} TF/s)" for v in VARIANTS)
+        print(f"M={M} {name:8s} N={N} K={Kd}: {s}", flush=True)
+        del a, w, b, gate, x, out
+for k in ("VS_GEMM_BACKEND", "VSTYLER_GEMM_TILE"):
+    os.environ.pop(k, None)

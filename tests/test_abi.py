@@ -149,17 +149,22 @@ def test_gemm_split_plan_host_only():
 def test_gemm_route_rule(monkeypatch):
     """vs_gemm_route: hipBLASLt for grids of >= 1024 256x256 tiles, or >= 256 tiles with K <= 8192,
     or smaller grids with N >= 2048 and 1024 <= K <= 8192 (gemm.hip lt_route, measured in
-    profiles/r1/gemm_backend_ab_r1j.log and gemm_backend_ab_ctx_r1s.log); VS_GEMM_BACKEND forces."""
+    profiles/r1/gemm_backend_ab_r1j.log and gemm_backend_ab_ctx_r1s.log), except the FFN shapes where
+    the staggered MFMA kernel measured faster (r3); VS_GEMM_BACKEND forces."""
     from vstyler import _lib
     lib = _lib.load()
     monkeypatch.delenv("VS_GEMM_BACKEND", raising=False)
     assert lib.vs_gemm_route(59280, 5120, 13824) == 1       # 4640 tiles
     assert lib.vs_gemm_route(7410, 5120, 5120) == 1         # 580 tiles, K 5120
     assert lib.vs_gemm_route(3705, 5120, 5120) == 1         # 300 tiles
-    # 580 tiles, K 13824: hipBLASLt only on the private ROCm-7.2 copy (gemm.hip lt_route, r2)
-    private = lib.vs_blaslt_library().decode() != "linked"
-    assert lib.vs_gemm_route(7410, 5120, 13824) == (1 if private else 0)
-    assert lib.vs_gemm_route(3705, 5120, 13824) == (1 if private else 0)
+    # r3: the staggered 8-phase kernel keeps the FFN GEMMs of the Ulysses per-rank row counts
+    # (gemm.hip own_wins, profiles/r3/gemm_stagger_ab_s2.log)
+    assert lib.vs_gemm_route(7410, 5120, 13824) == 0        # FFN-down, SP = 8 merged phase
+    assert lib.vs_gemm_route(3705, 5120, 13824) == 0
+    assert lib.vs_gemm_route(14820, 5120, 13824) == 0       # SP = 4
+    assert lib.vs_gemm_route(7410, 15360, 5120) == 1        # q|k|v stays on hipBLASLt
+    # (FFN-up at <= 8192 rows also stays on the MFMA kernel: that rule keys on its GELU epilogue,
+    # which vs_gemm_route, a bias-epilogue query, does not take)
     assert lib.vs_gemm_route(1024, 10240, 5120) == 1        # 160 tiles: cross k|v over the context
     assert lib.vs_gemm_route(2, 30720, 5120) == 1           # time projection
     assert lib.vs_gemm_route(512, 4096, 10240) == 0         # 32 tiles, K 10240 (UMT5 FFN-down)
