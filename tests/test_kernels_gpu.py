@@ -92,13 +92,13 @@ def test_gemm_epilogues(K):
 
 def test_gemm_split_tail_exact(K, monkeypatch):
     """Split tail of the 256x256 schedule: 18 x 16 = 288 tiles (last row and column partial) on
-    256 CUs run 256 whole tiles and 32 tail tiles as 8 K pieces (7 x 544 + 352), summed and finished by the
+    256 CUs run 256 whole tiles and 32 tail tiles as 8 K pieces (7 x 576 + 128), summed and finished by the
     combine kernel.  Integer operands keep every fp32 sum exact, so the result must equal the
     exact product and, for every epilogue, the unsplit grid bit for bit."""
     M, N, Kd = 4452, 4000, 4160
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     if cus == 256:
-        assert K.gemm_split_plan(M, N, Kd, cus) == (256, 32, 8, 544)
+        assert K.gemm_split_plan(M, N, Kd, cus) == (256, 32, 8, 576)
     g = torch.Generator(device="cuda").manual_seed(80)
     a = torch.randint(-3, 4, (M, Kd), device="cuda", generator=g).to(BF16)
     w = torch.randint(-3, 4, (N, Kd), device="cuda", generator=g).to(BF16)

@@ -89,18 +89,7 @@ constexpr float SUM_MIN = 0x1p-60f;
 // FLOPs as two v_mfma_f32_16x16x32_bf16 on the same operands, to measure the clock / issue effect
 // of the smaller MFMA shape on this loop (MI355X_MICROARCH 'DVFS give-back' item 7)
 __device__ __forceinline__ f32x16_t mfma32(bf16x8_t a, bf16x8_t b, f32x16_t c, int half = 0) {
-#ifdef VS_ATTN_DIAG_MFMA16
-    // alternate calls update the two halves of the accumulator, so all of it stays live
-    const int o = half ? 8 : 0;
-    f32x4_t c0 = {c[o], c[o + 1], c[o + 2], c[o + 3]}, c1 = {c[o + 4], c[o + 5], c[o + 6], c[o + 7]};
-    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, c1, 0, 0, 0);
-    c[o] = c0[0]; c[o + 1] = c0[1]; c[o + 2] = c0[2]; c[o + 3] = c0[3];
-    c[o + 4] = c1[0]; c[o + 5] = c1[1]; c[o + 6] = c1[2]; c[o + 7] = c1[3];
-    return c;
-#else
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-#endif
 }
 
 // v_mfma_f32_16x16x32_bf16 on the 4-value group g of a 16-value accumulator block (the M16 layout
@@ -122,33 +111,10 @@ __device__ __forceinline__ f32x16_t mfma16g(bf16x8_t a, bf16x8_t b, f32x16_t c, 
 
 // scheduling fences inside the QK / PV step sequences (VS_ATTN_SB_FREE_QK / _PV: A/B builds that let
 // the machine scheduler move instructions across k-steps)
-#ifdef VS_ATTN_SB_FREE_QK
-#define ATTN_SB_QK() do {} while (0)
-#else
 #define ATTN_SB_QK() __builtin_amdgcn_sched_barrier(0)
-#endif
-#ifdef VS_ATTN_SB_FREE_PV
-#define ATTN_SB_PV() do {} while (0)
-#else
 #define ATTN_SB_PV() __builtin_amdgcn_sched_barrier(0)
-#endif
 
-#ifdef VS_ATTN_STAMPS
-// debug build: s_memtime at the 4 phase boundaries of tiles 2..33 for wave 0 (group 0) and wave 4
-// (group 1) of workgroup 0, kept in an LDS tail during the loop (no loop-carried registers) and
-// copied out after it.  The stamp's lgkmcnt wait sits next to a barrier that drains LDS anyway.
-__device__ unsigned long long g_attn_stamps[2][4 * 32];
-constexpr int STAMP_LDS = 8 * 4 * 32 * 8;
-#define ATTN_STAMP(slot)                                                                          \
-    do {                                                                                          \
-        unsigned long long t_;                                                                    \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_));                          \
-        *reinterpret_cast<volatile unsigned long long*>(                                          \
-            smem + LDS_BYTES + 8 * (wave * 128 + 8 * (stamp_it & 15) + (slot))) = t_;             \
-    } while (0)
-#else
 #define ATTN_STAMP(slot) do {} while (0)
-#endif
 
 
 template <bool REBASE, bool M16, bool PF, int MODE>
@@ -282,9 +248,6 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             kst[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, kvo0, 0, 0);
             kst[1] = __builtin_amdgcn_raw_buffer_load_b128(rs, kvo1, 0, 0);
         } else {
-#ifdef VS_ATTN_DIAG_HOTKV
-            kv0 &= BKV;      // timing diagnostic only (wrong results): every tile reads tile 0 or 1 (L2-hot)
-#endif
             const int ks = kv0 * ldk32 * 2;
             kst[0] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo0, ks, 0);
             kst[1] = __builtin_amdgcn_raw_buffer_load_b128(krs, kvo1, ks, 0);
@@ -296,9 +259,6 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             vst[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, vvo0, 0, 0);
             vst[1] = __builtin_amdgcn_raw_buffer_load_b128(rs, vvo1, 0, 0);
         } else {
-#ifdef VS_ATTN_DIAG_HOTKV
-            kv0 &= BKV;
-#endif
             const int vs = kv0 * ldv32 * 2;
             vst[0] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo0, vs, 0);
             vst[1] = __builtin_amdgcn_raw_buffer_load_b128(vrs, vvo1, vs, 0);
@@ -499,9 +459,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
                 const int e = 2 * (j - 8);
                 s[0][e] = __builtin_amdgcn_exp2f(s[0][e]);
                 s[0][e + 1] = __builtin_amdgcn_exp2f(s[0][e + 1]);
-#ifndef VS_ATTN_NC_NOTIE
                 asm volatile("" : "+v"(s[0][e]), "+v"(s[0][e + 1]));
-#endif
             } else if (t == 1) {
                 const int e = 2 * (j - 8);
                 s[0][e] = __builtin_amdgcn_exp2f(s[0][e]);
@@ -582,11 +540,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
                 }
             }
             if constexpr (NC) {
-#ifndef VS_ATTN_ONES_ODD
                 if ((ks & 1) == 0) {
-#else
-                if ((ks & 1) == 1) {
-#endif
 #pragma unroll
                     for (int qb = 0; qb < 2; ++qb)
                         lsum[qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
@@ -604,9 +558,6 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
     // M16: the steps run key chunk 1 first (steps ks = 2, 3), then chunk 0 (ks = 0, 1): once chunk
     // 1's MFMAs are issued, the s[1] half's softmax (exps, sums, packs into the chunk-1 operands)
     // runs beside chunk 0's; the s[0] half (exponentiated in the QK phase) is packed at the end.
-#ifdef VS_ATTN_STAMPS
-    int stamp_it = 0;
-#endif
     auto pv_softmax = [&](int slot, bool with_pv) __attribute__((always_inline)) {
         const char* base = smem + 2 * KTS + slot * VTS;
         rs0 = 0.f;
@@ -757,9 +708,6 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
     };
     __syncthreads();
     const int grp = wave >> 2;
-#ifdef VS_ATTN_PRIO_YOUNG
-    if (grp == 1) __builtin_amdgcn_s_setprio(1);      // static priority for the second-dispatched half
-#endif
     if (grp == 1) phase_bar();
     // the normalised bf16 output of a finished item in 8 chunks of 16 B per lane, emit(c, w) storing
     // or staging chunk c; one column block dt at a time (8 live registers).  Each lane's chunk c
@@ -842,15 +790,8 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
         constexpr bool first0 = decltype(first_c)::value;
         const bool first = first0 || ti == 0;
         const int kv0 = ti * BKV;
-#ifdef VS_ATTN_DIAG_NOQPREF
-        const bool qpref = false;         // timing diagnostic only: the next item reuses this Q
-#else
         const bool qpref = PF && tj + 1 < n_items && ti < PERSIST_MIN_TILES;
-#endif
         const bool odrain = PF && tj > 0 && ti < PERSIST_MIN_TILES;
-#ifdef VS_ATTN_STAMPS
-        stamp_it = T;
-#endif
         ATTN_STAMP(0);
         // each phase opens with the LDS store of the tile staged one phase earlier (its slot's last
         // reader finished before the barrier that opened this phase), then the next global loads
@@ -900,14 +841,10 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
         if constexpr (PF) {
             // chunk ti of the previous item's O (range 0 unless draining: the store is dropped)
             const u32x4_t w = *reinterpret_cast<const u32x4_t*>(qslot(ti == 0 ? 8 : (ti & 7)));
-#ifndef VS_ATTN_DIAG_NOSTORE
             __builtin_amdgcn_raw_buffer_store_b128(
                 __builtin_bit_cast(i32x4_t, w),
                 make_rsrc(ob_prev + (long long)q0_prev * ldo, odrain ? (unsigned)(max(Sq - q0_prev, 0) * ldo * 2) : 0u),
                 (unsigned)(ooff(ti & 7) * 2), 0, 0);
-#else
-            asm volatile("" :: "v"(w));
-#endif
         }
         if (qpref) {
             bf16x8_t qs;
@@ -918,11 +855,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
         if constexpr (!NC) {
             const float rt0 = row_tot(0), rt1 = M16 ? row_tot(1) : rt0;
             const bool low = first && !(fminf(rt0, rt1) >= SUM_MIN);
-#ifdef VS_ATTN_DIAG_MFMA16
-            if (__any(rt0 > 1e30f && low)) exact_split(first, kv0, low);   // (never: garbage scores)
-#else
             if (__any(fmaxf(rt0, rt1) > SUM_THR || low)) exact_split(first, kv0, low);
-#endif
         }
         if constexpr (!NC) {
             lq[0] += row_tot(0);
@@ -933,14 +866,12 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             // block); the V loader and the exact-path recompute follow the QK item, the K loader
             // is already on it
             ti = 0;
-#ifndef VS_ATTN_DIAG_NOQPREF
             if constexpr (PF) {
 #pragma unroll
                 for (int s2 = 0; s2 < 8; ++s2) qf[s2] = *reinterpret_cast<const bf16x8_t*>(qslot(s2));
             } else {
                 load_q(qb_nxt, q0_nxt);
             }
-#endif
 #pragma unroll
             for (int i = 0; i < 16; ++i) negm[i] = 0.f;
             mq[0] = 0.f;
@@ -964,14 +895,6 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
     };
     tile(0, std::true_type{});
     for (int T = 1; T < Ttot; ++T) tile(T, std::false_type{});
-#ifdef VS_ATTN_STAMPS
-    // stamps of tiles (Ttot-32) .. Ttot-1 (ring of 32), copied out by workgroup 0's waves 0 and 4
-    if (blockIdx.x == 0 && (wave & 3) == 0) {
-        for (int i = lane; i < 128; i += 64)
-            g_attn_stamps[wave >> 2][i] =
-                *reinterpret_cast<volatile unsigned long long*>(smem + LDS_BYTES + 8 * (wave * 128 + i));
-    }
-#endif
     // ---- B_{Ttot-1}: the last tile's PV.  Group 0 first waits for group 1's half of V(Ttot-1)
     // (stored in group 1's A_{Ttot-1}, one phase later): the extra barrier that balances the count
     if (grp == 0) phase_bar();
@@ -1086,11 +1009,6 @@ SplitPlan plan_split(long long nwg, int nkv, int cus) {
 
 }  // namespace
 
-#ifdef VS_ATTN_STAMPS
-extern "C" int vs_debug_attn_stamps(unsigned long long* host_out) {
-    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps)) == hipSuccess ? 0 : 2;
-}
-#endif
 
 extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o, int batch, int sq,
                            int skv, int heads, int head_dim, long long ldq, long long ldk,
@@ -1156,11 +1074,7 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
             nc_cap = (int)std::min(cap, (long long)0x7fffffff);
         }
     }
-#ifdef VS_ATTN_STAMPS
-    const int lds = LDS_BYTES + STAMP_LDS;
-#else
     const int lds = LDS_BYTES;      // + the kernel's static QPRE_BYTES Q buffer
-#endif
     const long long grid = (long long)npers + (long long)sp.ntail * sp.nsplit;
     AttnArgs args{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, bsq, bsk, bsv, bso,
                   ldq, ldk, ldv, ldo, part, flags, c, sq, skv, heads, nqb, sp.nmain, npers, sp.nsplit,

@@ -440,11 +440,7 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
         // softmax of elements e, e+1 of one 16-value S block of row block rb: P pair -> dword
         // (e >> 1) & 3 of k-step (e >> 3) of pkd, the two p into rb's row sum
         auto smp = [&](const f32x16_t& sv, int e, u32x4_t (&pkd)[2], int rb) __attribute__((always_inline)) {
-#ifndef VS_W4_DIAG_NOEXP            // (timing diagnostic only: no transcendental)
             const float pa = __builtin_amdgcn_exp2f(sv[e]), pb = __builtin_amdgcn_exp2f(sv[e + 1]);
-#else
-            const float pa = sv[e] * 0.5f, pb = sv[e + 1] * 0.5f;
-#endif
             lsum[rb] += pa + pb;
             const bf16x2_t w = {(__bf16)pa, (__bf16)pb};
             unsigned wu = __builtin_bit_cast(unsigned, w);
@@ -544,9 +540,7 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
             sync(T);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {                                   // D
-#ifndef VS_W4_DIAG_NODMA            // (timing diagnostic only: no K/V staging after the prologue)
                 stage_piece(i);
-#endif
                 rdK(kf0[i], T + 1, 0, i);
                 if (!FIRST) mfV(vfb[i], p1, i >> 2, i & 3);
                 fence();
