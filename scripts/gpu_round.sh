@@ -7,7 +7,7 @@ TAG=${1:-r3}
 mkdir -p $R/gpurun_out
 cd $R
 K=${2:+-k "$2"}
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q -rA --timeout 300 --timeout-method thread $K \
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread $K \
   > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -40 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
 grep -E "passed|failed" gpurun_out/pytest_gpu_$TAG.log | tail -2
 timeout -k 10 600 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -20 gpurun_out/bench_$TAG.err; exit 1; }

@@ -7,6 +7,7 @@
   kernel is row/head-local with a fixed reduction order, so sharding changes no rounding).
 """
 import os
+import sys
 import socket
 
 import pytest
@@ -152,6 +153,7 @@ def _rccl_worker(port, q):
         init_distributed()
         assert torch.distributed.get_backend() == "nccl"
         res = {}
+        print("[rccl worker] 1 stages", file=sys.stderr, flush=True)
         # (1) the stages driven directly: exchange_start -> attend -> finish == plain attention
         g = torch.Generator().manual_seed(7)
         B, S, H = 2, 320, 2
@@ -170,6 +172,7 @@ def _rccl_worker(port, q):
         full = sp.gather_tokens(xl[:, :64].contiguous(), rc2)
         torch.cuda.synchronize()
         res["gather"] = torch.equal(full, ref[:, :64]) and sp.collective_calls == 3
+        print("[rccl worker] 2 model", file=sys.stderr, flush=True)
         # (2) the whole model through the sharded path, both schedules
         cfg = O.WAN_CONFIGS["tiny"]
         W = O.random_weights(cfg, seed=5)
@@ -193,6 +196,7 @@ def _rccl_worker(port, q):
             res[key] = torch.equal(single.cpu(), par.cpu()) and sp.collective_calls == want_calls
             res["calls_" + key] = (sp.collective_calls, want_calls)
         os.environ.pop("VSTYLER_SP_MERGE_FFN")
+        print("[rccl worker] 3 fused", file=sys.stderr, flush=True)
         # (3) the residual + LayerNorm fusions on the hipBLASLt route under the overlap schedule (the
         # merged cross-attention/FFN phase fuses the last block's FFN-down with the head's norm):
         # bit-identical to the unfused sharded forward
@@ -207,6 +211,7 @@ def _rccl_worker(port, q):
         res["fused_lt_sp"] = torch.equal(outs[0], outs[1])
         os.environ.pop("VS_GEMM_BACKEND")
         os.environ.pop("VSTYLER_FUSE_RES_LN")
+        print("[rccl worker] 4 native", file=sys.stderr, flush=True)
         # (4) the C-ABI collectives (vs_sp_*: RCCL opened by libvstyler itself, its own communicator
         # and comm stream) under the overlap schedule: bit-identical too, and the raw exchanges
         # move exactly the bytes asked for
@@ -224,6 +229,7 @@ def _rccl_worker(port, q):
         nblk = cfg["num_layers"] + len(cfg["vace_layers"])
         res["native_model"] = torch.equal(single.cpu(), par.cpu()) and sp.collective_calls == 2 + nblk * 4 + 1
         sp.native.close()
+        print("[rccl worker] 5 graph", file=sys.stderr, flush=True)
         # (5) the SP denoising step captured into one hipGraph (RCCL collectives inside the graph,
         # wan_video_new.py:515-542's loop): replays bit-identical to eager steps, for torch.distributed
         # RCCL and for libvstyler's own communicator
