@@ -82,7 +82,7 @@ def cpu_baseline(m, S, rows=2048):
 
     def block(n, vace):
         x = torch.randn(1, n, D, generator=g).to(bf)
-        freqs = O.rope_freqs(1, 1, n)
+        freqs = O.rope_freqs(1, n // 64, 64)      # a (1, n/64, 64) token grid: RoPE tables hold 1024 positions
         t0 = time.perf_counter()
         mod = O.bf(Wb["modulation"].float() + t_mod.float())
         sh, sc, ga, sh2, sc2, ga2 = mod.chunk(6, dim=1)

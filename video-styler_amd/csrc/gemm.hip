@@ -317,7 +317,7 @@ __device__ __forceinline__ constexpr int hoff(int which, int b) { return (2 * wh
 
 __device__ __forceinline__ int q_off(int row, int ch) { return row * 128 + 16 * (ch ^ (row & 7)); }
 
-template <bool LORA>
+template <bool LORA, bool WIDE>    // WIDE: 16-B epilogue accesses (host-checked alignment, N % 8 == 0)
 __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
     const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
     bf16_t* C, long long ldc, int M, int N, int K, const bf16_t* __restrict__ A2, long long lda2,
@@ -526,6 +526,35 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
                     for (int j = 0; j < 2; ++j)
                         *reinterpret_cast<f32x4_t*>(pp + (128 * a + 64 * wr + 16 * i + (lane & 15)) * T8 + 128 * b +
                                                     32 * wc + 16 * j + 4 * (lane >> 4)) = acc[a][b][i][j];
+        return;
+    }
+    if constexpr (WIDE) {
+        // 16-B epilogue (CDNA guide T21): lanes of row groups g, g^1 (lane ^ 16) trade one column
+        // block through permlane16_swap, so an even-g lane holds columns 4g .. 4g+7 of block j = 0 and
+        // an odd-g lane columns 16 + 4(g-1) .. +7 of block 1: one 8-column epilogue (16-B loads of
+        // bias / residual / gate / hint, one 16-B store) instead of two 4-column ones
+        const int g = lane >> 4;
+        const int nw = 16 * (g & 1) + 4 * (g & ~1);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int m = m0 + 128 * a + 64 * wr + 16 * i + (lane & 15);
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    float v[8];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, acc[a][b][i][0][e]),
+                                                                         __builtin_bit_cast(unsigned, acc[a][b][i][1][e]),
+                                                                         false, false);
+                        v[e] = __builtin_bit_cast(float, (unsigned)sw[0]);
+                        v[4 + e] = __builtin_bit_cast(float, (unsigned)sw[1]);
+                    }
+                    const int n = n0 + 128 * b + 32 * wc + nw;
+                    if (m < M && n < N) epilogue_store_w<8>(v, m, n, C, ldc, ep);
+                }
+            }
         return;
     }
 #pragma unroll
@@ -986,17 +1015,26 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
         const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
         static bool attr8 = false;
         if (!attr8) {
-            (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_8p<false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
-            (void)hipFuncSetAttribute((const void*)gemm_bf16_tn_8p<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
+            for (const void* f : {(const void*)gemm_bf16_tn_8p<false, false>, (const void*)gemm_bf16_tn_8p<true, false>,
+                                  (const void*)gemm_bf16_tn_8p<false, true>, (const void*)gemm_bf16_tn_8p<true, true>})
+                (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
             attr8 = true;
         }
+        // 16-B epilogue accesses when every epilogue operand allows them (VS_GEMM_WIDE=0: 8-B, A/B)
+        const char* we = getenv("VS_GEMM_WIDE");
+        const bool wide = !(we && we[0] == '0') && n % 8 == 0 && ldc % 8 == 0 && aligned16(c) &&
+                          (!ep.bias || aligned16(ep.bias)) && (!ep.res || (ep.ld_res % 8 == 0 && aligned16(ep.res))) &&
+                          (!ep.gate || (ep.gate_bstride % 8 == 0 && aligned16(ep.gate))) &&
+                          (!ep.hint || (ep.ld_hint % 8 == 0 && aligned16(ep.hint)));
         KSplit sp = k2 ? KSplit{tm * tn, 0, 1, 0} : plan_ksplit(tm * tn, k / 64, vs_cus_for_split("VS_GEMM_NO_SPLIT"), 64);
         float* part = nullptr;
         if (sp.ntail) {
             part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
             if (!part) sp = KSplit{tm * tn, 0, 1, 0};
         }
-        hipLaunchKernelGGL(k2 ? gemm_bf16_tn_8p<true> : gemm_bf16_tn_8p<false>, dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)),
+        hipLaunchKernelGGL(k2 ? (wide ? gemm_bf16_tn_8p<true, true> : gemm_bf16_tn_8p<true, false>)
+                              : (wide ? gemm_bf16_tn_8p<false, true> : gemm_bf16_tn_8p<false, false>),
+                           dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)),
                            dim3(512), LDS8, (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw,
                            (bf16_t*)c, ldc, m, n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2, k2, ep, tm, tn,
                            sp.nmain, sp.ksplit, sp.piece_k, part);
