@@ -30,7 +30,8 @@ def main():
         if n.startswith(("Cijk", "Custom")):
             k = "hipBLASLt MT" + n.split("MT")[1].split("_")[0] + f" grid {r['Grid_Size_X']}"
         elif "attn_fwd" in n:
-            k = "attn_fwd_d128 self" if dur(r) > 5_000_000 else "attn_fwd_d128 cross"
+            k = ("attn_fwd_w4 self" if "attn_fwd_w4" in n else "attn_fwd_d128 self") if dur(r) > 5_000_000 \
+                else ("attn_fwd_w4 cross" if "attn_fwd_w4" in n else "attn_fwd_d128 cross")
         else:
             k = n.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         agg[k] += dur(r)

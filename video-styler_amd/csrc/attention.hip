@@ -35,15 +35,10 @@ constexpr int VROW = 320;        // LDS row pitch of the V tile (256 B + 64): tr
 constexpr int KT = BKV * KROW;   // 17408
 constexpr int VT = BKV * VROW;   // 20480
 constexpr int LDS_BYTES = 2 * (KT + VT);   // K ring 2 x 17408 + V ring 2 x 20480
-constexpr int QPRE_BYTES = 9 * NTHR * 16;  // persistent mode: next item's Q / previous item's O, lane-private
 constexpr int PERSIST_MIN_TILES = 8;
-// items of fewer key tiles prefetch Q / drain O inside the tile loop.  0: never -- measured on the
-// 14B shapes the synchronous item switch wins for long items (self-attention 31.0 -> 29.1 ms) and
-// ties or wins for the 8-tile cross-attention items too (0.935 -> 0.92 ms), profiles/r2/attn_pf_ab.log
-constexpr int PF_MAX_TILES = 0;
 #ifndef VS_ATTN_MFMA16_DEFAULT
 #define VS_ATTN_MFMA16_DEFAULT true
-#endif       // the Q prefetch spreads its 8 chunks over the first 8 tiles
+#endif
 
 
 
@@ -117,14 +112,13 @@ __device__ __forceinline__ f32x16_t mfma16g(bf16x8_t a, bf16x8_t b, f32x16_t c, 
 #define ATTN_STAMP(slot) do {} while (0)
 
 
-template <bool REBASE, bool M16, bool PF, int MODE>
+template <bool REBASE, bool M16, int MODE>
 __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
-    // PF (VS_ATTN_PF=1; the r2 persistent kernel): the next item's Q is prefetched and the finished
-    // item's O drained inside the first 8 tiles of each item (kernel comment at `tile`).  !PF
-    // (default): that per-tile code -- range-gated loads/stores and their descriptor arithmetic in
-    // every tile -- is compiled out; an item switch stores O and loads the next Q directly (one
-    // stall per item) while the K/V pipeline still runs across the boundary: -6 % self-attention
-    // time on the 14B shape.
+    // Persistent items: an item switch stores O and loads the next Q directly (one stall per item)
+    // while the K/V pipeline runs on across the boundary (r2 measured the alternative -- the next
+    // Q prefetched and O drained inside the first 8 tiles through range-gated loads / stores -- 6 %
+    // slower on the 14B self-attention: the per-tile descriptor arithmetic costs more than the
+    // stall; profiles/r2/attn_pf_ab.log).
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // NC: optimistic softmax (comment at NC_LMIN); M16 only
     // REDO: the checked kernel over the items the NC launch listed (grid-strided over the list)
@@ -323,12 +317,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
         load_k(ki * BKV);
         k_next();
     }
-    // persistent mode: the next item's Q (prescaled) and the previous item's O pass through here,
-    // 8 chunks of 16 B per lane at c * 8 KB + tid * 16 (each lane reads back only what it wrote:
-    // no barrier needed)
-    __shared__ __attribute__((aligned(16))) char qbuf_lds[QPRE_BYTES];
-    char* const qbuf = qbuf_lds;
-    int q0_nxt = 0;                 // the next item: Q rows (for the prefetch), its (b, h)
+    int q0_nxt = 0;                 // the next item: its Q rows and (b, h)
     int bh_nxt = n_items > 1 ? item_bh(1, q0_nxt) : 0;
     const bf16_t* qb_nxt = q_base(bh_nxt);
     q0_nxt += wave * 32;
@@ -769,7 +758,6 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
                 }
             }
     };
-    auto qslot = [&](int cidx) { return qbuf + cidx * (NTHR * 16) + tid * 16; };
 
     // One tile T of the flattened sequence (tile ti of item tj): B_{T-1} (QK(T) + the s[0] half's
     // exps), A_T (PV(T-1) + the s[1] half).  Tile 0 (no PV) is peeled out of the loop: with one
@@ -790,18 +778,11 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
         constexpr bool first0 = decltype(first_c)::value;
         const bool first = first0 || ti == 0;
         const int kv0 = ti * BKV;
-        const bool qpref = PF && tj + 1 < n_items && ti < PERSIST_MIN_TILES;
-        const bool odrain = PF && tj > 0 && ti < PERSIST_MIN_TILES;
         ATTN_STAMP(0);
         // each phase opens with the LDS store of the tile staged one phase earlier (its slot's last
         // reader finished before the barrier that opened this phase), then the next global loads
         if (T + 1 < Ttot) store_k((T + 1) & 1);      // K(T+1), loaded at the start of A_{T-1}
         load_v(kv0);
-        bf16x8_t qraw{};
-        if constexpr (PF)
-            qraw = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
-                make_rsrc(qb_nxt + (long long)q0_nxt * ldq, qpref ? (unsigned)(max(Sq - q0_nxt, 0) * ldq * 2) : 0u),
-                (unsigned)(qoff(ti & 7) * 2), 0, 0));
         qk(T & 1, kv0);
         ATTN_STAMP(1);
         phase_bar();
@@ -818,16 +799,10 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
         pv_softmax((T - 1) & 1, !first0);
         if (!first0 && ti == 0) {
             nc_flag(g0 + (tj - 1) * gstride);      // the finished item's row sums
-            if constexpr (PF) {
-                out_chunks([&](int cidx, u32x4_t w) __attribute__((always_inline)) {
-                    *reinterpret_cast<u32x4_t*>(qslot(cidx == 0 ? 8 : cidx)) = w;
-                });
-            } else {
-                bf16_t* op = ob_prev + (long long)q0_prev * ldo;
-                out_chunks([&](int cidx, u32x4_t w) __attribute__((always_inline)) {
-                    if (out_row_ok(q0_prev, cidx)) *reinterpret_cast<u32x4_t*>(op + ooff(cidx)) = w;
-                });
-            }
+            bf16_t* op = ob_prev + (long long)q0_prev * ldo;
+            out_chunks([&](int cidx, u32x4_t w) __attribute__((always_inline)) {
+                if (out_row_ok(q0_prev, cidx)) *reinterpret_cast<u32x4_t*>(op + ooff(cidx)) = w;
+            });
             // the new item starts from O = 0, l = 0
             lq[0] = 0.f;
             lq[1] = 0.f;
@@ -837,20 +812,6 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
-        }
-        if constexpr (PF) {
-            // chunk ti of the previous item's O (range 0 unless draining: the store is dropped)
-            const u32x4_t w = *reinterpret_cast<const u32x4_t*>(qslot(ti == 0 ? 8 : (ti & 7)));
-            __builtin_amdgcn_raw_buffer_store_b128(
-                __builtin_bit_cast(i32x4_t, w),
-                make_rsrc(ob_prev + (long long)q0_prev * ldo, odrain ? (unsigned)(max(Sq - q0_prev, 0) * ldo * 2) : 0u),
-                (unsigned)(ooff(ti & 7) * 2), 0, 0);
-        }
-        if (qpref) {
-            bf16x8_t qs;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) qs[j] = (__bf16)((float)qraw[j] * c);
-            *reinterpret_cast<bf16x8_t*>(qslot(ti)) = qs;
         }
         if constexpr (!NC) {
             const float rt0 = row_tot(0), rt1 = M16 ? row_tot(1) : rt0;
@@ -866,12 +827,7 @@ __global__ __launch_bounds__(NTHR) void attn_fwd_d128(const AttnArgs args) {
             // block); the V loader and the exact-path recompute follow the QK item, the K loader
             // is already on it
             ti = 0;
-            if constexpr (PF) {
-#pragma unroll
-                for (int s2 = 0; s2 < 8; ++s2) qf[s2] = *reinterpret_cast<const bf16x8_t*>(qslot(s2));
-            } else {
-                load_q(qb_nxt, q0_nxt);
-            }
+            load_q(qb_nxt, q0_nxt);
 #pragma unroll
             for (int i = 0; i < 16; ++i) negm[i] = 0.f;
             mq[0] = 0.f;
@@ -1074,25 +1030,17 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
             nc_cap = (int)std::min(cap, (long long)0x7fffffff);
         }
     }
-    const int lds = LDS_BYTES;      // + the kernel's static QPRE_BYTES Q buffer
+    const int lds = LDS_BYTES;
     const long long grid = (long long)npers + (long long)sp.ntail * sp.nsplit;
     AttnArgs args{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, bsq, bsk, bsv, bso,
                   ldq, ldk, ldv, ldo, part, flags, c, sq, skv, heads, nqb, sp.nmain, npers, sp.nsplit,
                   sp.piece_tiles, nc_cap};
-    // in-loop Q prefetch / O drain only for short items (VS_ATTN_PF=0|1 overrides)
-    const char* pf_env = getenv("VS_ATTN_PF");
-    const bool pf = pf_env ? pf_env[0] == '1' : nkv < PF_MAX_TILES;
-    auto pick = [&](int mode, bool pfv) -> void (*)(AttnArgs) {
+    auto pick = [&](int mode) -> void (*)(AttnArgs) {
         constexpr int C = MODE_CHK, N = MODE_NC, R = MODE_REDO;
-        if (mode == R)
-            return rebase ? attn_fwd_d128<true, true, false, R> : attn_fwd_d128<false, true, false, R>;
-        if (mode == N)
-            return pfv ? (rebase ? attn_fwd_d128<true, true, true, N> : attn_fwd_d128<false, true, true, N>)
-                       : (rebase ? attn_fwd_d128<true, true, false, N> : attn_fwd_d128<false, true, false, N>);
-        return pfv ? (m16 ? (rebase ? attn_fwd_d128<true, true, true, C> : attn_fwd_d128<false, true, true, C>)
-                          : (rebase ? attn_fwd_d128<true, false, true, C> : attn_fwd_d128<false, false, true, C>))
-                   : (m16 ? (rebase ? attn_fwd_d128<true, true, false, C> : attn_fwd_d128<false, true, false, C>)
-                          : (rebase ? attn_fwd_d128<true, false, false, C> : attn_fwd_d128<false, false, false, C>));
+        if (mode == R) return rebase ? attn_fwd_d128<true, true, R> : attn_fwd_d128<false, true, R>;
+        if (mode == N) return rebase ? attn_fwd_d128<true, true, N> : attn_fwd_d128<false, true, N>;
+        return m16 ? (rebase ? attn_fwd_d128<true, true, C> : attn_fwd_d128<false, true, C>)
+                   : (rebase ? attn_fwd_d128<true, false, C> : attn_fwd_d128<false, false, C>);
     };
     auto launch = [&](void (*kern)(AttnArgs), long long nblk, const AttnArgs& a) {
         static std::mutex mu;
@@ -1112,7 +1060,7 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
     const bool w4 = flags && (impl_env ? impl_env[0] == '4' : nkv >= 16);
     if (w4) {
         if (attn_w4_launch(args, rebase, (unsigned)grid, (hipStream_t)stream) != hipSuccess) return VS_E_LAUNCH;
-    } else if (!launch(pick(flags ? MODE_NC : MODE_CHK, pf), grid, args)) {
+    } else if (!launch(pick(flags ? MODE_NC : MODE_CHK), grid, args)) {
         return VS_E_LAUNCH;
     }
     if (sp.ntail) {
@@ -1131,7 +1079,7 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
         r.piece_tiles = 0;
         const long long rgrid = std::min<long long>(nwg, ncu > 0 ? ncu : 256);
         r.nmain = r.npers = (int)rgrid;
-        if (!launch(pick(MODE_REDO, false), rgrid, r)) return VS_E_LAUNCH;
+        if (!launch(pick(MODE_REDO), rgrid, r)) return VS_E_LAUNCH;
     }
     return VS_OK;
 }

@@ -426,9 +426,6 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
         for (int j = 0; j < 8; ++j) {                                   // A
             float pa = 0.f, pb = 0.f;
             rdK(kf1[j], T, 1, j);
-#ifdef VS_W4_DMA_A
-            if (j & 1) stage_piece(4 + (j >> 1));       // the V half of tile T+2's DMA (A/B build)
-#endif
             mfK1(kf0[j], j, s0, 0);
             fence();
             if (!FIRST) smp_e(s1p[0], 2 * j, pa, pb);
@@ -443,9 +440,6 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
         for (int j = 0; j < 8; ++j) {                                   // B
             float pa = 0.f, pb = 0.f;
             if (!FIRST) rdV(vfa[j], T - 1, j >> 2, j & 3);
-#ifdef VS_W4_DMA_B
-            if (j & 1) stage_piece(4 + (j >> 1));       // the V half of tile T+2's DMA (A/B build)
-#endif
             mfK1(kf1[j], j, s1c, 0);
             fence();
             if (!FIRST) smp_e(s1p[1], 2 * j, pa, pb);
@@ -474,11 +468,7 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
         sync(T);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {                                   // D
-#if defined(VS_W4_DMA_A) || defined(VS_W4_DMA_B)
-            if (!(i & 1)) stage_piece(i >> 1);             // the K half; the V half in the next A / B
-#else
             stage_piece(i);
-#endif
             rdK(kf0[i], T + 1, 0, i);
             if (!FIRST) mfV(vfb[i], p1, i >> 2, i & 3);
             fence();
@@ -514,14 +504,7 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
     fence();
     asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
     fence();
-#if defined(VS_W4_DMA_A) || defined(VS_W4_DMA_B)
-    stage_begin(2);                 // tile 2's K half; its V half goes out in iteration 0
-#pragma unroll
-    for (int i = 0; i < 4; ++i) stage_piece(i);
-    stage_next();
-#else
     stage(2);
-#endif
 #pragma unroll
     for (int i = 0; i < 8; ++i) rdK(kf0[i], 0, 0, i);
     int T = 0, q0 = 0;

@@ -545,11 +545,12 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
                     float v[8];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, acc[a][b][i][0][e]),
-                                                                         __builtin_bit_cast(unsigned, acc[a][b][i][1][e]),
-                                                                         false, false);
-                        v[e] = __builtin_bit_cast(float, (unsigned)sw[0]);
-                        v[4 + e] = __builtin_bit_cast(float, (unsigned)sw[1]);
+                        // (element first, then __float_as_uint: hipcc 7.2 folds __builtin_bit_cast of a
+                        // vector element to element 0 -- every swap then moved the same value)
+                        const float x = acc[a][b][i][0][e], y = acc[a][b][i][1][e];
+                        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+                        v[e] = __uint_as_float(sw[0]);
+                        v[4 + e] = __uint_as_float(sw[1]);
                     }
                     const int n = n0 + 128 * b + 32 * wc + nw;
                     if (m < M && n < N) epilogue_store_w<8>(v, m, n, C, ldc, ep);
