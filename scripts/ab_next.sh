@@ -3,8 +3,7 @@
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p gpurun_out
-bash scripts/ab_attn.sh dma dmaa dmab || exit 1
 for w in 1 0 1 0; do
-  echo "== VS_GEMM_WIDE=$w" | tee -a gpurun_out/gemm_wide_ab.log
-  VS_GEMM_WIDE=$w AB_VARIANTS=vstyler timeout -k 10 300 python -u tests/probes/gemm_ab.py 59280 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/gemm_wide_ab.log || exit 1
+  echo "== VS_GEMM_WIDE=$w" | tee -a gpurun_out/gemm_wide_ab2.log
+  VS_GEMM_WIDE=$w AB_VARIANTS=vstyler,lt timeout -k 10 300 python -u tests/probes/gemm_ab.py 59280 7410 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/gemm_wide_ab2.log || exit 1
 done
