@@ -111,7 +111,6 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
     auto o_base = [&](int bh) { const int H = cold->H; return cold->O + (long long)(bh / H) * cold->bso + (bh % H) * HD; };
 
     const int nkv = (Skv + BKV - 1) / BKV;
-    const int Ttot = n_items * nkv;
     const float npad = (float)(nkv * BKV - Skv);
 
     // ---- LDS-DMA loader: tile T of the flattened sequence into slot T & 3, two tiles ahead of QK.
