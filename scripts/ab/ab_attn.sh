@@ -1,5 +1,5 @@
 #!/bin/bash
-# scratch: interleaved same-box A/B of attention builds: scripts/ab_attn.sh <tag> <diag name>...
+# scratch: interleaved same-box A/B of attention builds: scripts/ab/ab_attn.sh <tag> <diag name>...
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p gpurun_out

@@ -1,6 +1,6 @@
 #!/bin/bash
 # scratch: timing of GEMM diagnostic builds (VSTYLER_LIB per build) on the 59280-row 14B shapes
-#   bash scripts/ab_gemm_diag.sh <variant for AB_VARIANTS> <diag name>...
+#   bash scripts/ab/ab_gemm_diag.sh <variant for AB_VARIANTS> <diag name>...
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p gpurun_out

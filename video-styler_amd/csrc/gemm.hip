@@ -900,9 +900,13 @@ bool vs_lt_is_private();
 // Ulysses per-rank row counts (same box, profiles/r3/gemm_stagger_ab_s2.log): FFN-down (K = 13824,
 // gate-residual) at 3705 / 7410 / 14820 rows 1.02x / 1.14x / 1.13x, FFN-up (GELU epilogue) at
 // 3705 / 7410 rows 1.04x / 1.10x; the library keeps everything else (q|k|v 0.80-0.85x, o-proj
-// 0.92-0.99x, and every 14B GEMM at the SP = 1 row count, 0.85-0.95x).
+// 0.92-0.99x, and every 14B GEMM at the SP = 1 row count, 0.85-0.95x).  With the 16-B epilogue the
+// o-proj (gate-residual, N = K = 5120) joins them at 7410 / 3705 rows: 0.336-0.339 vs 0.348-0.353 ms
+// and 0.189 vs 0.194 ms, four interleaved runs (profiles/r3/gemm_persist_ab.log); the library pays a
+// staging pass for a residual epilogue, so the rule keys on those.
 static bool own_wins(int m, int n, int k, int epilogue) {
-    return (k >= 12288 && m <= 16384) || (epilogue == VS_EPI_GELU && k <= 8192 && m <= 8192);
+    return (k >= 12288 && m <= 16384) || (epilogue == VS_EPI_GELU && k <= 8192 && m <= 8192) ||
+           ((epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES) && k <= 8192 && m <= 8192);
 }
 static bool lt_route(int m, int n, int k, int epilogue = VS_EPI_BIAS) {
     const char* e = getenv("VS_GEMM_BACKEND");

@@ -186,10 +186,13 @@ class ModelConfig:
 
 def sp_graph_ok(plan):
     """True when the sequence-parallel plan's collectives can be captured into the step's hipGraph:
-    device-side RCCL collectives (torch.distributed 'nccl' or libvstyler's vs_sp_*) -- not
-    host-staged substitutes (tests) -- and VSTYLER_SP_GRAPH=1.  Opt-in since r3: the world-1 RCCL
-    capture test stalled on MI355X (tests/probes/sp_graph_probe.py), so SP steps run eager by
-    default (the r2 behaviour) until the capture is proven on hardware."""
+    VSTYLER_SP_GRAPH=1 and RCCL through libvstyler's vs_sp_* on the capture stream
+    (VSTYLER_SP_COMM=native; NativeComm then runs its collectives on the caller's stream) -- not
+    torch.distributed's RCCL, whose process-group stream the capture does not survive on this
+    image's HIP (segfault in hipStreamEndCapture, profiles/r3/sp_graph_probe_faulthandler.log), and
+    not host-staged substitutes (tests).  Opt-in: it trades the exchange/compute overlap for the
+    launch savings, and only world size 1 has run on hardware (bit-identical replay,
+    test_ulysses_rccl_world1_graph_capture); SP steps run eager by default."""
     if os.environ.get("VSTYLER_SP_GRAPH", "0") != "1":
         return False
     if plan is None:

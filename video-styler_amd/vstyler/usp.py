@@ -87,7 +87,7 @@ class NativeComm:
     communicator is destroyed by close() or when the object is collected.  Selected with
     VSTYLER_SP_COMM=native."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, stream=None):
         from . import _lib
         self._lib = _lib
         lib = _lib.load()
@@ -102,7 +102,22 @@ class NativeComm:
         uid = ctypes.create_string_buffer(box[0], 128)
         self._check(lib.vs_sp_init(self.rank, self.world, uid, torch.cuda.current_device(),
                                    ctypes.byref(self.handle)))
-        self.stream = torch.cuda.Stream()
+        # stream="caller" (VSTYLER_SP_COMM_STREAM=caller; the default under VSTYLER_SP_GRAPH=1): the
+        # collectives run on the caller's stream, in order with the compute -- no exchange/compute
+        # overlap, but capturable: RCCL on a side stream forked into a hipGraph capture segfaults in
+        # hipStreamEndCapture on this image's HIP 7.0 (torch's ProcessGroupNCCL stream and this
+        # class's own alike; profiles/r3/sp_graph_probe_faulthandler.log), on the capture stream it
+        # captures and replays bit-identical (profiles/r3/sp_graph_probe_caller_stream.log)
+        if stream is None:
+            stream = os.environ.get("VSTYLER_SP_COMM_STREAM") or \
+                ("caller" if os.environ.get("VSTYLER_SP_GRAPH") == "1" else "side")
+        if stream not in ("caller", "side"):
+            raise ValueError(f"VSTYLER_SP_COMM_STREAM must be 'caller' or 'side', not {stream!r}")
+        self.stream = None if stream == "caller" else torch.cuda.Stream()
+
+    @property
+    def capturable(self):
+        return self.stream is None
 
     def _check(self, code):
         if code != 0:
@@ -117,6 +132,11 @@ class NativeComm:
         return nbytes // self.world
 
     def all_to_all(self, recv, send):
+        if self.stream is None:
+            self._check(self._lib.load().vs_sp_all_to_all(self.handle, send.data_ptr(), recv.data_ptr(),
+                                                          self._bytes_per_rank(send),
+                                                          torch.cuda.current_stream().cuda_stream))
+            return _Done()
         self.stream.wait_stream(torch.cuda.current_stream())
         self._check(self._lib.load().vs_sp_all_to_all(self.handle, send.data_ptr(), recv.data_ptr(),
                                                       self._bytes_per_rank(send), self.stream.cuda_stream))
@@ -126,6 +146,10 @@ class NativeComm:
 
     def all_gather(self, recv, send):
         cur = torch.cuda.current_stream()
+        if self.stream is None:
+            self._check(self._lib.load().vs_sp_all_gather(self.handle, send.data_ptr(), recv.data_ptr(),
+                                                          send.numel() * send.element_size(), cur.cuda_stream))
+            return
         self.stream.wait_stream(cur)
         self._check(self._lib.load().vs_sp_all_gather(self.handle, send.data_ptr(), recv.data_ptr(),
                                                       send.numel() * send.element_size(),
@@ -158,7 +182,12 @@ class UlyssesGroup:
     on the process group, default) or "native" (NativeComm: RCCL through libvstyler's vs_sp_* ABI);
     default from VSTYLER_SP_COMM."""
 
-    capturable = True       # device-side RCCL collectives: the step's hipGraph may capture them
+    @property
+    def capturable(self):
+        """The step's hipGraph may capture this plan's collectives: RCCL through vs_sp_* on the
+        caller's stream (NativeComm.capturable); torch.distributed's RCCL runs on the process
+        group's own stream, which the capture does not survive (NativeComm's comment)."""
+        return self.native is not None and self.native.capturable
 
     def __init__(self, group=None, force_collectives=False, comm=None):
         self.group = group
@@ -332,6 +361,11 @@ class CfgParallel:
         # the velocity exchange goes through the same comm kind as the Ulysses exchanges
         self.pair_native = NativeComm(self.pair_group) if comm == "native" else None
         self.collective_calls = 0
+
+    @property
+    def capturable(self):
+        """The velocity exchange is capturable as UlyssesGroup's (its sub-plans are checked apart)."""
+        return self.pair_native is not None and self.pair_native.capturable
 
     def gather_cfg(self, out_pair, out_local):
         """out_local [1, ...] of this rank's CFG sample -> out_pair [2, ...] (sample 0, sample 1)."""
