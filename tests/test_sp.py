@@ -296,6 +296,40 @@ def test_ulysses_rccl_world1_graph_capture():
         assert res[f"sp_graph_{comm}"] is True, res
 
 
+def _capturable_worker(port, q):
+    """gloo, world 1: which plans the SP hipGraph may capture (pipeline.sp_graph_ok)."""
+    try:
+        _init(0, 1, port)
+        from vstyler.pipeline import sp_graph_ok
+        from vstyler.usp import UlyssesGroup
+        from sp_util import CpuUlysses
+        torch_plan = UlyssesGroup(comm="torch")
+        os.environ["VSTYLER_SP_GRAPH"] = "1"
+        res = {"torch_plan": torch_plan.capturable, "torch_ok": sp_graph_ok(torch_plan),
+               "host_staged_ok": sp_graph_ok(CpuUlysses(None, None)), "no_plan_ok": sp_graph_ok(None)}
+        os.environ["VSTYLER_SP_GRAPH"] = "0"
+        res["opt_out_ok"] = sp_graph_ok(None)
+        torch.distributed.destroy_process_group()
+        q.put(res)
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(traceback.format_exc())
+
+
+def test_sp_graph_capturable_plans_cpu():
+    """torch.distributed plans (RCCL on the process group's stream; also the default plan that
+    sp_graph_ok falls back to when handed none) and host-staged substitutes are never captured,
+    and nothing is without VSTYLER_SP_GRAPH=1."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_capturable_worker, args=(_port(), q))
+    p.start()
+    res = q.get(timeout=120)
+    p.join(30)
+    assert res == {"torch_plan": False, "torch_ok": False, "host_staged_ok": False, "no_plan_ok": False,
+                   "opt_out_ok": False}, res
+
+
 # ------------------------------------------------------------------ CFG parallelism x Ulysses
 def _cfg_cpu_worker(rank, world, port, q):
     """gloo, world 4: the CfgParallel plan's rank mapping and subgroups (halves = Ulysses groups,
