@@ -4,7 +4,7 @@ data stands in for every peer, so the numbers are garbage; the work and the byte
 are the real ones).  Bounds the SP speedup the 8-GPU run can reach: t(SP=1) / t(rank, SP=P).
   python tests/probes/sp_rank_compute.py [P ...]
 SPC_SIZE=720p: BASELINE C4's 1280x720x121 (latent 31 x 90 x 160, S = 111 600) instead of 832x480x73;
-SPC_REPS: timed repetitions (default 3)."""
+SPC_REPS: timed repetitions (default 3); SPC_GRAPH=1: eager vs hipGraph replay of the per-rank step."""
 import os, sys, time
 ROOT = os.path.join(os.path.dirname(__file__), "..", "..")
 sys.path.insert(0, os.path.join(ROOT, "video-styler_amd"))
@@ -63,6 +63,35 @@ if AB:
             res[v].append(1000 * min(ts))
     for v, ms in res.items():
         print(f"SP={P} {var}={v}: per-rank CFG step " + " ".join(f"{x:.1f}" for x in ms) + " ms", flush=True)
+    sys.exit(0)
+if os.environ.get("SPC_GRAPH") == "1":
+    # the per-rank step eager vs hipGraph-replayed (the exchanges are device copies on the caller's
+    # stream, so the step is capturable as with vs_sp_* under VSTYLER_SP_GRAPH=1): the launch cost
+    # the SP graph removes, interleaved rounds on one stream
+    for a in sys.argv[1:] or ["8"]:
+        P = int(a)
+        sp = LocalUlysses(P, overlap=OVL) if P > 1 else None
+        fn = lambda: model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=ctx, vace_context=vc,
+                                        use_unified_sequence_parallel=sp is not None, sp_group=sp)
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            fn(); fn()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                fn()
+            torch.cuda.synchronize()
+            res = {"eager": [], "graph": []}
+            for rnd in range(REPS):
+                for mode in res:
+                    t0 = time.perf_counter()
+                    (g.replay() if mode == "graph" else fn())
+                    torch.cuda.synchronize()
+                    res[mode].append(1000 * (time.perf_counter() - t0))
+        print(f"SP={P} overlap={OVL}: per-rank CFG step eager " + " ".join(f"{x:.1f}" for x in res["eager"]) +
+              " ms | graph " + " ".join(f"{x:.1f}" for x in res["graph"]) + " ms", flush=True)
+        del g
     sys.exit(0)
 # args: P = Ulysses over P ranks (both CFG samples per rank); cU = CFG parallelism x Ulysses over u
 # ranks (world 2u): a rank's work is its CFG sample's batch-1 forward sharded over u (+ one velocity
