@@ -369,25 +369,29 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
     const __amdgpu_buffer_rsrc_t rw = rsrc(W + (long long)n0 * ldw + kb);
     const int alim = M - 1 - m0, wlim = N - 1 - n0;
     const unsigned ldab = (unsigned)(lda * 2), ldwb = (unsigned)(ldw * 2);
-    // stage half-tile `which` (0 A0, 1 A1, 2 B0, 3 B1) of K-tile t into buffer t & 1.  The two row
-    // offsets are formed here from two live VGPRs (row, chunk) -- kept opaque so the compiler does
-    // not hoist eight loop-invariant offsets into registers the fragment prefetch needs
+    // stage half-tile `which` (0 A0, 1 A1, 2 B0, 3 B1) of K-tile t into buffer t & 1
+    // the eight DMA row offsets (half-tile x piece; the K offset goes in soffset) computed once and
+    // held in VGPRs across the K loop: forming them per stage cost a 32-bit multiply (v_mad_u64_u32),
+    // a clamp and an add per LDS-DMA instruction -- hoisted, +4-5 % on every 14B shape at 59 280 and
+    // 7410 rows, 4 more VGPRs (profiles/r3/gemm_preoff_ab.log)
+    unsigned voff[4][2];
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int r = (w & 1) * 128 + prow + 8 * j;
+            voff[w][j] = w >= 2 ? (unsigned)min(r, wlim) * ldwb + pcol : (unsigned)min(r, alim) * ldab + pcol;
+        }
     auto stage = [&](int t, int which) {
         char* dst = smem + hoff(which, t & 1) + wave * 2048;
         const bool isw = which >= 2;
         const int h = which & 1;
         if (!LORA || t < nk1) {
             const unsigned ko = (unsigned)t * 128u;
-            int pr = prow;
-            unsigned pc = pcol;
-            asm volatile("" : "+v"(pr), "+v"(pc));
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int r = h * 128 + pr + 8 * j;
-                const unsigned vo = isw ? (unsigned)min(r, wlim) * ldwb + pc : (unsigned)min(r, alim) * ldab + pc;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(isw ? rw : ra, (LDS_AS void*)(dst + j * 1024), 16, vo, ko,
-                                                         0, 0);
-            }
+            for (int j = 0; j < 2; ++j)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(isw ? rw : ra, (LDS_AS void*)(dst + j * 1024), 16,
+                                                         voff[which][j], ko, 0, 0);
         } else {
             // second K phase (un-merged LoRA): A2 . W2^T, rank-sized, addresses formed here
             const unsigned ko = (unsigned)(t - nk1) * 128u;
@@ -904,6 +908,12 @@ bool vs_lt_is_private();
 // o-proj (gate-residual, N = K = 5120) joins them at 7410 / 3705 rows: 0.336-0.339 vs 0.348-0.353 ms
 // and 0.189 vs 0.194 ms, four interleaved runs (profiles/r3/gemm_persist_ab.log); the library pays a
 // staging pass for a residual epilogue, so the rule keys on those.
+// With the DMA row offsets hoisted (+4-5 %, profiles/r3/gemm_preoff_ab.log) the kernel also passes
+// the library + its epilogue pass in isolation at the SP = 1 row count on FFN-up (6.150 vs 6.205
+// ms) and FFN-down (5.948 vs 6.018), but routing those two to it cost the graph-replayed step 1.4 %
+// (0.3831 / 0.3843 vs 0.3888 / 0.3894 steps/s, same box, interleaved; in the step the kernel ran
+// 6.38 ms per launch: profiles/r3/bench_own_sp1_ab.log, step_breakdown_own_sp1.txt), so the SP = 1
+// block GEMMs stay on the library.
 static bool own_wins(int m, int n, int k, int epilogue) {
     return (k >= 12288 && m <= 16384) || (epilogue == VS_EPI_GELU && k <= 8192 && m <= 8192) ||
            ((epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES) && k <= 8192 && m <= 8192);
