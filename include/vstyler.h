@@ -89,7 +89,8 @@ int vs_gemm_route(int m, int n, int k);
  * x8 = e4m3fn(x / (s + 1e-8)) (OCP e4m3, round-to-nearest-even); vs_gemm_fp8 computes
  * C = epilogue(s[m] * (A8 . W8^T)) with unscaled e4m3 weights W8 [N][K] (scale_b = 1, as the
  * reference) and the same epilogues as vs_gemm (bias added in fp32 before the single bf16 rounding,
- * as torch._scaled_mm).  K % 64 == 0, N % 4 == 0, lda/ldw multiples of 16 bytes.
+ * as torch._scaled_mm).  K % 128 == 0 on every route (the MFMA kernel's K-tile is 128 fp8; the 14B
+ * shapes K = 5120 / 13824 qualify), N % 4 == 0, lda/ldw multiples of 16 bytes.
  */
 int vs_quant_fp8_rows(const void* x, long long ldx, void* x8, long long ld8, float* scale, int rows, int cols,
                       void* stream);

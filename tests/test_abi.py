@@ -43,6 +43,15 @@ def test_invalid_arguments_rejected_before_launch():
     # null pointers
     assert lib.vs_gemm(None, 64, None, 64, None, 64, 8, 8, 64, 0, ep, None, 0, None, 0, 0, None) == 1
     fake = 1 << 20   # aligned non-null (never dereferenced: validation fails first)
+    # fp8: K must be a multiple of 128 on every backend (K = 192 rejected up front, whichever route
+    # VS_FP8_BACKEND selects), and 256 passes validation only to fail on the null scale vector
+    for backend in ("lt", "vstyler"):
+        os.environ["VS_FP8_BACKEND"] = backend
+        try:
+            assert lib.vs_gemm_fp8(fake, 192, fake, fake, 192, fake, 8, 8, 8, 192, 0, ep, None) == 1
+            assert lib.vs_gemm_fp8(fake, 256, None, fake, 256, fake, 8, 8, 8, 256, 0, ep, None) == 1
+        finally:
+            del os.environ["VS_FP8_BACKEND"]
     # K not a multiple of 64
     assert lib.vs_gemm(fake, 48, fake, 48, fake, 8, 8, 8, 48, 0, ep, None, 0, None, 0, 0, None) == 1
     # bad epilogue id

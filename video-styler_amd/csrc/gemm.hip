@@ -642,7 +642,9 @@ __global__ __launch_bounds__(512, 2) void gemm_fp8_tn_8p(
     const __amdgpu_buffer_rsrc_t rw = rsrc(W + (long long)n0 * ldw + kb);
     const unsigned pcol = 16u * ((lane & 7) ^ (lane >> 3));
     const int alim = M - 1 - m0, wlim = N - 1 - n0;
-    // row offsets formed per stage from two opaque VGPRs (see gemm_bf16_tn_8p)
+    // row offsets formed per stage from two opaque VGPRs (kept for the fragment prefetch's registers;
+    // a variant holding the eight offsets across the K loop compiles without spills but has not been
+    // A/B-tested on a GPU yet: scripts/ab/ab_fp8_preoff.sh)
     auto stage = [&](int t, int which) {
         char* dst = smem + hoff(which, t & 1) + wave * 2048;
         const bool isw = which >= 2;
@@ -1084,7 +1086,8 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
                            void* c, long long ldc, int m, int n, int k, int epilogue, const vs_epilogue* epi,
                            void* stream) {
     if (!a8 || !scale_a || !w8 || !c || m <= 0 || n <= 0 || k <= 0) return VS_E_INVALID;
-    if (k % 64 || n % 4 || lda < k || ldw < k || ldc < n || (lda & 15) || (ldw & 15) || (ldc & 3))
+    // K % 128 on both routes (the MFMA kernel's K-tile), so a shape never works on one backend only
+    if (k % 128 || n % 4 || lda < k || ldw < k || ldc < n || (lda & 15) || (ldw & 15) || (ldc & 3))
         return VS_E_INVALID;
     if (!aligned16(a8) || !aligned16(w8) || !aligned8(c)) return VS_E_INVALID;
     Epi ep;
@@ -1107,7 +1110,6 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
         }))
         return VS_OK;
     // the fp8 8-phase MFMA kernel (K-tiles of 128 fp8)
-    if (k % 128) return VS_E_INVALID;
     const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
     static bool attr8 = false;
     if (!attr8) {

@@ -147,7 +147,7 @@ def gemm_fp8(a8, scale_a, w8, out, epilogue=VS_EPI_BIAS, bias=None, residual=Non
         raise ValueError(f"gemm_fp8 shape mismatch a8={tuple(a8.shape)} w8={tuple(w8.shape)} out={tuple(out.shape)}")
     ep = _epilogue(bias, residual, gate, gate_bstride, hint, hint_scale, alpha, rows_per_batch)
     _split_ws(1, a8)                                                    # split tail of the MFMA kernel
-    if not os.environ.get("VS_FP8_BACKEND", "").startswith(("v", "p")):   # hipBLASLt route (vs_gemm_fp8)
+    if not os.environ.get("VS_FP8_BACKEND", "").startswith("v"):   # hipBLASLt route (vs_gemm_fp8's own test)
         _split_ws(2, a8)
         if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES):
             _split_ws(3, a8, M * N * 2)

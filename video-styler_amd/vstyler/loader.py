@@ -20,6 +20,7 @@ WAN_COMMON = dict(in_dim=16, out_dim=16, text_dim=4096, freq_dim=256, eps=1e-6, 
 VACE_14B_HASH = "3b2726384e4f64837bdf216eea3f310d"
 VACE_14B = dict(vace_layers=(0, 5, 10, 15, 20, 25, 30, 35), vace_in_dim=96, patch_size=(1, 2, 2),
                 dim=5120, num_heads=40, ffn_dim=13824, eps=1e-6)
+MAIN_LAYERS_BY_DIM = {1536: 30, 5120: 40}
 VACE_DEFAULT = dict(vace_layers=tuple(range(0, 30, 2)), vace_in_dim=96, patch_size=(1, 2, 2),
                     dim=1536, num_heads=12, ffn_dim=8960, eps=1e-6)   # VaceWanModel() defaults
 
@@ -144,6 +145,13 @@ def build_vace(state_dict, device, num_layers=None):
             _n_blocks(sd, "vace_blocks") == len(VACE_DEFAULT["vace_layers"]):
         cfg = VACE_DEFAULT
     else:
+        if not num_layers:
+            # the main-block count fixes the injection spacing; without the DiT it is known only for
+            # the two published widths (wan_video_dit.py:509-536: 1536 -> 30 blocks, 5120 -> 40)
+            num_layers = MAIN_LAYERS_BY_DIM.get(sd["vace_patch_embedding.weight"].shape[0])
+            if not num_layers:
+                raise ValueError("VACE module of an unlisted layout and width: load it together with its DiT "
+                                 "so the injection layers follow the DiT's block count")
         cfg = vace_config_from_shapes(sd, num_layers)
     model = VaceWanModel(device=device, **cfg)
     model.load_state_dict({k: v.to(torch.bfloat16) for k, v in sd.items()}, strict=True)
@@ -170,16 +178,38 @@ def build_vae(state_dict, device):
 T5_HASH = "9c8818c2cbea55eca56c7b447df170da"   # configs/model_config.py:161 (WanTextEncoder)
 
 
-def build_text_encoder(state_dict, device):
-    if hash_state_dict_keys(state_dict) != T5_HASH:
+def t5_config_from_shapes(sd):
+    """The WanTextEncoder config of a UMT5 key set the hash table does not list (other widths, the
+    tiny test checkpoints), read off the shapes of wan_video_text_encoder.py:209-252's layout
+    (shared_pos=False, head_dim 64).  None when the layout is not that encoder's."""
+    need = ("token_embedding.weight", "norm.weight", "blocks.0.attn.q.weight", "blocks.0.ffn.fc1.weight",
+            "blocks.0.pos_embedding.embedding.weight")
+    if not all(k in sd for k in need):
         return None
+    vocab, dim = sd["token_embedding.weight"].shape
+    dim_attn = sd["blocks.0.attn.q.weight"].shape[0]
+    num_buckets, num_heads = sd["blocks.0.pos_embedding.embedding.weight"].shape
+    if dim_attn != 64 * num_heads:
+        return None
+    return dict(vocab=vocab, dim=dim, dim_attn=dim_attn, dim_ffn=sd["blocks.0.ffn.fc1.weight"].shape[0],
+                num_heads=num_heads, num_layers=_n_blocks(sd, "blocks"), num_buckets=num_buckets)
+
+
+def build_text_encoder(state_dict, device):
+    if hash_state_dict_keys(state_dict) == T5_HASH:
+        cfg = {}
+    else:
+        cfg = t5_config_from_shapes(state_dict)
+        if cfg is None:
+            return None
     from .t5 import WanTextEncoder
-    return WanTextEncoder(device=device).load_state_dict(state_dict)
+    return WanTextEncoder(device=device, **cfg).load_state_dict(state_dict)
 
 
 def load_models(paths, device="cuda"):
     """Returns {'wan_video_dit': WanModel, 'wan_video_vace': VaceWanModel, ...} for the files given."""
     out = {}
+    vace_only = []
     for path in paths:
         sd = normalize_keys(load_state_dict(path, device="cpu"))
         vae = build_vae(sd, device)
@@ -191,8 +221,9 @@ def load_models(paths, device="cuda"):
             out["wan_video_text_encoder"] = te
             continue
         if sd and all(k.startswith("vace") for k in sd):
-            # a VACE-module-only file (the ComfyUI workflow's WanVideoVACEModelSelect input)
-            out["wan_video_vace"] = build_vace(sd, device)
+            # a VACE-module-only file (the ComfyUI workflow's WanVideoVACEModelSelect input): built
+            # once every file is read, with the DiT's block count when a DiT came with it
+            vace_only.append(sd)
             continue
         dit = build_dit(sd, device)
         if dit is not None:
@@ -202,4 +233,7 @@ def load_models(paths, device="cuda"):
                 out["wan_video_vace"] = vace
             continue
         raise NotImplementedError(f"unrecognised checkpoint {path} (hash {hash_state_dict_keys(sd)})")
+    dit = out.get("wan_video_dit")
+    for sd in vace_only:
+        out["wan_video_vace"] = build_vace(sd, device, num_layers=len(dit.blocks) if dit is not None else None)
     return out

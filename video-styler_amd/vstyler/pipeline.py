@@ -184,6 +184,31 @@ class ModelConfig:
         self.path = files[0] if len(files) == 1 else files
 
 
+# wan_video_new.py:352-363: the files every Wan2.1 release ships identically are read from one
+# model_id, so a ./models tree laid out by the reference's downloads holds them only there
+REDIRECT_COMMON_FILES = {
+    "models_t5_umt5-xxl-enc-bf16.pth": "Wan-AI/Wan2.1-T2V-1.3B",
+    "Wan2.1_VAE.pth": "Wan-AI/Wan2.1-T2V-1.3B",
+    "models_clip_open-clip-xlm-roberta-large-vit-huge-14.pth": "Wan-AI/Wan2.1-I2V-14B-480P",
+}
+
+
+def redirect_model_configs(model_configs):
+    """Rewrites model_id in place for the common files, with the reference's notice
+    (wan_video_new.py:352-363).  Configs without a model_id or file pattern are left alone."""
+    for mc in model_configs:
+        if mc.origin_file_pattern is None or mc.model_id is None:
+            continue
+        if not isinstance(mc.origin_file_pattern, str):
+            continue
+        target = REDIRECT_COMMON_FILES.get(mc.origin_file_pattern)
+        if target is not None and mc.model_id != target:
+            print(f"To avoid repeatedly downloading model files, ({mc.model_id}, {mc.origin_file_pattern}) is "
+                  f"redirected to ({target}, {mc.origin_file_pattern}). You can use `redirect_common_files=False` "
+                  "to disable file redirection.")
+            mc.model_id = target
+
+
 def sp_graph_ok(plan):
     """True when the sequence-parallel plan's collectives can be captured into the step's hipGraph:
     VSTYLER_SP_GRAPH=1 and RCCL through libvstyler's vs_sp_* on the capture stream
@@ -239,15 +264,31 @@ class DenoiseStepper:
 
     def capture(self):
         g = torch.cuda.CUDAGraph()
+        err = None
         try:
             with torch.cuda.graph(g, stream=self.stream):
                 self.step_fn(self.t_buf, self.d_buf)
         except Exception as e:      # e.g. a collective backend that cannot be captured: stay eager
+            err = e
+        # the decision is collective: with several ranks replaying graphs whose collectives must
+        # pair up, one rank falling back to eager steps while the others replay would deadlock or
+        # mismatch, so every rank keeps its graph only if every rank captured one
+        if not self._all_ranks_agree(err is None):
             import warnings
-            warnings.warn(f"hipGraph capture of the denoising step failed ({e!r}); running eager steps")
+            why = repr(err) if err is not None else "another rank's capture failed"
+            warnings.warn(f"hipGraph capture of the denoising step failed ({why}); running eager steps")
             self.use_graph = False
             return
         self.graph = g
+
+    def _all_ranks_agree(self, ok):
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return ok
+        dev = self.t_buf.device if dist.get_backend() == "nccl" else torch.device("cpu")
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return bool(flag.item())
 
 
 class WanVideoPipeline:
@@ -282,6 +323,8 @@ class WanVideoPipeline:
                         audio_processor_config=None, redirect_common_files=True, use_usp=False):
         """wan_video_new.py:341-413 (local files only)."""
         from .loader import load_models
+        if redirect_common_files:
+            redirect_model_configs(model_configs)
         pipe = WanVideoPipeline(device=device, torch_dtype=torch_dtype)
         if use_usp:
             pipe.initialize_usp()
