@@ -1,5 +1,6 @@
-"""A/B: the hand-written staggered 8-phase GEMM (vstyler) vs the hipBLASLt route (lt, + its epilogue
-pass), per 14B block GEMM with its real epilogue; interleaved rounds, one process.  A third build
+"""A/B: the hand-written staggered 8-phase GEMM (vstyler), the 4-wave kernel (w4) and the hipBLASLt
+route (lt, + its epilogue pass), per 14B block GEMM with its real epilogue; interleaved rounds, one
+process (AB_VARIANTS=vstyler,w4,lt).  A third build
 can join with AB_VARIANTS=vstyler,lt,diag:<path to libvstyler.so> (not loaded here: run per build).
 usage: gemm_ab.py [M ...]"""
 import os, sys
@@ -35,6 +36,7 @@ for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
         def setv(v):
             os.environ["VS_GEMM_BACKEND"] = "lt" if v == "lt" else "vstyler"
             os.environ["VSTYLER_GEMM_TILE"] = "256"
+            os.environ["VS_GEMM_KERNEL"] = "4w" if v == "w4" else "8p"
         t = {v: [] for v in VARIANTS}
         for v in VARIANTS:             # warm (hipBLASLt autotune happens here)
             setv(v); K.gemm(a, w, out, **kw); torch.cuda.synchronize()
@@ -45,5 +47,5 @@ for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
         s = "  ".join(f"{v} {min(t[v]):.3f} ms ({fl / min(t[v]) / 1e9:.0f} TF/s)" for v in VARIANTS)
         print(f"M={M} {name:8s} N={N} K={Kd}: {s}", flush=True)
         del a, w, b, gate, x, out
-for k in ("VS_GEMM_BACKEND", "VSTYLER_GEMM_TILE"):
+for k in ("VS_GEMM_BACKEND", "VSTYLER_GEMM_TILE", "VS_GEMM_KERNEL"):
     os.environ.pop(k, None)

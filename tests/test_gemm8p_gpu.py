@@ -1,5 +1,5 @@
-"""The 256x256 8-phase GEMM (gemm_bf16_tn_8p, csrc/gemm.hip) through vs_gemm, forced onto the
-hand-written kernel (VS_GEMM_BACKEND=vstyler, VSTYLER_GEMM_TILE=256).
+"""The 256x256 GEMMs (gemm_bf16_tn_8p and gemm_bf16_tn_4w, csrc/gemm.hip) through vs_gemm, forced
+onto the hand-written kernels (VS_GEMM_BACKEND=vstyler, VSTYLER_GEMM_TILE=256, VS_GEMM_KERNEL).
 
 Integer-valued operands keep every fp32 sum exact, so every output must equal the exact product
 bit for bit (through each epilogue's reference rounding points, oracle/wan_oracle.py) for:
@@ -18,10 +18,13 @@ from gpu_util import BF16
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture
-def K(monkeypatch):
+@pytest.fixture(params=["8p", "4w"])
+def K(monkeypatch, request):
+    """Both 256x256 kernels: gemm_bf16_tn_8p and gemm_bf16_tn_4w (VS_GEMM_KERNEL); the LoRA second
+    phase always runs on the 8-phase kernel."""
     monkeypatch.setenv("VS_GEMM_BACKEND", "vstyler")
     monkeypatch.setenv("VSTYLER_GEMM_TILE", "256")
+    monkeypatch.setenv("VS_GEMM_KERNEL", request.param)
     from vstyler import kernels
     return kernels
 
@@ -31,7 +34,7 @@ def ints(*shape, g, lo=-3, hi=4):
 
 
 @pytest.mark.parametrize("M,N,Kd", [(256, 256, 64), (300, 260, 128), (513, 256, 192), (256, 520, 256),
-                                    (700, 300, 320), (257, 1000, 384), (1024, 512, 5120)])
+                                    (700, 300, 320), (257, 1000, 384), (1024, 512, 5120), (512, 768, 13824)])
 def test_gemm8p_integer_exact(K, M, N, Kd):
     g = torch.Generator(device="cuda").manual_seed(M * 7 + Kd)
     a, w = ints(M, Kd, g=g), ints(N, Kd, g=g)

@@ -1,0 +1,121 @@
+"""Parity at the three production shapes VERDICT r3 found unchecked (its 'What's weak' 1), with the
+machinery of test_production_model_gpu.py (oracle through torch's GPU ops, fp32 and fp64
+accumulation; the product within NOISE_X times that noise floor):
+
+  * C5 (config 5): Wan2.1-14B dims at 832x480x73, ONE main DiT block + ONE VACE block, CFG batch 2,
+    a rank-32 CausVid-style LoRA (kohya lora_down/lora_up/alpha keys) merged into the DiT block,
+    then every block Linear as AutoWrappedLinear.fp8_linear (vram_management/layers.py:115-151:
+    per-row activation scale, e4m3fn weights), VACE strength 0.975 -- on BOTH fp8 routes
+    (VS_FP8_BACKEND lt = hipBLASLt fp8, vstyler = the hand-written gemm_fp8_tn_8p);
+  * C4: Wan2.1-VACE-14B block pair at 1280x720x121 (S = 111 600, 2 x 111 600 = 223 200 GEMM rows:
+    every block GEMM route and split plan at that M);
+  * VAE: tiled encode and decode at 480x832 with the real 3x3 grid of 30x52-latent tiles (stride
+    15x26, wan_video_vae.py:1103-1203) at the Wan2.1 widths, 5 frames (two latent frames: the causal
+    cache path), vs the CPU oracle (oracle/wan_vae_oracle.py).
+"""
+import pytest
+import torch
+
+from gpu_util import BF16, err
+from oracle import wan_oracle as O
+from test_production_model_gpu import NOISE_X, build, floor_check, gpu_weights, inputs, oracle_both
+
+pytestmark = pytest.mark.gpu
+LORA_TARGETS = [f"{a}.{l}" for a in ("self_attn", "cross_attn") for l in "qkvo"] + ["ffn.0", "ffn.2"]
+
+
+def causvid_lora(cfg, rank, alpha, seed):
+    """A CausVid-style LoRA for block 0 of the DiT in the kohya layout the ComfyUI workflow loads
+    (diffusion_model.<name>.lora_down / lora_up / alpha)."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    D, F = cfg["dim"], cfg["ffn_dim"]
+    sd = {}
+    for t in LORA_TARGETS:
+        out_f, in_f = {"ffn.0": (F, D), "ffn.2": (D, F)}.get(t, (D, D))
+        base = f"diffusion_model.blocks.0.{t}"
+        sd[base + ".lora_down.weight"] = (0.02 * torch.randn(rank, in_f, generator=g, device="cuda")).to(BF16)
+        sd[base + ".lora_up.weight"] = (0.02 * torch.randn(out_f, rank, generator=g, device="cuda")).to(BF16)
+        sd[base + ".alpha"] = torch.tensor(float(alpha))
+    return sd
+
+
+@pytest.mark.parametrize("backend", ["lt", "vstyler"])
+def test_c5_14b_fp8_block_pair_causvid_lora_832x480x73(backend, monkeypatch):
+    from vstyler import model_fn_wan_video
+    from vstyler.lora import merge_lora, normalize_lora_keys
+    from vstyler.loader import normalize_keys
+    from vstyler.models import quantize_fp8_
+    monkeypatch.setenv("VS_FP8_BACKEND", backend)
+    cfg = dict(O.WAN_CONFIGS["14B"], num_layers=1, vace_layers=(0,))
+    W = gpu_weights(cfg, seed=17)
+    dit, vace = build(cfg, W)
+    rank, alpha = 32, 16.0
+    lora = normalize_lora_keys(normalize_keys(causvid_lora(cfg, rank, alpha, seed=18)))
+    assert merge_lora(dit, lora, alpha=1.0) == len(LORA_TARGETS)
+    assert quantize_fp8_(dit) + quantize_fp8_(vace) == 20
+    # oracle: GeneralLoRALoader's bf16 merge (B scaled by alpha / rank as the kohya layout means it)
+    Wm = dict(W)
+    for t in LORA_TARGETS:
+        key = f"blocks.0.{t}.weight"
+        la, lb = lora[f"blocks.0.{t}.lora_A.weight"], lora[f"blocks.0.{t}.lora_B.weight"]
+        Wm[key] = O.lora_merge(W[key], lb, la, 1.0)
+        assert torch.equal(dit.state_dict()[key], Wm[key])
+    lat, ctx, vc = inputs(cfg, 2)
+    t = torch.tensor([937.5], device="cuda").to(BF16)
+    out = model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=ctx, vace_context=vc,
+                             vace_scale=0.975)
+    torch.cuda.synchronize()
+    old = O.FP8_BLOCK_LINEARS
+    O.FP8_BLOCK_LINEARS = True
+    try:
+        ref32, ref64 = oracle_both(lambda: O.model_fn(Wm, cfg, torch.cat([lat, lat]), t.expand(2), ctx,
+                                                      torch.cat([vc, vc]), vace_scale=0.975))
+    finally:
+        O.FP8_BLOCK_LINEARS = old
+    # fp8 re-quantisation turns the fp32/fp64 differences into e4m3 rounding flips, as in the tiny
+    # fp8 model test (test_fp8_gpu.py): the same 1.5x floor plus that test's absolute slack
+    o, r, r64 = out.float(), ref32.float(), ref64.float()
+    mx, rl = (o - r).abs().max().item(), ((o - r).norm() / r.norm()).item()
+    fmx, frl = (r - r64).abs().max().item(), ((r - r64).norm() / r64.norm()).item()
+    print(f"C5 fp8 ({backend}) 14B 1+1 blocks 832x480x73 CFG2, CausVid LoRA r32 merged: max-abs {mx:.4g} "
+          f"rel-L2 {rl:.4g} (noise floor {fmx:.4g} / {frl:.4g})")
+    assert rl <= NOISE_X * frl + 2e-3 and mx <= NOISE_X * fmx + 2e-2, (mx, rl, fmx, frl)
+
+
+def test_c4_14b_block_pair_1280x720x121():
+    from vstyler import model_fn_wan_video
+    cfg = dict(O.WAN_CONFIGS["14B"], num_layers=1, vace_layers=(0,))
+    W = gpu_weights(cfg, seed=27)
+    dit, vace = build(cfg, W)
+    lat, cp, cn, vc = O.synthetic_inputs(cfg, 121, 720, 1280)
+    assert lat.shape == (1, 16, 31, 90, 160)
+    lat, ctx, vc = lat.cuda(), torch.cat([cp, cn]).cuda(), vc.cuda()
+    t = torch.tensor([875.0], device="cuda").to(BF16)
+    out = model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=ctx, vace_context=vc)
+    torch.cuda.synchronize()
+    del dit, vace
+    ref32, ref64 = oracle_both(lambda: O.model_fn(W, cfg, torch.cat([lat, lat]), t.expand(2), ctx,
+                                                  torch.cat([vc, vc])))
+    floor_check(out, ref32, ref64, "C4 14B 1+1 blocks 1280x720x121 CFG2 (223 200 GEMM rows)")
+
+
+def test_vae_tiled_encode_decode_480x832_3x3_tiles():
+    from oracle import wan_vae_oracle as V
+    from test_vae_gpu import _floor, _model, _within_floor
+    from vae_util import synthetic_video
+    from vstyler.vae import WanVideoVAE
+    W = V.random_vae_weights(seed=31)
+    video = synthetic_video(5, 480, 832)
+    ts, st = (30, 52), (15, 26)
+    assert len(WanVideoVAE.tile_tasks(60, 104, ts, st)) == 9
+    m = _model(V.VAE_CONFIG, W)
+    got = m.encode(video.cuda(), "cuda", tiled=True, tile_size=ts, tile_stride=st)
+    ref, floor = _floor(lambda: V.tiled_encode(video, W, ts, st))
+    assert got.shape == ref.shape == (1, 16, 2, 60, 104)
+    print(f"VAE tiled encode 480x832x5 (3x3 tiles): {err(got, ref)} floor {floor}")
+    _within_floor(got, ref, floor)
+    zgot = m.decode(ref.cuda(), "cuda", tiled=True, tile_size=ts, tile_stride=st)
+    zref, zfloor = _floor(lambda: V.tiled_decode(ref, W, ts, st))
+    assert zgot.shape == zref.shape == (1, 3, 5, 480, 832)
+    print(f"VAE tiled decode 480x832x5 (3x3 tiles): {err(zgot, zref)} floor {zfloor}")
+    _within_floor(zgot, zref, zfloor)

@@ -21,6 +21,8 @@
 // ds_read_b128 conflict free; grouped (8 m-tiles) + XCD-aware tile order for L2 reuse.
 #include "common.h"
 #include <stdlib.h>
+#include <utility>
+#include <type_traits>
 
 namespace {
 
@@ -580,6 +582,260 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
 }
 
 
+// ---------------------------------------------------------------------------------------------
+// gemm_bf16_tn_4w: 256x256x64 tile, 4 waves (one per SIMD), each wave a 128x128 quadrant (8 x 8
+// v_mfma_f32_16x16x32_bf16 tiles, 256 accumulator AGPRs).  The issue order is the one ROCm's own
+// hipBLASLt uses for this tile on gfx950 (its MT256x256x64_MI16x16 DTLA1_DTLB1 PGR2 kernel, read
+// from the disassembly of the image's TensileLibrary code object), written here from scratch
+// for this library's epilogue / split-tail contract:
+//  * LDS image per operand and buffer: 32 rows of 1056 B = 8 global rows x 128 B (64 k) + 32 B of
+//    pad.  LDS row rho, column block q holds global row 128 (rho / 16) + 16 q + rho % 16, so one
+//    LDS-DMA instruction (buffer_load_dwordx4 ... lds, 64 lanes x 16 B) fills exactly one LDS row
+//    from 8 whole 128-B row segments, and a 16x32 fragment (lane l: row l % 16, 16-B chunk l / 16)
+//    of m-tile i is one ds_read_b128 at row (16 wm + l % 16), +128 i, +64 s: the 1056-B stride
+//    moves consecutive rows 8 banks apart, conflict-free for every lane group of ds_read_b128.
+//  * Two buffers (K-tiles t, t+1); the DMA of K-tile t+2 goes into the buffer of t as soon as the
+//    four waves have its fragments in registers: a K-tile's fragments (both k-steps, 128 VGPRs)
+//    are held in registers, so each operand region is released by one barrier in the first
+//    k-step and refilled during the rest of the iteration (one iteration of latency hiding).
+//  * One iteration = 128 MFMAs (k-step 0, then k-step 1); interleaved in the MFMA stream: the
+//    k-step-1 fragment reads of the current buffer, the 16 DMA instructions of K-tile t+2 (8 W rows
+//    first, then 8 A), the k-step-0 fragment reads of the next buffer, and four barriers
+//    (W region free, A region free, W of t+1 landed -- counted vmcnt(18) --, A of t+1 landed --
+//    vmcnt(15)).  Every instruction group is fenced (sched_barrier), so issue order = source order.
+// Product D[n][m] = W.A^T (W fragment as the A operand): each lane owns 4 consecutive output
+// columns for the fused epilogue, as the other kernels.
+// ---------------------------------------------------------------------------------------------
+// straight-line expansion f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>): every
+// index is a compile-time constant (a 128-step #pragma unroll loop is not fully unrolled by hipcc,
+// leaving the fragment arrays runtime-indexed, i.e. in scratch)
+template <class F, int... Q>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Q...>) {
+    (f(std::integral_constant<int, Q>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+constexpr int W4_ROWB = 1056;                 // LDS row: 8 global rows x 128 B + 32 B pad
+constexpr int W4_OPB = 32 * W4_ROWB;          // one operand's K-tile image (256 rows x 64 k)
+constexpr int W4_LDS = 4 * W4_OPB;            // [A b0][A b1][W b0][W b1] = 135168 B
+
+template <bool WIDE>
+__global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
+    const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
+    bf16_t* C, long long ldc, int M, int N, int K, Epi ep, int ntm, int ntn, int nmain, int ksplit,
+    int piece_k, float* __restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    int pid, piece = -1;
+    if ((int)blockIdx.x < nmain) {
+        pid = xcd_remap(blockIdx.x, nmain);
+    } else {
+        const int t = blockIdx.x - nmain;
+        pid = nmain + t / ksplit;
+        piece = t % ksplit;
+    }
+    int tm, tn;
+    tile_of(pid, ntm, ntn, tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int kb = piece < 0 ? 0 : piece * piece_k;
+    const int nt = (piece < 0 ? K : min(K - kb, piece_k)) / 64;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+
+    f32x4_t acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    // DMA: instruction j of wave w fills LDS row 4j + w of an operand image; lane L lands in column
+    // block L / 8, chunk L % 8 = global row 128 (rho / 16) + 16 (L / 8) + rho % 16, bytes 16 (L % 8)..
+    // (rows past the matrix re-read its last row; their outputs are discarded).  Row offsets are
+    // formed once (16 VGPRs); the K-tile offset goes in soffset.
+    auto rsrc = [](const void* base) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t ra = rsrc(A + (long long)m0 * lda + kb);
+    const __amdgpu_buffer_rsrc_t rw = rsrc(W + (long long)n0 * ldw + kb);
+    const int alim = M - 1 - m0, wlim = N - 1 - n0;
+    const unsigned ldab = (unsigned)(lda * 2), ldwb = (unsigned)(ldw * 2);
+    unsigned voa[8], vow[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int rho = 4 * j + wave;
+        const int g = (rho >> 4) * 128 + 16 * (lane >> 3) + (rho & 15);
+        voa[j] = (unsigned)min(g, alim) * ldab + 16u * (lane & 7);
+        vow[j] = (unsigned)min(g, wlim) * ldwb + 16u * (lane & 7);
+    }
+    // LDS-DMA destinations (wave-uniform byte offsets of the wave's first row in the current
+    // buffer) and the per-lane fragment bases; both toggle between the two buffers by XOR once per
+    // K-tile, so the loop body is one instance with immediate ds_read offsets
+    unsigned dw = 2 * W4_OPB + wave * W4_ROWB, da = wave * W4_ROWB;
+    const unsigned dw_tog = dw ^ (dw + W4_OPB), da_tog = da ^ (da + W4_OPB);
+    auto dma_w = [&](unsigned ko, int j) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (LDS_AS void*)(smem + dw + 4 * j * W4_ROWB), 16, vow[j], ko, 0, 0);
+    };
+    auto dma_a = [&](unsigned ko, int j) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(smem + da + 4 * j * W4_ROWB), 16, voa[j], ko, 0, 0);
+    };
+
+    // fragment bases (lane: row l % 16 of the wave's LDS rows, 16-B chunk l / 16), kept opaque so
+    // every read is base + immediate
+    int abase = (int)(uintptr_t)smem + (wm * 16 + (lane & 15)) * W4_ROWB + 16 * (lane >> 4);
+    int wbase = (int)(uintptr_t)smem + 2 * W4_OPB + (wn * 16 + (lane & 15)) * W4_ROWB + 16 * (lane >> 4);
+    int atog = abase ^ (abase + W4_OPB), wtog = wbase ^ (wbase + W4_OPB);
+    asm volatile("" : "+v"(abase), "+v"(wbase), "+v"(atog), "+v"(wtog));
+    auto frag = [&](int addr) {
+        return *reinterpret_cast<const LDS_AS bf16x8_t*>((const LDS_AS char*)(uintptr_t)(unsigned)addr);
+    };
+    bf16x8_t fa0[8], fa1[8], fw0[8], fw1[8];
+    auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
+    auto bar = [&]() {
+        fence();
+        asm volatile("s_barrier" ::: "memory");
+        fence();
+    };
+    auto wait_lgkm_bar = [&]() {
+        fence();
+        __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0), visible to the compiler's wait-count pass
+        asm volatile("s_barrier" ::: "memory");
+        fence();
+    };
+
+    // K-tile offsets in bytes; past the last K-tile the DMA re-reads it (into the buffer no later
+    // read uses), which keeps every iteration's wait counts identical
+    const unsigned klast = (unsigned)(nt - 1) * 128u;
+    auto kofs = [&](int t) { return min((unsigned)t * 128u, klast); };
+
+    // prologue: K-tiles 0 and 1 in flight (W then A each), then the k-step-0 fragments of tile 0
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dma_w(0, j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dma_a(0, j);
+    dw ^= dw_tog;
+    da ^= da_tog;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dma_w(kofs(1), j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dma_a(kofs(1), j);
+    dw ^= dw_tog;
+    da ^= da_tog;
+    fence();
+    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    bar();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fw0[j] = frag(wbase + 128 * j);
+    fence();
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    bar();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa0[i] = frag(abase + 128 * i);
+    fence();
+
+    // one K-tile t: 128 MFMAs with, before MFMA q, the reads / DMA / barriers of this table
+#pragma nounroll
+    for (int t = 0; t < nt; ++t) {
+        const unsigned ko = kofs(t + 2);
+        static_for<128>([&](auto qc) __attribute__((always_inline)) {
+            constexpr int q = decltype(qc)::value;
+            if constexpr (q < 16 && (q & 1)) fw1[q >> 1] = frag(wbase + 128 * (q >> 1) + 64);
+            if constexpr (q == 17) wbase ^= wtog;                          // next buffer's W fragments
+            if constexpr (q == 20) wait_lgkm_bar();                        // W region of this buffer free
+            if constexpr (q >= 21 && q <= 37 && (q - 21) % 4 == 0) dma_w(ko, (q - 21) / 4);
+            if constexpr (q >= 23 && q <= 39 && (q - 23) % 4 == 0) fa1[(q - 23) / 4] = frag(abase + 128 * ((q - 23) / 4) + 64);
+            if constexpr (q >= 41 && q <= 45 && (q & 1)) fa1[5 + (q - 41) / 2] = frag(abase + 128 * (5 + (q - 41) / 2) + 64);
+            if constexpr (q == 47) abase ^= atog;
+            if constexpr (q == 52) wait_lgkm_bar();                        // A region of this buffer free
+            if constexpr (q == 53 || q == 56 || q == 59) dma_w(ko, 5 + (q - 53) / 3);
+            if constexpr (q == 62) dma_a(ko, 0);
+            if constexpr (q == 65) dma_a(ko, 1);
+            if constexpr (q == 69) {                                       // W of K-tile t+1 landed
+                fence();
+                asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+                bar();
+            }
+            if constexpr (q >= 70 && q <= 84 && !(q & 1)) fw0[(q - 70) / 2] = frag(wbase + 128 * ((q - 70) / 2));
+            if constexpr (q >= 86 && q <= 98 && (q - 86) % 3 == 0) dma_a(ko, 2 + (q - 86) / 3);
+            if constexpr (q == 101) {                                      // A of K-tile t+1 landed
+                fence();
+                asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+                bar();
+            }
+            if constexpr (q >= 102 && q <= 116 && !(q & 1)) fa0[(q - 102) / 2] = frag(abase + 128 * ((q - 102) / 2));
+            if constexpr (q == 122) dma_a(ko, 7);
+            // MFMA q: k-step q / 64, tile (i, j) = ((q % 64) / 8, q % 8).  Inline asm with the
+            // accumulator tied in place: the 256 accumulators then fill the AGPR file exactly (the
+            // builtin let the register allocator rename them per MFMA: AGPR copies and spills)
+            constexpr int i = (q & 63) >> 3, j = q & 7;
+            if constexpr (q < 64)
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fw0[j]), "v"(fa0[i]));
+            else
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fw1[j]), "v"(fa1[i]));
+            fence();
+        });
+        dw ^= dw_tog;
+        da ^= da_tog;
+    }
+    // drain the re-read DMAs of the last two iterations; the accumulators leave through
+    // v_accvgpr_read: cover the last MFMAs' write latency by hand (the hazard recognizer does not
+    // see into the asm statements)
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+
+    // output: acc[i][j][e] = C[m][n], m = m0 + 128 wm + 16 i + (lane & 15), n = n0 + 128 wn + 16 j + 4 (lane >> 4) + e
+    if (piece >= 0) {
+        float* pp = part + ((long long)(pid - nmain) * ksplit + piece) * 256 * 256;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                *reinterpret_cast<f32x4_t*>(pp + (128 * wm + 16 * i + (lane & 15)) * 256 + 128 * wn + 16 * j +
+                                            4 * (lane >> 4)) = acc[i][j];
+        return;
+    }
+    if constexpr (WIDE) {
+        // 16-B epilogue: column blocks (2p, 2p+1) traded between lane groups g, g^1 (permlane16_swap,
+        // as gemm_bf16_tn_8p): an even-g lane ends with columns 32p + 4g .. +7, an odd-g lane with
+        // 32p + 16 + 4(g-1) .. +7
+        const int g = lane >> 4;
+        const int nw = 16 * (g & 1) + 4 * (g & ~1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int m = m0 + 128 * wm + 16 * i + (lane & 15);
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float x = acc[i][2 * p][e], y = acc[i][2 * p + 1][e];
+                    const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+                    v[e] = __uint_as_float(sw[0]);
+                    v[4 + e] = __uint_as_float(sw[1]);
+                }
+                const int n = n0 + 128 * wn + 32 * p + nw;
+                if (m < M && n < N) epilogue_store_w<8>(v, m, n, C, ldc, ep);
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = m0 + 128 * wm + 16 * i + (lane & 15);
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int n = n0 + 128 * wn + 16 * j + 4 * (lane >> 4);
+            if (n >= N) continue;
+            epilogue_store(acc[i][j], m, n, C, ldc, ep);
+        }
+    }
+}
+
+
 typedef int i32x8_t __attribute__((ext_vector_type(8)));
 
 // ---------------------------------------------------------------------------------------------
@@ -964,6 +1220,12 @@ static bool lt_with_epilogue(void* c, long long ldc, int m, int n, int epilogue,
     return true;
 }
 
+// which 256x256 kernel runs the un-split-phase (k2 == 0) GEMMs: VS_GEMM_KERNEL=4w|8p
+static bool use_4w() {
+    const char* e = getenv("VS_GEMM_KERNEL");
+    return e && e[0] == '4';
+}
+
 static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n) {
     if (epilogue < VS_EPI_BIAS || epilogue > VS_EPI_RES) return VS_E_INVALID;
     ep = Epi{};
@@ -1049,6 +1311,19 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
             part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
             if (!part) sp = KSplit{tm * tn, 0, 1, 0};
         }
+        if (k2 == 0 && use_4w()) {
+            static bool attr4 = false;
+            if (!attr4) {
+                for (const void* f : {(const void*)gemm_bf16_tn_4w<false>, (const void*)gemm_bf16_tn_4w<true>})
+                    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS);
+                attr4 = true;
+            }
+            hipLaunchKernelGGL(wide ? gemm_bf16_tn_4w<true> : gemm_bf16_tn_4w<false>,
+                               dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(256), W4_LDS,
+                               (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw, (bf16_t*)c, ldc, m,
+                               n, k, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part);
+            VS_CHECK_LAUNCH();
+        } else {
         hipLaunchKernelGGL(k2 ? (wide ? gemm_bf16_tn_8p<true, true> : gemm_bf16_tn_8p<true, false>)
                               : (wide ? gemm_bf16_tn_8p<false, true> : gemm_bf16_tn_8p<false, false>),
                            dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)),
@@ -1056,6 +1331,7 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
                            (bf16_t*)c, ldc, m, n, k, (const bf16_t*)a2, lda2, (const bf16_t*)w2, ldw2, k2, ep, tm, tn,
                            sp.nmain, sp.ksplit, sp.piece_k, part);
         VS_CHECK_LAUNCH();
+        }
         if (sp.ntail) {
             const long long threads = (long long)sp.ntail * BT * (BT / 4);
             hipLaunchKernelGGL(gemm_split_combine, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,

@@ -211,13 +211,13 @@ def redirect_model_configs(model_configs):
 
 def sp_graph_ok(plan):
     """True when the sequence-parallel plan's collectives can be captured into the step's hipGraph:
-    VSTYLER_SP_GRAPH=1 and RCCL through libvstyler's vs_sp_* on the capture stream
-    (VSTYLER_SP_COMM=native; NativeComm then runs its collectives on the caller's stream) -- not
+    VSTYLER_SP_GRAPH=1 and RCCL through libvstyler's vs_sp_* (VSTYLER_SP_COMM=native) -- not
     torch.distributed's RCCL, whose process-group stream the capture does not survive on this
     image's HIP (segfault in hipStreamEndCapture, profiles/r3/sp_graph_probe_faulthandler.log), and
-    not host-staged substitutes (tests).  Opt-in: it trades the exchange/compute overlap for the
-    launch savings, and only world size 1 has run on hardware (bit-identical replay,
-    test_ulysses_rccl_world1_graph_capture); SP steps run eager by default."""
+    not host-staged substitutes (tests).  NativeComm in side-stream mode keeps its exchange/compute
+    overlap in the graph: DenoiseStepper binds its comm stream to the capture origin and forks the
+    compute (usp.NativeComm).  Opt-in: only world size 1 has run on hardware
+    (test_ulysses_rccl_world1_graph_capture); SP steps run eager by default."""
     if os.environ.get("VSTYLER_SP_GRAPH", "0") != "1":
         return False
     if plan is None:
@@ -236,13 +236,30 @@ class DenoiseStepper:
     captured once into a hipGraph and every later call refreshes the two slots and replays it.
     The eager step and the capture run on one dedicated stream, so the split-tail workspaces that
     libvstyler keeps per (device, stream) and allocates in the eager step are the ones the captured
-    launches use (a capture on a fresh stream could not allocate them and would launch unsplit)."""
+    launches use (a capture on a fresh stream could not allocate them and would launch unsplit).
 
-    def __init__(self, step_fn, timesteps_bf16, dsigmas_f32, use_graph=True, on_replay=None):
+    comms: side-stream NativeComm objects of an SP plan (usp.plan_native_comms).  With a graph they
+    are bound to the stepper's stream -- the capture origin -- and the step's compute runs on a
+    second stream forked from it and joined back, so the collectives overlap the compute inside
+    the graph while RCCL itself only ever runs on the origin stream."""
+
+    def __init__(self, step_fn, timesteps_bf16, dsigmas_f32, use_graph=True, on_replay=None, comms=()):
         self.step_fn, self.ts, self.ds = step_fn, timesteps_bf16, dsigmas_f32
         self.t_buf, self.d_buf = timesteps_bf16[0:1].clone(), dsigmas_f32[0:1].clone()
         self.use_graph, self.graph, self.on_replay = use_graph, None, on_replay
-        self.stream = torch.cuda.Stream(device=self.t_buf.device) if use_graph else None
+        dev = self.t_buf.device
+        self.stream = torch.cuda.Stream(device=dev) if use_graph else None
+        self.comms = list(comms) if use_graph else []
+        self.compute = torch.cuda.Stream(device=dev) if self.comms else None
+
+    def _run(self):
+        if self.compute is None:
+            self.step_fn(self.t_buf, self.d_buf)
+            return
+        self.compute.wait_stream(self.stream)          # fork
+        with torch.cuda.stream(self.compute):
+            self.step_fn(self.t_buf, self.d_buf)
+        self.stream.wait_stream(self.compute)          # join
 
     def __call__(self, i):
         self.t_buf.copy_(self.ts[i:i + 1])
@@ -257,9 +274,14 @@ class DenoiseStepper:
             return
         cur = torch.cuda.current_stream(self.t_buf.device)
         self.stream.wait_stream(cur)
-        with torch.cuda.stream(self.stream):
-            self.step_fn(self.t_buf, self.d_buf)
-            self.capture()
+        old = [c.bind_stream(self.stream) for c in self.comms]
+        try:
+            with torch.cuda.stream(self.stream):
+                self._run()
+                self.capture()
+        finally:
+            for c, s in zip(self.comms, old):
+                c.bind_stream(s)
         cur.wait_stream(self.stream)
 
     def capture(self):
@@ -267,7 +289,7 @@ class DenoiseStepper:
         err = None
         try:
             with torch.cuda.graph(g, stream=self.stream):
-                self.step_fn(self.t_buf, self.d_buf)
+                self._run()
         except Exception as e:      # e.g. a collective backend that cannot be captured: stay eager
             err = e
         # the decision is collective: with several ranks replaying graphs whose collectives must
@@ -437,7 +459,11 @@ class WanVideoPipeline:
                               sp_group=self.sp_group, tea_cache=tea_cache)
             K.cfg_euler_dev(v[0:1], v[1:2] if use_cfg else None, latents, cfg_scale, d_buf)
 
-        stepper = DenoiseStepper(step, ts, ds, use_graph)
+        comms = ()
+        if use_graph and self.use_unified_sequence_parallel:
+            from .usp import plan_native_comms
+            comms = plan_native_comms(self.sp_group)
+        stepper = DenoiseStepper(step, ts, ds, use_graph, comms=comms)
         steps = range(n_steps)
         if progress_bar_cmd is not None:
             steps = progress_bar_cmd(steps)

@@ -102,22 +102,34 @@ class NativeComm:
         uid = ctypes.create_string_buffer(box[0], 128)
         self._check(lib.vs_sp_init(self.rank, self.world, uid, torch.cuda.current_device(),
                                    ctypes.byref(self.handle)))
-        # stream="caller" (VSTYLER_SP_COMM_STREAM=caller; the default under VSTYLER_SP_GRAPH=1): the
-        # collectives run on the caller's stream, in order with the compute -- no exchange/compute
-        # overlap, but capturable: RCCL on a side stream forked into a hipGraph capture segfaults in
+        # stream="side" (default): the collectives run on a stream of their own, ordered after the
+        # caller's work by events, so they overlap the compute enqueued meanwhile.  "caller"
+        # (VSTYLER_SP_COMM_STREAM=caller): on the caller's stream, in order with the compute.
+        # hipGraph capture: RCCL on a side stream FORKED into a capture segfaults in
         # hipStreamEndCapture on this image's HIP 7.0 (torch's ProcessGroupNCCL stream and this
-        # class's own alike; profiles/r3/sp_graph_probe_faulthandler.log), on the capture stream it
-        # captures and replays bit-identical (profiles/r3/sp_graph_probe_caller_stream.log)
+        # class's own alike; profiles/r3/sp_graph_probe_faulthandler.log), while RCCL on the capture's
+        # ORIGIN stream captures and replays bit-identical (sp_graph_probe_caller_stream.log).  So the
+        # denoising step's capture inverts the fork instead (pipeline.DenoiseStepper): the comm stream
+        # is bound to the capture origin (bind_stream) and the compute runs on a stream forked from
+        # it -- the same event-ordered overlap, with RCCL where the capture accepts it.
         if stream is None:
-            stream = os.environ.get("VSTYLER_SP_COMM_STREAM") or \
-                ("caller" if os.environ.get("VSTYLER_SP_GRAPH") == "1" else "side")
+            stream = os.environ.get("VSTYLER_SP_COMM_STREAM") or "side"
         if stream not in ("caller", "side"):
             raise ValueError(f"VSTYLER_SP_COMM_STREAM must be 'caller' or 'side', not {stream!r}")
         self.stream = None if stream == "caller" else torch.cuda.Stream()
 
     @property
     def capturable(self):
-        return self.stream is None
+        """On the caller's stream, or on a side stream the step's capture binds to its origin."""
+        return True
+
+    def bind_stream(self, stream):
+        """Run the side-stream collectives on `stream` (the capture origin of DenoiseStepper);
+        returns the previous stream.  No effect in caller mode."""
+        old = self.stream
+        if old is not None:
+            self.stream = stream
+        return old
 
     def _check(self, code):
         if code != 0:
@@ -321,6 +333,25 @@ class UlyssesGroup:
 
 
 _WS_BY_DEV = {}
+
+
+def plan_native_comms(plan):
+    """Every NativeComm of a parallel plan (Ulysses groups, CfgParallel's pair exchange and its
+    sub-plans) whose collectives run on a side stream: the ones a step capture must bind."""
+    out, seen = [], set()
+
+    def visit(p):
+        if p is None or id(p) in seen:
+            return
+        seen.add(id(p))
+        for name in ("native", "pair_native"):
+            c = getattr(p, name, None)
+            if c is not None and c.stream is not None and c not in out:
+                out.append(c)
+        for name in ("ulysses", "full"):
+            visit(getattr(p, name, None))
+    visit(plan)
+    return out
 
 
 def _ws_of(t):
