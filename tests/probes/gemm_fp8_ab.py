@@ -36,15 +36,19 @@ for M in [int(v) for v in sys.argv[1:]] or (59280,):
             kw.update(residual=x, gate=gate, gate_bstride=N, rows_per_batch=(M + 1) // 2)
         out = x if epi == K.VS_EPI_GATE_RES else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         t = {v: [] for v in VARIANTS}
+        def setv(v):      # vstyler = the 8-phase kernel, w4 = the 4-wave kernel, lt = hipBLASLt fp8
+            os.environ["VS_FP8_BACKEND"] = "vstyler" if v in ("vstyler", "w4") else v
+            os.environ["VS_GEMM_KERNEL"] = "4w" if v == "w4" else "8p"
         for v in VARIANTS:
-            os.environ["VS_FP8_BACKEND"] = v
+            setv(v)
             K.gemm_fp8(a8, sc, w8, out, **kw); torch.cuda.synchronize()
         for r in range(4):
             for v in VARIANTS:
-                os.environ["VS_FP8_BACKEND"] = v
+                setv(v)
                 t[v].append(timed(lambda: K.gemm_fp8(a8, sc, w8, out, **kw)))
         fl = 2.0 * M * N * Kd
         print(f"fp8 M={M} {name:8s} N={N} K={Kd}: " +
               "  ".join(f"{v} {min(t[v]):.3f} ms ({fl / min(t[v]) / 1e9:.0f} TF/s)" for v in VARIANTS), flush=True)
         del a, w8, a8, sc, b, gate, x, out
 os.environ.pop("VS_FP8_BACKEND", None)
+os.environ.pop("VS_GEMM_KERNEL", None)

@@ -123,13 +123,16 @@ def test_gemm8p_random_vs_fp32(K):
     assert rel < 4e-3, rel
 
 
-@pytest.mark.parametrize("M,N,Kd", [(256, 256, 128), (300, 520, 256), (1000, 768, 640), (520, 300, 5120)])
-def test_gemm_fp8_8p_integer_exact(M, N, Kd, monkeypatch):
+@pytest.mark.parametrize("kern", ["8p", "4w"])
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 128), (300, 520, 256), (1000, 768, 640), (520, 300, 5120),
+                                    (512, 512, 384)])
+def test_gemm_fp8_8p_integer_exact(M, N, Kd, kern, monkeypatch):
     """gemm_fp8_tn_8p (VS_FP8_BACKEND=vstyler): integer operands exact in e4m3 with exact fp32 sums
     must reproduce oracle.fp8_linear (layers.py:115-151) bit for bit: pins the MX 32x32x64 operand
     maps, the fp8 chunk swizzle and the per-row scale."""
     from vstyler import kernels as K
     monkeypatch.setenv("VS_FP8_BACKEND", os.environ.get("VS_FP8_BACKEND", "vstyler"))
+    monkeypatch.setenv("VS_GEMM_KERNEL", kern)
     g = torch.Generator().manual_seed(M + N + Kd)
     x = torch.randint(-4, 5, (M, Kd), generator=g).to(BF16)
     x[::5] *= 512          # rows whose max exceeds 448: scale 2**k > 1
@@ -145,11 +148,13 @@ def test_gemm_fp8_8p_integer_exact(M, N, Kd, monkeypatch):
     assert torch.equal(out.cpu(), ref)
 
 
-def test_gemm_fp8_8p_split_tail_and_epilogue(monkeypatch):
+@pytest.mark.parametrize("kern", ["8p", "4w"])
+def test_gemm_fp8_8p_split_tail_and_epilogue(kern, monkeypatch):
     """272 tiles: the split-tail pieces + combine (per-row scale applied after the sum) equal the
     unsplit kernel on integer data; gate-residual + hint epilogue bit-exact vs the oracle."""
     from vstyler import kernels as K
     monkeypatch.setenv("VS_FP8_BACKEND", os.environ.get("VS_FP8_BACKEND", "vstyler"))
+    monkeypatch.setenv("VS_GEMM_KERNEL", kern)
     M, N, Kd, S = 4352, 4096, 1024, 2176
     g = torch.Generator().manual_seed(21)
     x = torch.randint(-4, 5, (M, Kd), generator=g).to(BF16)

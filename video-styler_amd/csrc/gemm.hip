@@ -1064,6 +1064,238 @@ __global__ __launch_bounds__(512, 2) void gemm_fp8_tn_8p(
 }
 
 
+// ---------------------------------------------------------------------------------------------
+// gemm_fp8_tn_4w: the 4-wave 256x256 schedule of gemm_bf16_tn_4w for the fp8 path (config 5;
+// AutoWrappedLinear.fp8_linear, layers.py:115-151): C = epilogue(scale_a[m] * (A8 . W8^T)), e4m3
+// operands.  A K-tile is 128 fp8 = the same 128-B row segments, LDS-DMA pieces and 1-KB LDS rows
+// as the bf16 kernel; per wave and K-tile 64 MX-rate v_mfma_scale_f32_16x16x128_f8f6f4 (unit E8M0
+// scales, 32 cycles each: twice the bf16 FLOPs per cycle).  A 16x16x128 fragment is 32 B per lane
+// (row l % 16, bytes 32 (l / 16) ..), one K-tile's 16 fragments are all 128 VGPRs, so instead of
+// holding two k-steps the MFMA order lets fragments die early: rows 0-3 of the 8x8 tile grid
+// i-major (q < 32), then rows 4-7 column by column; the next K-tile's fragments are read into the
+// dead registers (A 0-3 from q = 32, W column j after its last use at q = 35 + 4j, W 7 and A 4-7 at
+// the top of the next iteration).  LDS rows of 1088 B (64-B pad) with the 16-B chunk XOR
+// 3 (r >> 3) on rows r % 16 >= 8 (applied on the DMA source address): conflict-free for both 16-B
+// halves of every fragment read (tests/probes: searched over pads and XOR swizzles).
+// Per iteration: top reads of K-tile t, one barrier (buffer of t free), the 16 DMA instructions of
+// K-tile t+2 into it (every 3 MFMAs from q = 11), vmcnt(6) + barrier at q = 29 (K-tile t+1 landed),
+// then the next K-tile's reads.
+// ---------------------------------------------------------------------------------------------
+constexpr int F4_ROWB = 1088;
+constexpr int F4_OPB = 32 * F4_ROWB;
+constexpr int F4_LDS = 4 * F4_OPB;            // [A b0][A b1][W b0][W b1] = 139264 B
+__device__ __forceinline__ int f4_swz(int r) { return ((r >> 3) & 1) * 3; }
+
+template <bool WIDE>
+__global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
+    const uint8_t* __restrict__ A, long long lda, const float* __restrict__ scale_a, const uint8_t* __restrict__ W,
+    long long ldw, bf16_t* C, long long ldc, int M, int N, int K, Epi ep, int ntm, int ntn, int nmain, int ksplit,
+    int piece_k, float* __restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    int pid, piece = -1;
+    if ((int)blockIdx.x < nmain) {
+        pid = xcd_remap(blockIdx.x, nmain);
+    } else {
+        const int t = blockIdx.x - nmain;
+        pid = nmain + t / ksplit;
+        piece = t % ksplit;
+    }
+    int tm, tn;
+    tile_of(pid, ntm, ntn, tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int kb = piece < 0 ? 0 : piece * piece_k;
+    const int nt = (piece < 0 ? K : min(K - kb, piece_k)) / 128;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+
+    f32x4_t acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    auto rsrc = [](const void* base) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t ra = rsrc(A + (long long)m0 * lda + kb);
+    const __amdgpu_buffer_rsrc_t rw = rsrc(W + (long long)n0 * ldw + kb);
+    const int alim = M - 1 - m0, wlim = N - 1 - n0;
+    unsigned voa[8], vow[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int rho = 4 * j + wave;
+        const int g = (rho >> 4) * 128 + 16 * (lane >> 3) + (rho & 15);
+        const unsigned ch = 16u * (unsigned)((lane & 7) ^ f4_swz(rho & 15));
+        voa[j] = (unsigned)min(g, alim) * (unsigned)lda + ch;
+        vow[j] = (unsigned)min(g, wlim) * (unsigned)ldw + ch;
+    }
+    unsigned dw = 2 * F4_OPB + wave * F4_ROWB, da = wave * F4_ROWB;
+    const unsigned dw_tog = dw ^ (dw + F4_OPB), da_tog = da ^ (da + F4_OPB);
+    auto dma_w = [&](unsigned ko, int j) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (LDS_AS void*)(smem + dw + 4 * j * F4_ROWB), 16, vow[j], ko, 0, 0);
+    };
+    auto dma_a = [&](unsigned ko, int j) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(smem + da + 4 * j * F4_ROWB), 16, voa[j], ko, 0, 0);
+    };
+
+    // fragment bases: the two 16-B halves of a lane's 32 B (logical chunks 2c, 2c+1 of row r)
+    const int fr = lane & 15, fc = lane >> 4, sw = f4_swz(fr);
+    int a0 = (int)(uintptr_t)smem + (wm * 16 + fr) * F4_ROWB + 16 * ((2 * fc) ^ sw);
+    int a1 = (int)(uintptr_t)smem + (wm * 16 + fr) * F4_ROWB + 16 * ((2 * fc + 1) ^ sw);
+    int w0 = (int)(uintptr_t)smem + 2 * F4_OPB + (wn * 16 + fr) * F4_ROWB + 16 * ((2 * fc) ^ sw);
+    int w1 = (int)(uintptr_t)smem + 2 * F4_OPB + (wn * 16 + fr) * F4_ROWB + 16 * ((2 * fc + 1) ^ sw);
+    int a0t = a0 ^ (a0 + F4_OPB), a1t = a1 ^ (a1 + F4_OPB), w0t = w0 ^ (w0 + F4_OPB), w1t = w1 ^ (w1 + F4_OPB);
+    asm volatile("" : "+v"(a0), "+v"(a1), "+v"(w0), "+v"(w1));
+    asm volatile("" : "+v"(a0t), "+v"(a1t), "+v"(w0t), "+v"(w1t));
+    auto frag = [&](int lo, int hi, int off) {
+        const u32x4_t x = *reinterpret_cast<const LDS_AS u32x4_t*>((const LDS_AS char*)(uintptr_t)(unsigned)(lo + off));
+        const u32x4_t y = *reinterpret_cast<const LDS_AS u32x4_t*>((const LDS_AS char*)(uintptr_t)(unsigned)(hi + off));
+        return i32x8_t{(int)x[0], (int)x[1], (int)x[2], (int)x[3], (int)y[0], (int)y[1], (int)y[2], (int)y[3]};
+    };
+    // the same read from inline asm: invisible to the compiler's wait-count pass, waited for by the
+    // hand-placed lgkmcnt of the loop body (the pass would otherwise wait for it at the loop top)
+    auto frag_asm = [&](int lo, int hi, int off) {
+        u32x4_t x, y;
+        asm volatile("ds_read_b128 %0, %2 offset:%4\n\tds_read_b128 %1, %3 offset:%4"
+                     : "=&v"(x), "=&v"(y) : "v"(lo), "v"(hi), "i"(off) : "memory");
+        return i32x8_t{(int)x[0], (int)x[1], (int)x[2], (int)x[3], (int)y[0], (int)y[1], (int)y[2], (int)y[3]};
+    };
+    i32x8_t fa[8], fw[8];
+    const int unit = 0x7f7f7f7f;        // E8M0 scale 2^0 in every byte
+    auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
+    auto bar = [&]() {
+        fence();
+        asm volatile("s_barrier" ::: "memory");
+        fence();
+    };
+    const unsigned klast = (unsigned)(nt - 1) * 128u;
+    auto kofs = [&](int t) { return min((unsigned)t * 128u, klast); };
+
+    // prologue: K-tiles 0 and 1 in flight; the fragments of tile 0 but W 7 and A 4-7 (read by the
+    // first iteration's top)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dma_w(0, j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dma_a(0, j);
+    dw ^= dw_tog;
+    da ^= da_tog;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dma_w(kofs(1), j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dma_a(kofs(1), j);
+    dw ^= dw_tog;
+    da ^= da_tog;
+    fence();
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    bar();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = frag(a0, a1, 128 * i);
+#pragma unroll
+    for (int j = 0; j < 7; ++j) fw[j] = frag(w0, w1, 128 * j);
+    fence();
+
+#pragma nounroll
+    for (int t = 0; t < nt; ++t) {
+        const unsigned ko = kofs(t + 2);
+        // the previous iteration's fragment reads (compiler-visible) complete here, so the reads of
+        // W 7 and A 4-7 below (inline asm, counted by hand: used from MFMA 7 / 32) stay in flight
+        fence();
+        __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0)
+        fence();
+        static_for<64>([&](auto qc) __attribute__((always_inline)) {
+            constexpr int q = decltype(qc)::value;
+            if constexpr (q == 0) fw[7] = frag_asm(w0, w1, 128 * 7);                // K-tile t, this buffer
+            if constexpr (q >= 1 && q <= 4) fa[3 + q] = frag_asm(a0, a1, 128 * (3 + q));
+            if constexpr (q == 7) {                  // W 7 landed (the 8 reads of A 4-7 may still fly)
+                fence();
+                asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+                fence();
+            }
+            if constexpr (q == 5) {                                                  // to the next buffer
+                a0 ^= a0t; a1 ^= a1t; w0 ^= w0t; w1 ^= w1t;
+            }
+            if constexpr (q == 10) {                                                 // this buffer free
+                fence();
+                __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0)
+                asm volatile("s_barrier" ::: "memory");
+                fence();
+            }
+            if constexpr (q >= 11 && q <= 56 && (q - 11) % 3 == 0) {
+                constexpr int d = (q - 11) / 3;
+                if constexpr (d < 8) dma_w(ko, d);
+                else dma_a(ko, d - 8);
+            }
+            if constexpr (q == 29) {                                                 // K-tile t+1 landed
+                fence();
+                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                bar();
+            }
+            if constexpr (q >= 32 && q <= 35) fa[q - 32] = frag(a0, a1, 128 * (q - 32));
+            if constexpr (q >= 36 && q <= 60 && (q - 36) % 4 == 0) fw[(q - 36) / 4] = frag(w0, w1, 128 * ((q - 36) / 4));
+            // MFMA q: rows 0-3 i-major, then rows 4-7 column by column
+            constexpr int i = q < 32 ? (q >> 3) : 4 + ((q - 32) & 3);
+            constexpr int j = q < 32 ? (q & 7) : (q - 32) >> 2;
+            asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
+                         : "+a"(acc[i][j]) : "v"(fw[j]), "v"(fa[i]), "v"(unit));
+            fence();
+        });
+        dw ^= dw_tog;
+        da ^= da_tog;
+    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+
+    // acc[i][j][e] = D[n][m]: m = m0 + 128 wm + 16 i + (lane & 15), n = n0 + 128 wn + 16 j + 4 (lane >> 4) + e
+    if (piece >= 0) {
+        float* pp = part + ((long long)(pid - nmain) * ksplit + piece) * 256 * 256;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                *reinterpret_cast<f32x4_t*>(pp + (128 * wm + 16 * i + (lane & 15)) * 256 + 128 * wn + 16 * j +
+                                            4 * (lane >> 4)) = acc[i][j];
+        return;
+    }
+    if constexpr (WIDE) {
+        const int g = lane >> 4;
+        const int nw = 16 * (g & 1) + 4 * (g & ~1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int m = m0 + 128 * wm + 16 * i + (lane & 15);
+            const float sa = scale_a[min(m, M - 1)];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float x = acc[i][2 * p][e], y = acc[i][2 * p + 1][e];
+                    const auto swp = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+                    v[e] = __uint_as_float(swp[0]) * sa;
+                    v[4 + e] = __uint_as_float(swp[1]) * sa;
+                }
+                const int n = n0 + 128 * wn + 32 * p + nw;
+                if (m < M && n < N) epilogue_store_w<8>(v, m, n, C, ldc, ep);
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = m0 + 128 * wm + 16 * i + (lane & 15);
+        if (m >= M) continue;
+        const float sa = scale_a[m];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int n = n0 + 128 * wn + 16 * j + 4 * (lane >> 4);
+            if (n >= N) continue;
+            epilogue_store(acc[i][j] * sa, m, n, C, ldc, ep);
+        }
+    }
+}
+
+
 __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __restrict__ x, long long ldx,
                                                              uint8_t* __restrict__ x8, long long ld8,
                                                              float* __restrict__ scale, int rows, int cols) {
@@ -1398,6 +1630,22 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
         part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
         if (!part) sp = KSplit{tm * tn, 0, 1, 0};
     }
+    if (use_4w()) {
+        static bool attr4 = false;
+        if (!attr4) {
+            for (const void* f : {(const void*)gemm_fp8_tn_4w<false>, (const void*)gemm_fp8_tn_4w<true>})
+                (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, F4_LDS);
+            attr4 = true;
+        }
+        const bool wide = n % 8 == 0 && ldc % 8 == 0 && aligned16(c) && (!ep.bias || aligned16(ep.bias)) &&
+                          (!ep.res || (ep.ld_res % 8 == 0 && aligned16(ep.res))) &&
+                          (!ep.gate || (ep.gate_bstride % 8 == 0 && aligned16(ep.gate))) &&
+                          (!ep.hint || (ep.ld_hint % 8 == 0 && aligned16(ep.hint)));
+        hipLaunchKernelGGL(wide ? gemm_fp8_tn_4w<true> : gemm_fp8_tn_4w<false>,
+                           dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(256), F4_LDS, (hipStream_t)stream,
+                           (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c, ldc, m, n, k, ep, tm,
+                           tn, sp.nmain, sp.ksplit, sp.piece_k, part);
+    } else
     hipLaunchKernelGGL(gemm_fp8_tn_8p, dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(512), LDS8,
                        (hipStream_t)stream, (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c,
                        ldc, m, n, k, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part);
