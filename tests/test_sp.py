@@ -424,3 +424,21 @@ def test_cfg_parallel_model_bit_identical_on_one_gpu(world):
         assert isinstance(r, dict), res
         assert r["cfg"] is True and r["cfg_slg"] is True and r.get("nocfg", True) is True, res
         assert r["gathers"] == 2, res
+
+
+def test_plan_native_comms_cpu():
+    """The side-stream NativeComm objects a step capture binds to its origin stream
+    (pipeline.DenoiseStepper, usp.plan_native_comms): every one of a plan and its sub-plans, once,
+    and none in caller-stream mode or for torch.distributed plans."""
+    from types import SimpleNamespace as NS
+    from vstyler.usp import plan_native_comms
+    side = [NS(stream=object()) for _ in range(3)]
+    caller = NS(stream=None)
+    ul = NS(native=side[0])
+    plan = NS(native=None, pair_native=side[1], ulysses=ul, full=NS(native=side[2], ulysses=None, full=None))
+    assert plan_native_comms(plan) == [side[1], side[0], side[2]]
+    assert plan_native_comms(NS(native=caller)) == []
+    assert plan_native_comms(NS(native=None)) == []
+    assert plan_native_comms(None) == []
+    shared = NS(native=side[0], ulysses=NS(native=side[0]))
+    assert plan_native_comms(shared) == [side[0]]
