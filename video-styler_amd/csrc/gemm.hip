@@ -42,7 +42,17 @@ struct Epi {
     float alpha;
     int rows_per_batch;
     int mode;
+    int desync;       // diagnostic (VS_GEMM_DESYNC): the first round's blocks sleep (b % 256) / 256 x this many ~4 us units
 };
+
+// staggered start of the first round of blocks (diagnostic: do tile epilogues that coincide on
+// every CU cost more than staggered ones?)
+__device__ __forceinline__ void desync_start(const Epi& ep) {
+    if (ep.desync > 0 && blockIdx.x < 256) {
+        const int n = (int)(blockIdx.x % 256) * ep.desync / 256;
+        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+}
 
 __device__ __forceinline__ int g_off(int row, int ch) { return row * 128 + 16 * (ch ^ (row & 7)); }
 
@@ -340,6 +350,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
     int tm, tn;
     tile_of(pid, ntm, ntn, tm, tn);
     const int m0 = tm * T8, n0 = tn * T8;
+    desync_start(ep);
     const int kb = piece < 0 ? 0 : piece * piece_k;
     const int Kp = piece < 0 ? K : min(K - kb, piece_k);
     const int nk1 = Kp / 64;
@@ -618,70 +629,362 @@ __device__ __forceinline__ void static_for(F&& f) {
     static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
+// ---------------------------------------------------------------------------------------------
+// Tile epilogue of the 4-wave kernels (16-B accesses): a wave owns rows m = m_w + 16 i + (lane & 15)
+// (i = 0..7) and, after the permlane16_swap pairing of column blocks (2p, 2p+1), 8 consecutive
+// columns n = n_w + 32 p .. +7 (p = 0..3).  The per-element epilogue branch of epilogue_store_w
+// (mode tested per 8 columns, each load waited for before its store: 32 serialised HBM round trips
+// per wave) becomes one mode-specialised body per launch that issues the residual / hint loads of
+// rows i+4 while rows i are computed (4 rows of loads in flight), with the bias and gate rows loaded
+// once per tile.  Same arithmetic and rounding points as epilogue_store_w.
+// SCALED: the fp8 kernel's per-row activation scale (applied to the accumulator first).
+// ---------------------------------------------------------------------------------------------
+#ifndef W4_EPI_DEPTH
+#define W4_EPI_DEPTH 2
+#endif
+__device__ __forceinline__ u32x4_t ld16(const bf16_t* p) { return *reinterpret_cast<const u32x4_t*>(p); }
+__device__ __forceinline__ void unpack8(const u32x4_t& w, float* v) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v[2 * i] = bflo(w[i]); v[2 * i + 1] = bfhi(w[i]); }
+}
+
+// v + s in a VGPR, formed at the point of use: a buffer access's row step kept in voffset (the
+// resource's range check then covers it, so rows past the matrix load 0 whether or not the
+// hardware checks soffset) without the compiler hoisting one VGPR per row step out of the loop
+__device__ __forceinline__ int vadd_opq(int v, int s) {
+    int r;
+    asm volatile("v_add_u32 %0, %1, %2" : "=v"(r) : "s"(s), "v"(v));
+    return r;
+}
+
+// one accumulator element AGPR -> VGPR at its point of use: left to the compiler, the copies of
+// all 256 accumulators were made at the K loop's exit (the class change from the MFMA asm's "a"
+// operands) and the overflow spilled to scratch
+__device__ __forceinline__ float acc_rd(float a) {
+    float v;
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v) : "a"(a));
+    return v;
+}
+
+template <int MODE, bool HINT, bool SCALED, class AccT>
+__device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n_w, int lane, bf16_t* C, long long ldc,
+                                                 int M, int N, const Epi& ep, const float* __restrict__ scale_a) {
+    constexpr bool RESID = MODE == VS_EPI_GATE_RES || MODE == VS_EPI_RES;
+    const int g = lane >> 4;
+    const int ncol = 16 * (g & 1) + 4 * (g & ~1);         // lane's column within a 32-column pair block
+    const int nl = n_w + ncol;                            // + 32 p
+    const int r = lane & 15;                              // + 16 i
+    // buffer resources rebased on the wave's first row: one voffset per lane, the row step i in
+    // soffset and the column block p in the immediate offset (no 64-bit address per access);
+    // rows past M read as 0 (range), their stores are masked
+    const int rows = max(0, min(128, M - m_w));
+    auto rsrc = [&](const bf16_t* base, long long ld, bool load) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base + (long long)m_w * ld), 0,
+                                                 load ? (int)((long long)rows * ld * 2) : 0x7fffffff, 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t rc = rsrc(C, ldc, false);
+    const int vo_c = (int)((r * ldc + n_w + ncol) * 2);
+    u32x4_t bw[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) bw[p] = ep.bias ? ld16(ep.bias + min(nl + 32 * p, N - 8)) : u32x4_t{0, 0, 0, 0};
+    u32x4_t gw0[4], gw1[4];
+    int b_lo = 0;
+    if constexpr (MODE == VS_EPI_GATE_RES) {
+        b_lo = min(m_w, M - 1) / ep.rows_per_batch;
+        const int b_hi = min(m_w + 127, M - 1) / ep.rows_per_batch;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int n = min(nl + 32 * p, N - 8);
+            gw0[p] = ld16(ep.gate + (long long)b_lo * ep.gate_bstride + n);
+            gw1[p] = ld16(ep.gate + (long long)b_hi * ep.gate_bstride + n);
+        }
+    }
+    // (resources of absent operands point at C with an empty range: never read)
+    const __amdgpu_buffer_rsrc_t rr = RESID ? rsrc(ep.res, ep.ld_res, true) : rsrc(C, ldc, false);
+    const __amdgpu_buffer_rsrc_t rh = HINT ? rsrc(ep.hint, ep.ld_hint, true) : rsrc(C, ldc, false);
+    const int vo_r = RESID ? (int)((r * ep.ld_res + n_w + ncol) * 2) : 0;
+    const int vo_h = HINT ? (int)((r * ep.ld_hint + n_w + ncol) * 2) : 0;
+    constexpr int DEPTH = W4_EPI_DEPTH;        // rows of residual / hint loads in flight
+    u32x4_t rs[DEPTH][4], hs[DEPTH][4];
+    auto load_rows = [&](auto ic, u32x4_t (&r_)[4], u32x4_t (&h_)[4]) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            r_[p] = __builtin_amdgcn_raw_buffer_load_b128(rr, vadd_opq(vo_r, (int)(16 * i * ep.ld_res * 2)) + 64 * p, 0, 0);
+            if constexpr (HINT) h_[p] = __builtin_amdgcn_raw_buffer_load_b128(rh, vadd_opq(vo_h, (int)(16 * i * ep.ld_hint * 2)) + 64 * p, 0, 0);
+        }
+    };
+    if constexpr (RESID) {
+        static_for<DEPTH>([&](auto ic) __attribute__((always_inline)) {
+            constexpr int i = decltype(ic)::value;
+            load_rows(ic, rs[i], hs[i]);
+        });
+    }
+    static_for<8>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        const int m = m_w + r + 16 * i;
+        float sa = 1.f;
+        if constexpr (SCALED) sa = scale_a[min(m, M - 1)];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            float y[8], bv[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float x = acc_rd(acc[i][2 * p][e]), z = acc_rd(acc[i][2 * p + 1][e]);
+                const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(z), false, false);
+                y[e] = __uint_as_float(sw[0]);
+                y[4 + e] = __uint_as_float(sw[1]);
+            }
+            unpack8(bw[p], bv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[e] = rbf((SCALED ? y[e] * sa : y[e]) + bv[e]);
+            if constexpr (MODE == VS_EPI_GELU) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) y[e] = gelu_tanh_f(y[e]);
+            } else if constexpr (MODE == VS_EPI_SILU) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) y[e] = silu_f(y[e]);
+            } else if constexpr (MODE == VS_EPI_GATE_RES) {
+                float rv[8], gv[8];
+                unpack8(rs[i % DEPTH][p], rv);
+                const bool hi = m / ep.rows_per_batch != b_lo;
+                const u32x4_t gsel = hi ? gw1[p] : gw0[p];
+                unpack8(gsel, gv);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) y[e] = rbf(rv[e] + rbf(gv[e] * y[e]));
+                if constexpr (HINT) {
+                    float hv[8];
+                    unpack8(hs[i % DEPTH][p], hv);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) y[e] = y[e] + rbf(hv[e] * ep.hint_scale);
+                }
+            } else if constexpr (MODE == VS_EPI_RES) {
+                float rv[8];
+                unpack8(rs[i % DEPTH][p], rv);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) y[e] = rv[e] + rbf(ep.alpha * y[e]);
+            }
+            if (m < M && nl + 32 * p < N)
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    u32x4_t{pack2(y[0], y[1]), pack2(y[2], y[3]), pack2(y[4], y[5]), pack2(y[6], y[7])}, rc,
+                    vo_c, (int)(16 * i * ldc * 2) + 64 * p, 0);
+            // one column block at a time: the scheduler would otherwise hoist the accumulator reads
+            // of later blocks (AGPR -> VGPR copies) and run out of VGPRs
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (RESID && i + DEPTH < 8) load_rows(std::integral_constant<int, i + DEPTH>{}, rs[i % DEPTH], hs[i % DEPTH]);
+    });
+}
+
+// The same epilogue with 8-B accesses straight from the MFMA layout (lane: 4 consecutive columns
+// n_w + 16 j + 4 (lane >> 4) of each of its 8 rows): no permlane pairing, twice the store
+// instructions (W4_NARROW A/B).
+__device__ __forceinline__ u32x2_t ld8(const bf16_t* p) { return *reinterpret_cast<const u32x2_t*>(p); }
+template <int MODE, bool HINT, bool SCALED, class AccT>
+__device__ __forceinline__ void tile_epilogue_w4n(const AccT& acc, int m_w, int n_w, int lane, bf16_t* C, long long ldc,
+                                                  int M, int N, const Epi& ep, const float* __restrict__ scale_a) {
+    constexpr bool RESID = MODE == VS_EPI_GATE_RES || MODE == VS_EPI_RES;
+    const int ncol = 4 * (lane >> 4);
+    const int nl = n_w + ncol;                            // + 16 j
+    const int r = lane & 15;                              // + 16 i
+    const int rows = max(0, min(128, M - m_w));
+    auto rsrc = [&](const bf16_t* base, long long ld, bool load) {
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base + (long long)m_w * ld), 0,
+                                                 load ? (int)((long long)rows * ld * 2) : 0x7fffffff, 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t rc = rsrc(C, ldc, false);
+    const int vo_c = (int)((r * ldc + n_w + ncol) * 2);
+    const __amdgpu_buffer_rsrc_t rr = RESID ? rsrc(ep.res, ep.ld_res, true) : rsrc(C, ldc, false);
+    const __amdgpu_buffer_rsrc_t rh = HINT ? rsrc(ep.hint, ep.ld_hint, true) : rsrc(C, ldc, false);
+    const int vo_r = RESID ? (int)((r * ep.ld_res + n_w + ncol) * 2) : 0;
+    const int vo_h = HINT ? (int)((r * ep.ld_hint + n_w + ncol) * 2) : 0;
+    int b_lo = 0;
+    if constexpr (MODE == VS_EPI_GATE_RES) b_lo = min(m_w, M - 1) / ep.rows_per_batch;
+    const int b_hi = MODE == VS_EPI_GATE_RES ? min(m_w + 127, M - 1) / ep.rows_per_batch : 0;
+    static_for<8>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        const int m = m_w + r + 16 * i;
+        float sa = 1.f;
+        if constexpr (SCALED) sa = scale_a[min(m, M - 1)];
+        u32x2_t rv2[8], hv2[8];
+        if constexpr (RESID) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                rv2[j] = __builtin_amdgcn_raw_buffer_load_b64(rr, vadd_opq(vo_r, (int)(16 * i * ep.ld_res * 2)) + 32 * j, 0, 0);
+                if constexpr (HINT) hv2[j] = __builtin_amdgcn_raw_buffer_load_b64(rh, vadd_opq(vo_h, (int)(16 * i * ep.ld_hint * 2)) + 32 * j, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int n = nl + 16 * j;
+            const int nc = min(n, N - 4);
+            float y[4], bv[4] = {0.f, 0.f, 0.f, 0.f};
+            if (ep.bias) loadw<4>(ep.bias + nc, bv);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float x = acc_rd(acc[i][j][e]);
+                y[e] = rbf((SCALED ? x * sa : x) + bv[e]);
+            }
+            if constexpr (MODE == VS_EPI_GELU) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) y[e] = gelu_tanh_f(y[e]);
+            } else if constexpr (MODE == VS_EPI_SILU) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) y[e] = silu_f(y[e]);
+            } else if constexpr (MODE == VS_EPI_GATE_RES) {
+                float gv[4];
+                const int bi = m / ep.rows_per_batch != b_lo ? b_hi : b_lo;
+                loadw<4>(ep.gate + (long long)bi * ep.gate_bstride + nc, gv);
+                const float rv[4] = {bflo(rv2[j][0]), bfhi(rv2[j][0]), bflo(rv2[j][1]), bfhi(rv2[j][1])};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) y[e] = rbf(rv[e] + rbf(gv[e] * y[e]));
+                if constexpr (HINT) {
+                    const float hv[4] = {bflo(hv2[j][0]), bfhi(hv2[j][0]), bflo(hv2[j][1]), bfhi(hv2[j][1])};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) y[e] = y[e] + rbf(hv[e] * ep.hint_scale);
+                }
+            } else if constexpr (MODE == VS_EPI_RES) {
+                const float rv[4] = {bflo(rv2[j][0]), bfhi(rv2[j][0]), bflo(rv2[j][1]), bfhi(rv2[j][1])};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) y[e] = rv[e] + rbf(ep.alpha * y[e]);
+            }
+            if (m < M && n < N)
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack2(y[0], y[1]), pack2(y[2], y[3])}, rc,
+                                                      vo_c + 32 * j, (int)(16 * i * ldc * 2), 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    });
+}
+
+template <bool SCALED, class AccT>
+__device__ __forceinline__ void tile_epilogue_w4_dispatch(const AccT& acc, int m_w, int n_w, int lane, bf16_t* C,
+                                                          long long ldc, int M, int N, const Epi& ep,
+                                                          const float* __restrict__ scale_a) {
+#ifdef W4_ONLY_BIAS
+    tile_epilogue_w4<W4_ONLY_BIAS, false, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a);
+    return;
+#endif
+    switch (ep.mode) {
+        case VS_EPI_GELU: tile_epilogue_w4<VS_EPI_GELU, false, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a); break;
+        case VS_EPI_SILU: tile_epilogue_w4<VS_EPI_SILU, false, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a); break;
+        case VS_EPI_GATE_RES:
+            if (ep.hint) tile_epilogue_w4<VS_EPI_GATE_RES, true, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a);
+            else tile_epilogue_w4<VS_EPI_GATE_RES, false, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a);
+            break;
+        case VS_EPI_RES: tile_epilogue_w4<VS_EPI_RES, false, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a); break;
+        default: tile_epilogue_w4<VS_EPI_BIAS, false, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a); break;
+    }
+}
+
 constexpr int W4_ROWB = 1056;                 // LDS row: 8 global rows x 128 B + 32 B pad
 constexpr int W4_OPB = 32 * W4_ROWB;          // one operand's K-tile image (256 rows x 64 k)
 constexpr int W4_LDS = 4 * W4_OPB;            // [A b0][A b1][W b0][W b1] = 135168 B
 
-template <bool WIDE>
+// Work of one 4w block.  Blocks [0, npers) are persistent: each walks tiles_per tiles of its XCD's
+// contiguous chunk of [0, npers * tiles_per) (block b: XCD b % 8, slot b / 8, tiles slot, slot + G8, ..)
+// as ONE stream of K-tiles -- the DMA runs two K-tiles ahead straight across tile boundaries, so a
+// tile's first K-tiles land during the previous tile's last iterations and its epilogue (no prologue
+// wait, no per-tile launch).  The blocks after them run one whole tile each (up to nmain) and then
+// the split-tail K pieces of the last tiles.
+struct W4Work {
+    int ntw;          // tiles in this block's list
+    int piece;        // split-tail piece (-1: whole tiles)
+    int kb, nt;       // K offset (elements) and K-tiles per tile
+    int p0, pstep;    // tile ids: p0 + k * pstep (persistent), or p0
+};
+__device__ __forceinline__ W4Work w4_work(int K, int nmain, int ksplit, int piece_k, int npers, int tiles_per, int kstep) {
+    W4Work w;
+    const int b = blockIdx.x;
+    w.piece = -1;
+    w.kb = 0;
+    w.nt = K / kstep;
+    if (b < npers) {
+        const int g8 = npers >> 3;
+        w.ntw = tiles_per;
+        w.p0 = (b & 7) * (g8 * tiles_per) + (b >> 3);
+        w.pstep = g8;
+    } else if (b < npers + (nmain - npers * tiles_per)) {
+        w.ntw = 1;
+        w.p0 = npers * tiles_per + (b - npers);
+        w.pstep = 0;
+    } else {
+        const int t = b - npers - (nmain - npers * tiles_per);
+        w.ntw = 1;
+        w.p0 = nmain + t / ksplit;
+        w.pstep = 0;
+        w.piece = t % ksplit;
+        w.kb = w.piece * piece_k;
+        w.nt = min(K - w.kb, piece_k) / kstep;
+    }
+    return w;
+}
+
+template <int MODE, bool HINT>
 __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
     bf16_t* C, long long ldc, int M, int N, int K, Epi ep, int ntm, int ntn, int nmain, int ksplit,
-    int piece_k, float* __restrict__ part) {
+    int piece_k, float* __restrict__ part, int npers, int tiles_per) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-
-    int pid, piece = -1;
-    if ((int)blockIdx.x < nmain) {
-        pid = xcd_remap(blockIdx.x, nmain);
-    } else {
-        const int t = blockIdx.x - nmain;
-        pid = nmain + t / ksplit;
-        piece = t % ksplit;
-    }
-    int tm, tn;
-    tile_of(pid, ntm, ntn, tm, tn);
-    const int m0 = tm * 256, n0 = tn * 256;
-    const int kb = piece < 0 ? 0 : piece * piece_k;
-    const int nt = (piece < 0 ? K : min(K - kb, piece_k)) / 64;
+    const W4Work wk = w4_work(K, nmain, ksplit, piece_k, npers, tiles_per, 64);
+    const int nt = wk.nt;
+    desync_start(ep);
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
 
     f32x4_t acc[8][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     // DMA: instruction j of wave w fills LDS row 4j + w of an operand image; lane L lands in column
     // block L / 8, chunk L % 8 = global row 128 (rho / 16) + 16 (L / 8) + rho % 16, bytes 16 (L % 8)..
-    // (rows past the matrix re-read its last row; their outputs are discarded).  Row offsets are
-    // formed once (16 VGPRs); the K-tile offset goes in soffset.
-    auto rsrc = [](const void* base) {
-        return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
-    };
-    const __amdgpu_buffer_rsrc_t ra = rsrc(A + (long long)m0 * lda + kb);
-    const __amdgpu_buffer_rsrc_t rw = rsrc(W + (long long)n0 * ldw + kb);
-    const int alim = M - 1 - m0, wlim = N - 1 - n0;
+    // Instruction j's rows are those of instruction 0 plus 4j (+112 from j = 4): one per-lane offset
+    // per operand plus the wave-uniform row step of j, added into voffset at the DMA (vadd_opq); the
+    // K-tile offset goes in soffset.  Rows past the matrix fall outside the resource's range (rebased
+    // on the tile, num_records = the bytes of its remaining rows) and load 0; their outputs are
+    // discarded.  The DMA cursor (tile dk, K-tile dkt) runs two K-tiles ahead of the compute; past the
+    // block's last K-tile it re-reads that K-tile (into the buffer no later read uses), which keeps
+    // every iteration's wait counts identical.
     const unsigned ldab = (unsigned)(lda * 2), ldwb = (unsigned)(ldw * 2);
-    unsigned voa[8], vow[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int rho = 4 * j + wave;
-        const int g = (rho >> 4) * 128 + 16 * (lane >> 3) + (rho & 15);
-        voa[j] = (unsigned)min(g, alim) * ldab + 16u * (lane & 7);
-        vow[j] = (unsigned)min(g, wlim) * ldwb + 16u * (lane & 7);
-    }
+    auto rsrc_rows = [](const bf16_t* base, long long rows, unsigned ldb) {
+        const long long bytes = rows > 0 ? rows * (long long)ldb : 0;
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base), 0, (int)min(bytes, 0x7fffffffLL), 0x00020000);
+    };
+    const unsigned vo0 = (unsigned)(16 * (lane >> 3) + wave) * 0u + 16u * (lane & 7);
+    const unsigned grow0 = (unsigned)(16 * (lane >> 3) + wave);     // row of instruction 0
+    const unsigned voa0 = grow0 * ldab + vo0, vow0 = grow0 * ldwb + vo0;
+    __amdgpu_buffer_rsrc_t ra, rw;
+    auto dma_tile = [&](int k) {
+        int tm, tn;
+        tile_of(wk.p0 + k * wk.pstep, ntm, ntn, tm, tn);
+        const int m0 = tm * 256, n0 = tn * 256;
+        ra = rsrc_rows(A + (long long)m0 * lda + wk.kb, M - m0, ldab);
+        rw = rsrc_rows(W + (long long)n0 * ldw + wk.kb, N - n0, ldwb);
+    };
+    auto jrow = [](int j) { return 4 * j + (j >= 4 ? 112 : 0); };
+    int dk = 0, dkt = 0;
+    auto dma_advance = [&]() {
+        if (++dkt == nt) {
+            if (dk + 1 < wk.ntw) {
+                ++dk;
+                dkt = 0;
+                dma_tile(dk);
+            } else {
+                dkt = nt - 1;
+            }
+        }
+    };
     // LDS-DMA destinations (wave-uniform byte offsets of the wave's first row in the current
     // buffer) and the per-lane fragment bases; both toggle between the two buffers by XOR once per
     // K-tile, so the loop body is one instance with immediate ds_read offsets
     unsigned dw = 2 * W4_OPB + wave * W4_ROWB, da = wave * W4_ROWB;
     const unsigned dw_tog = dw ^ (dw + W4_OPB), da_tog = da ^ (da + W4_OPB);
     auto dma_w = [&](unsigned ko, int j) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (LDS_AS void*)(smem + dw + 4 * j * W4_ROWB), 16, vow[j], ko, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (LDS_AS void*)(smem + dw + 4 * j * W4_ROWB), 16,
+                                                 vadd_opq((int)vow0, jrow(j) * (int)ldwb), ko, 0, 0);
     };
     auto dma_a = [&](unsigned ko, int j) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(smem + da + 4 * j * W4_ROWB), 16, voa[j], ko, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(smem + da + 4 * j * W4_ROWB), 16,
+                                                 vadd_opq((int)voa0, jrow(j) * (int)ldab), ko, 0, 0);
     };
 
     // fragment bases (lane: row l % 16 of the wave's LDS rows, 16-B chunk l / 16), kept opaque so
@@ -706,132 +1009,146 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
         asm volatile("s_barrier" ::: "memory");
         fence();
     };
+    auto read_k0 = [&]() {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fw0[j] = frag(wbase + 128 * j);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) fa0[i] = frag(abase + 128 * i);
+        fence();
+    };
 
-    // K-tile offsets in bytes; past the last K-tile the DMA re-reads it (into the buffer no later
-    // read uses), which keeps every iteration's wait counts identical
-    const unsigned klast = (unsigned)(nt - 1) * 128u;
-    auto kofs = [&](int t) { return min((unsigned)t * 128u, klast); };
-
-    // prologue: K-tiles 0 and 1 in flight (W then A each), then the k-step-0 fragments of tile 0
+    // prologue: K-tiles 0 and 1 of the stream in flight (W then A each), then the k-step-0 fragments
+    dma_tile(0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) dma_w(0, j);
 #pragma unroll
     for (int j = 0; j < 8; ++j) dma_a(0, j);
+    dma_advance();
     dw ^= dw_tog;
     da ^= da_tog;
+    {
+        const unsigned ko = (unsigned)dkt * 128u;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dma_w(kofs(1), j);
+        for (int j = 0; j < 8; ++j) dma_w(ko, j);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dma_a(kofs(1), j);
+        for (int j = 0; j < 8; ++j) dma_a(ko, j);
+    }
+    dma_advance();
     dw ^= dw_tog;
     da ^= da_tog;
-    fence();
-    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-    bar();
-#pragma unroll
-    for (int j = 0; j < 8; ++j) fw0[j] = frag(wbase + 128 * j);
     fence();
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     bar();
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa0[i] = frag(abase + 128 * i);
-    fence();
+    read_k0();
 
-    // one K-tile t: 128 MFMAs with, before MFMA q, the reads / DMA / barriers of this table
-#pragma nounroll
-    for (int t = 0; t < nt; ++t) {
-        const unsigned ko = kofs(t + 2);
-        static_for<128>([&](auto qc) __attribute__((always_inline)) {
-            constexpr int q = decltype(qc)::value;
-            if constexpr (q < 16 && (q & 1)) fw1[q >> 1] = frag(wbase + 128 * (q >> 1) + 64);
-            if constexpr (q == 17) wbase ^= wtog;                          // next buffer's W fragments
-            if constexpr (q == 20) wait_lgkm_bar();                        // W region of this buffer free
-            if constexpr (q >= 21 && q <= 37 && (q - 21) % 4 == 0) dma_w(ko, (q - 21) / 4);
-            if constexpr (q >= 23 && q <= 39 && (q - 23) % 4 == 0) fa1[(q - 23) / 4] = frag(abase + 128 * ((q - 23) / 4) + 64);
-            if constexpr (q >= 41 && q <= 45 && (q & 1)) fa1[5 + (q - 41) / 2] = frag(abase + 128 * (5 + (q - 41) / 2) + 64);
-            if constexpr (q == 47) abase ^= atog;
-            if constexpr (q == 52) wait_lgkm_bar();                        // A region of this buffer free
-            if constexpr (q == 53 || q == 56 || q == 59) dma_w(ko, 5 + (q - 53) / 3);
-            if constexpr (q == 62) dma_a(ko, 0);
-            if constexpr (q == 65) dma_a(ko, 1);
-            if constexpr (q == 69) {                                       // W of K-tile t+1 landed
-                fence();
-                asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-                bar();
-            }
-            if constexpr (q >= 70 && q <= 84 && !(q & 1)) fw0[(q - 70) / 2] = frag(wbase + 128 * ((q - 70) / 2));
-            if constexpr (q >= 86 && q <= 98 && (q - 86) % 3 == 0) dma_a(ko, 2 + (q - 86) / 3);
-            if constexpr (q == 101) {                                      // A of K-tile t+1 landed
-                fence();
-                asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
-                bar();
-            }
-            if constexpr (q >= 102 && q <= 116 && !(q & 1)) fa0[(q - 102) / 2] = frag(abase + 128 * ((q - 102) / 2));
-            if constexpr (q == 122) dma_a(ko, 7);
-            // MFMA q: k-step q / 64, tile (i, j) = ((q % 64) / 8, q % 8).  Inline asm with the
-            // accumulator tied in place: the 256 accumulators then fill the AGPR file exactly (the
-            // builtin let the register allocator rename them per MFMA: AGPR copies and spills)
-            constexpr int i = (q & 63) >> 3, j = q & 7;
-            if constexpr (q < 64)
-                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fw0[j]), "v"(fa0[i]));
-            else
-                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fw1[j]), "v"(fa1[i]));
-            fence();
-        });
-        dw ^= dw_tog;
-        da ^= da_tog;
-    }
-    // drain the re-read DMAs of the last two iterations; the accumulators leave through
-    // v_accvgpr_read: cover the last MFMAs' write latency by hand (the hazard recognizer does not
-    // see into the asm statements)
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-
-    // output: acc[i][j][e] = C[m][n], m = m0 + 128 wm + 16 i + (lane & 15), n = n0 + 128 wn + 16 j + 4 (lane >> 4) + e
-    if (piece >= 0) {
-        float* pp = part + ((long long)(pid - nmain) * ksplit + piece) * 256 * 256;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                *reinterpret_cast<f32x4_t*>(pp + (128 * wm + 16 * i + (lane & 15)) * 256 + 128 * wn + 16 * j +
-                                            4 * (lane >> 4)) = acc[i][j];
-        return;
-    }
-    if constexpr (WIDE) {
-        // 16-B epilogue: column blocks (2p, 2p+1) traded between lane groups g, g^1 (permlane16_swap,
-        // as gemm_bf16_tn_8p): an even-g lane ends with columns 32p + 4g .. +7, an odd-g lane with
-        // 32p + 16 + 4(g-1) .. +7
-        const int g = lane >> 4;
-        const int nw = 16 * (g & 1) + 4 * (g & ~1);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int m = m0 + 128 * wm + 16 * i + (lane & 15);
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                float v[8];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float x = acc[i][2 * p][e], y = acc[i][2 * p + 1][e];
-                    const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-                    v[e] = __uint_as_float(sw[0]);
-                    v[4 + e] = __uint_as_float(sw[1]);
+    // one K-tile: 128 MFMAs with, before MFMA q, the reads / DMA / barriers of this table.  FIRST:
+    // the tile's first K-tile, whose k-step-0 MFMAs start the accumulators from 0 (no zeroing pass,
+    // and no accumulator value live across the tile loop: the register allocator otherwise copied
+    // and spilled the 256 accumulators around the epilogue)
+    auto ktile = [&](auto firstc) __attribute__((always_inline)) {
+            constexpr bool FIRST = decltype(firstc)::value;
+            const unsigned ko = (unsigned)dkt * 128u;
+            static_for<128>([&](auto qc) __attribute__((always_inline)) {
+                constexpr int q = decltype(qc)::value;
+                if constexpr (q < 16 && (q & 1)) fw1[q >> 1] = frag(wbase + 128 * (q >> 1) + 64);
+                if constexpr (q == 17) wbase ^= wtog;                          // next buffer's W fragments
+                if constexpr (q == 20) wait_lgkm_bar();                        // W region of this buffer free
+                if constexpr (q >= 21 && q <= 37 && (q - 21) % 4 == 0) dma_w(ko, (q - 21) / 4);
+                if constexpr (q >= 23 && q <= 39 && (q - 23) % 4 == 0) fa1[(q - 23) / 4] = frag(abase + 128 * ((q - 23) / 4) + 64);
+                if constexpr (q >= 41 && q <= 45 && (q & 1)) fa1[5 + (q - 41) / 2] = frag(abase + 128 * (5 + (q - 41) / 2) + 64);
+                if constexpr (q == 47) abase ^= atog;
+                if constexpr (q == 52) wait_lgkm_bar();                        // A region of this buffer free
+                if constexpr (q == 53 || q == 56 || q == 59) dma_w(ko, 5 + (q - 53) / 3);
+                if constexpr (q == 62) dma_a(ko, 0);
+                if constexpr (q == 65) dma_a(ko, 1);
+                if constexpr (q == 69) {                                       // W of the next K-tile landed
+                    fence();
+                    asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+                    bar();
                 }
-                const int n = n0 + 128 * wn + 32 * p + nw;
-                if (m < M && n < N) epilogue_store_w<8>(v, m, n, C, ldc, ep);
-            }
-        }
-        return;
-    }
+                if constexpr (q >= 70 && q <= 84 && !(q & 1)) fw0[(q - 70) / 2] = frag(wbase + 128 * ((q - 70) / 2));
+                if constexpr (q >= 86 && q <= 98 && (q - 86) % 3 == 0) dma_a(ko, 2 + (q - 86) / 3);
+                if constexpr (q == 101) {                                      // A of the next K-tile landed
+                    fence();
+                    asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+                    bar();
+                }
+                if constexpr (q >= 102 && q <= 116 && !(q & 1)) fa0[(q - 102) / 2] = frag(abase + 128 * ((q - 102) / 2));
+                if constexpr (q == 122) dma_a(ko, 7);
+                // MFMA q: k-step q / 64, tile (i, j) = ((q % 64) / 8, q % 8).  Inline asm with the
+                // accumulator tied in place: the 256 accumulators then fill the AGPR file exactly (the
+                // builtin let the register allocator rename them per MFMA: AGPR copies and spills)
+                constexpr int i = (q & 63) >> 3, j = q & 7;
+                if constexpr (q < 64 && FIRST)
+                    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc[i][j]) : "v"(fw0[j]), "v"(fa0[i]));
+                else if constexpr (q < 64)
+                    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fw0[j]), "v"(fa0[i]));
+                else
+                    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fw1[j]), "v"(fa1[i]));
+                fence();
+            });
+            dw ^= dw_tog;
+            da ^= da_tog;
+            dma_advance();
+    };
+
+#pragma nounroll
+    for (int k = 0; k < wk.ntw; ++k) {
+        ktile(std::true_type{});
+#pragma nounroll
+        for (int t = 1; t < nt; ++t) ktile(std::false_type{});
+        // the accumulators leave through v_accvgpr_read: cover the last MFMAs' write latency by hand
+        // (the hazard recognizer does not see into the asm statements)
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+
+        int tm, tn;
+        tile_of(wk.p0 + k * wk.pstep, ntm, ntn, tm, tn);
+        const int m0 = tm * 256, n0 = tn * 256;
+        // output: acc[i][j][e] = C[m][n], m = m0 + 128 wm + 16 i + (lane & 15), n = n0 + 128 wn + 16 j + 4 (lane >> 4) + e
+#ifndef W4_DIAG_NOEPI
+        if (wk.piece >= 0) {
+            // fp32 partial tile through one buffer resource: a per-lane offset, the row block i in
+            // soffset and the column block j in the immediate (64 precomputed 64-bit addresses,
+            // hoisted out of the tile loop by the compiler, were spilled)
+            const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+                part + ((long long)(wk.p0 - nmain) * ksplit + wk.piece) * 256 * 256, 0, 256 * 256 * 4, 0x00020000);
+            const int vo = ((128 * wm + (lane & 15)) * 256 + 128 * wn + 4 * (lane >> 4)) * 4;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int m = m0 + 128 * wm + 16 * i + (lane & 15);
-        if (m >= M) continue;
+            for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int n = n0 + 128 * wn + 16 * j + 4 * (lane >> 4);
-            if (n >= N) continue;
-            epilogue_store(acc[i][j], m, n, C, ldc, ep);
+                for (int j = 0; j < 8; ++j)
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        u32x4_t{__float_as_uint(acc_rd(acc[i][j][0])), __float_as_uint(acc_rd(acc[i][j][1])),
+                                __float_as_uint(acc_rd(acc[i][j][2])), __float_as_uint(acc_rd(acc[i][j][3]))},
+                        rp, vo, 16 * i * 256 * 4 + 64 * j, 0);
+        } else {
+            // 16-B epilogue (host-checked alignment): column blocks (2p, 2p+1) traded between lane
+            // groups g, g^1 (permlane16_swap): an even-g lane ends with columns 32p + 4g .. +7, an
+            // odd-g lane with 32p + 16 + 4(g-1) .. +7; loads issued ahead (tile_epilogue_w4).  One
+            // epilogue mode per kernel instantiation (the runtime switch's six bodies beside the
+            // 256 live accumulators overflowed the register file)
+#ifdef W4_NARROW
+            tile_epilogue_w4n<MODE, HINT, false>(acc, m0 + 128 * wm, n0 + 128 * wn, lane, C, ldc, M, N, ep, nullptr);
+#else
+            tile_epilogue_w4<MODE, HINT, false>(acc, m0 + 128 * wm, n0 + 128 * wn, lane, C, ldc, M, N, ep, nullptr);
+#endif
         }
+#else
+        if (W4_DIAG_NOEPI == 1 && wk.piece >= 0) {
+            float* pp = part + ((long long)(wk.p0 - nmain) * ksplit + wk.piece) * 256 * 256;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    *reinterpret_cast<f32x4_t*>(pp + (128 * wm + 16 * i + (lane & 15)) * 256 + 128 * wn + 16 * j +
+                                                4 * (lane >> 4)) = acc[i][j];
+        } else if (W4_DIAG_NOEPI == 2) {
+            tile_epilogue_w4<MODE, HINT, false>(acc, m0 + 128 * wm, n0 + 128 * wn, lane, C, ldc, M, N, ep, nullptr);
+        }
+#endif
+        // the epilogue's loads and stores leave the counted DMA waits of the next tile exact
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (k + 1 < wk.ntw) read_k0();      // the next tile's k-step-0 fragments (its first K-tile has landed)
     }
 }
 
@@ -1259,26 +1576,7 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
         return;
     }
     if constexpr (WIDE) {
-        const int g = lane >> 4;
-        const int nw = 16 * (g & 1) + 4 * (g & ~1);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int m = m0 + 128 * wm + 16 * i + (lane & 15);
-            const float sa = scale_a[min(m, M - 1)];
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                float v[8];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float x = acc[i][2 * p][e], y = acc[i][2 * p + 1][e];
-                    const auto swp = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-                    v[e] = __uint_as_float(swp[0]) * sa;
-                    v[4 + e] = __uint_as_float(swp[1]) * sa;
-                }
-                const int n = n0 + 128 * wn + 32 * p + nw;
-                if (m < M && n < N) epilogue_store_w<8>(v, m, n, C, ldc, ep);
-            }
-        }
+        tile_epilogue_w4_dispatch<true>(acc, m0 + 128 * wm, n0 + 128 * wn, lane, C, ldc, M, N, ep, scale_a);
         return;
     }
 #pragma unroll
@@ -1465,6 +1763,8 @@ static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n)
     ep.rows_per_batch = m;
     ep.alpha = 1.f;
     ep.hint_scale = 1.f;
+    const char* ds = getenv("VS_GEMM_DESYNC");
+    ep.desync = ds ? atoi(ds) : 0;
     if (epi) {
         ep.bias = (const bf16_t*)epi->bias;
         ep.res = (const bf16_t*)epi->residual;
@@ -1543,17 +1843,27 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
             part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
             if (!part) sp = KSplit{tm * tn, 0, 1, 0};
         }
-        if (k2 == 0 && use_4w()) {
+        if (k2 == 0 && wide && use_4w()) {
+            using K4 = void (*)(const bf16_t*, long long, const bf16_t*, long long, bf16_t*, long long, int, int, int,
+                                Epi, int, int, int, int, int, float*, int, int);
+            static const K4 kern4[6] = {gemm_bf16_tn_4w<VS_EPI_BIAS, false>, gemm_bf16_tn_4w<VS_EPI_GELU, false>,
+                                        gemm_bf16_tn_4w<VS_EPI_SILU, false>, gemm_bf16_tn_4w<VS_EPI_GATE_RES, false>,
+                                        gemm_bf16_tn_4w<VS_EPI_RES, false>, gemm_bf16_tn_4w<VS_EPI_GATE_RES, true>};
             static bool attr4 = false;
             if (!attr4) {
-                for (const void* f : {(const void*)gemm_bf16_tn_4w<false>, (const void*)gemm_bf16_tn_4w<true>})
-                    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS);
+                for (const K4 f : kern4)
+                    (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS);
                 attr4 = true;
             }
-            hipLaunchKernelGGL(wide ? gemm_bf16_tn_4w<true> : gemm_bf16_tn_4w<false>,
-                               dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(256), W4_LDS,
+            const K4 kf = kern4[(ep.mode == VS_EPI_GATE_RES && ep.hint) ? 5 : ep.mode];
+            // persistent blocks (one per CU) over the first floor(nmain / CUs) * CUs tiles
+            const int cus = vs_cus_for_split(nullptr);
+            const int npers = (cus >= 8 && cus % 8 == 0 && sp.nmain >= cus && !getenv("VS_GEMM_NO_PERSIST")) ? cus : 0;
+            const int tiles_per = npers ? sp.nmain / npers : 0;
+            const unsigned grid = (unsigned)(npers + (sp.nmain - npers * tiles_per) + sp.ntail * sp.ksplit);
+            hipLaunchKernelGGL(kf, dim3(grid), dim3(256), W4_LDS,
                                (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw, (bf16_t*)c, ldc, m,
-                               n, k, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part);
+                               n, k, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part, npers, tiles_per);
             VS_CHECK_LAUNCH();
         } else {
         hipLaunchKernelGGL(k2 ? (wide ? gemm_bf16_tn_8p<true, true> : gemm_bf16_tn_8p<true, false>)
