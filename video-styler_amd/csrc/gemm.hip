@@ -653,7 +653,11 @@ __device__ __forceinline__ void unpack8(const u32x4_t& w, float* v) {
 // hardware checks soffset) without the compiler hoisting one VGPR per row step out of the loop
 __device__ __forceinline__ int vadd_opq(int v, int s) {
     int r;
+#if defined(__HIP_DEVICE_COMPILE__)         // (x86 reads "s" / "a" as register names: device pass only)
     asm volatile("v_add_u32 %0, %1, %2" : "=v"(r) : "s"(s), "v"(v));
+#else
+    r = v + s;
+#endif
     return r;
 }
 
@@ -662,7 +666,11 @@ __device__ __forceinline__ int vadd_opq(int v, int s) {
 // operands) and the overflow spilled to scratch
 __device__ __forceinline__ float acc_rd(float a) {
     float v;
+#if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(v) : "a"(a));
+#else
+    v = a;
+#endif
     return v;
 }
 
@@ -924,6 +932,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
     bf16_t* C, long long ldc, int M, int N, int K, Epi ep, int ntm, int ntn, int nmain, int ksplit,
     int piece_k, float* __restrict__ part, int npers, int tiles_per) {
+#if defined(__HIP_DEVICE_COMPILE__)     // (the AGPR asm operands are not host constraints)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const W4Work wk = w4_work(K, nmain, ksplit, piece_k, npers, tiles_per, 64);
     const int nt = wk.nt;
@@ -1150,6 +1159,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (k + 1 < wk.ntw) read_k0();      // the next tile's k-step-0 fragments (its first K-tile has landed)
     }
+#endif
 }
 
 
@@ -1846,7 +1856,8 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
         if (k2 == 0 && wide && use_4w()) {
             using K4 = void (*)(const bf16_t*, long long, const bf16_t*, long long, bf16_t*, long long, int, int, int,
                                 Epi, int, int, int, int, int, float*, int, int);
-            static const K4 kern4[6] = {gemm_bf16_tn_4w<VS_EPI_BIAS, false>, gemm_bf16_tn_4w<VS_EPI_GELU, false>,
+            // (a static table's constant initializer left the kernels' host stubs un-instantiated)
+            const K4 kern4[6] = {gemm_bf16_tn_4w<VS_EPI_BIAS, false>, gemm_bf16_tn_4w<VS_EPI_GELU, false>,
                                         gemm_bf16_tn_4w<VS_EPI_SILU, false>, gemm_bf16_tn_4w<VS_EPI_GATE_RES, false>,
                                         gemm_bf16_tn_4w<VS_EPI_RES, false>, gemm_bf16_tn_4w<VS_EPI_GATE_RES, true>};
             static bool attr4 = false;
