@@ -682,15 +682,18 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
     const int ncol = 16 * (g & 1) + 4 * (g & ~1);         // lane's column within a 32-column pair block
     const int nl = n_w + ncol;                            // + 32 p
     const int r = lane & 15;                              // + 16 i
-    // buffer resources rebased on the wave's first row: one voffset per lane, the row step i in
-    // soffset and the column block p in the immediate offset (no 64-bit address per access);
-    // rows past M read as 0 (range), their stores are masked
+    // buffer resources rebased on the wave's first row, num_records = the bytes of its rows < M:
+    // one voffset per lane plus the row step i (vadd_opq) and the column block p (no 64-bit address
+    // per access); rows past M read as 0 and their stores are dropped by the range check
     const int rows = max(0, min(128, M - m_w));
+    // (num_records through readfirstlane: the compiler formed the clamp with its 128 in a VGPR and
+    // then wrapped every access in a waterfall loop)
     auto rsrc = [&](const bf16_t* base, long long ld, bool load) {
         return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base + (long long)m_w * ld), 0,
-                                                 load ? (int)((long long)rows * ld * 2) : 0x7fffffff, 0x00020000);
+                                                 load ? __builtin_amdgcn_readfirstlane((int)((long long)rows * ld * 2))
+                                                      : 0x7fffffff, 0x00020000);
     };
-    const __amdgpu_buffer_rsrc_t rc = rsrc(C, ldc, false);
+    const __amdgpu_buffer_rsrc_t rc = rsrc(C, ldc, true);
     const int vo_c = (int)((r * ldc + n_w + ncol) * 2);
     u32x4_t bw[4];
 #pragma unroll
@@ -772,10 +775,12 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
 #pragma unroll
                 for (int e = 0; e < 8; ++e) y[e] = rv[e] + rbf(ep.alpha * y[e]);
             }
-            if (m < M && nl + 32 * p < N)
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    u32x4_t{pack2(y[0], y[1]), pack2(y[2], y[3]), pack2(y[4], y[5]), pack2(y[6], y[7])}, rc,
-                    vo_c, (int)(16 * i * ldc * 2) + 64 * p, 0);
+            // rows past M fall outside rc's range, columns past N get an offset outside it: the
+            // hardware drops those stores (no per-store branch)
+            const int so = vadd_opq(vo_c, (int)(16 * i * ldc * 2)) + 64 * p;
+            __builtin_amdgcn_raw_buffer_store_b128(
+                u32x4_t{pack2(y[0], y[1]), pack2(y[2], y[3]), pack2(y[4], y[5]), pack2(y[6], y[7])}, rc,
+                nl + 32 * p < N ? so : 0x7ffffff0, 0, 0);
             // one column block at a time: the scheduler would otherwise hoist the accumulator reads
             // of later blocks (AGPR -> VGPR copies) and run out of VGPRs
             __builtin_amdgcn_sched_barrier(0);
@@ -796,9 +801,12 @@ __device__ __forceinline__ void tile_epilogue_w4n(const AccT& acc, int m_w, int 
     const int nl = n_w + ncol;                            // + 16 j
     const int r = lane & 15;                              // + 16 i
     const int rows = max(0, min(128, M - m_w));
+    // (num_records through readfirstlane: the compiler formed the clamp with its 128 in a VGPR and
+    // then wrapped every access in a waterfall loop)
     auto rsrc = [&](const bf16_t* base, long long ld, bool load) {
         return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base + (long long)m_w * ld), 0,
-                                                 load ? (int)((long long)rows * ld * 2) : 0x7fffffff, 0x00020000);
+                                                 load ? __builtin_amdgcn_readfirstlane((int)((long long)rows * ld * 2))
+                                                      : 0x7fffffff, 0x00020000);
     };
     const __amdgpu_buffer_rsrc_t rc = rsrc(C, ldc, false);
     const int vo_c = (int)((r * ldc + n_w + ncol) * 2);
