@@ -1720,9 +1720,19 @@ bool vs_lt_is_private();
 // (0.3831 / 0.3843 vs 0.3888 / 0.3894 steps/s, same box, interleaved; in the step the kernel ran
 // 6.38 ms per launch: profiles/r3/bench_own_sp1_ab.log, step_breakdown_own_sp1.txt), so the SP = 1
 // block GEMMs stay on the library.
+static bool use_4w();
 static bool own_wins(int m, int n, int k, int epilogue) {
-    return (k >= 12288 && m <= 16384) || (epilogue == VS_EPI_GELU && k <= 8192 && m <= 8192) ||
-           ((epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES) && k <= 8192 && m <= 8192);
+    const bool resid = epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES;
+    if ((k >= 12288 && m <= 16384) || (epilogue == VS_EPI_GELU && k <= 8192 && m <= 8192) ||
+        (resid && k <= 8192 && m <= 8192))
+        return true;
+    // r4, the persistent 4-wave kernel: the fused gate-residual o-proj at every row count (59 280
+    // rows: 1393 vs 1305 TF/s for the library + its epilogue pass, gemm_w4p_ab.log); VS_GEMM_OWN=0
+    // keeps the r3 routing, =2 adds the gate-residual FFN-down at any row count (1399 vs 1419)
+    const char* o = getenv("VS_GEMM_OWN");
+    const int lvl = o ? atoi(o) : 1;
+    if (!use_4w() || lvl <= 0) return false;
+    return (resid && k <= 8192) || (lvl >= 2 && resid);
 }
 static bool lt_route(int m, int n, int k, int epilogue = VS_EPI_BIAS) {
     const char* e = getenv("VS_GEMM_BACKEND");
@@ -1768,10 +1778,11 @@ static bool lt_with_epilogue(void* c, long long ldc, int m, int n, int epilogue,
     return true;
 }
 
-// which 256x256 kernel runs the un-split-phase (k2 == 0) GEMMs: VS_GEMM_KERNEL=4w|8p
+// which 256x256 kernel runs the un-split-phase (k2 == 0) GEMMs: VS_GEMM_KERNEL=4w (default since
+// r4: 1-5 % over the 8-phase kernel on every 14B shape at 59 280 and 7410 rows) | 8p
 static bool use_4w() {
     const char* e = getenv("VS_GEMM_KERNEL");
-    return e && e[0] == '4';
+    return !(e && e[0] == '8');
 }
 
 static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n) {
@@ -1959,7 +1970,8 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
         part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
         if (!part) sp = KSplit{tm * tn, 0, 1, 0};
     }
-    if (use_4w()) {
+    const char* fk = getenv("VS_GEMM_KERNEL");      // the fp8 4-wave kernel: opt-in (VS_GEMM_KERNEL=4w)
+    if (fk && fk[0] == '4') {
         static bool attr4 = false;
         if (!attr4) {
             for (const void* f : {(const void*)gemm_fp8_tn_4w<false>, (const void*)gemm_fp8_tn_4w<true>})
