@@ -43,6 +43,7 @@ struct Epi {
     int rows_per_batch;
     int mode;
     int desync;       // diagnostic (VS_GEMM_DESYNC): the first round's blocks sleep (b % 256) / 256 x this many ~4 us units
+    int gm;           // M-tiles per raster group of the 256x256 tile order (VS_GEMM_GM, default VS_GEMM_GM)
 };
 
 // staggered start of the first round of blocks (diagnostic: do tile epilogues that coincide on
@@ -234,8 +235,7 @@ constexpr int BT = 256;
 
 // tile id -> (tm, tn): raster groups of GM M-tiles sweep all N-tiles, so consecutive ids on one
 // XCD share the weight tile in L2
-__device__ __forceinline__ void tile_of(int pid, int ntm, int ntn, int& tm, int& tn) {
-    constexpr int GM = VS_GEMM_GM;
+__device__ __forceinline__ void tile_of(int pid, int ntm, int ntn, int GM, int& tm, int& tn) {
     const int per_group = GM * ntn;
     const int group = pid / per_group;
     const int first_m = group * GM;
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(256) void gemm_split_combine(const float* __restric
     const int rem = (int)(idx % (BT * (BT / 4)));
     const int row = rem / (BT / 4), c4 = rem % (BT / 4);
     int tm, tn;
-    tile_of(nmain + t, ntm, ntn, tm, tn);
+    tile_of(nmain + t, ntm, ntn, ep.gm, tm, tn);
     const int m = tm * BT + row, n = tn * BT + 4 * c4;
     if (m >= M || n >= N) return;
     const float* pp = part + (long long)t * ksplit * BT * BT + row * BT + 4 * c4;
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
         piece = t % ksplit;
     }
     int tm, tn;
-    tile_of(pid, ntm, ntn, tm, tn);
+    tile_of(pid, ntm, ntn, ep.gm, tm, tn);
     const int m0 = tm * T8, n0 = tn * T8;
     desync_start(ep);
     const int kb = piece < 0 ? 0 : piece * piece_k;
@@ -620,6 +620,9 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
 // straight-line expansion f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>): every
 // index is a compile-time constant (a 128-step #pragma unroll loop is not fully unrolled by hipcc,
 // leaving the fragment arrays runtime-indexed, i.e. in scratch)
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+
 template <class F, int... Q>
 __device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Q...>) {
     (f(std::integral_constant<int, Q>{}), ...);
@@ -895,6 +898,7 @@ __device__ __forceinline__ void tile_epilogue_w4_dispatch(const AccT& acc, int m
 constexpr int W4_ROWB = 1056;                 // LDS row: 8 global rows x 128 B + 32 B pad
 constexpr int W4_OPB = 32 * W4_ROWB;          // one operand's K-tile image (256 rows x 64 k)
 constexpr int W4_LDS = 4 * W4_OPB;            // [A b0][A b1][W b0][W b1] = 135168 B
+static_assert(4 * W4_ROWB == 0x1080, "the 4w kernel's M0 step");
 
 // Work of one 4w block.  Blocks [0, npers) are persistent: each walks tiles_per tiles of its XCD's
 // contiguous chunk of [0, npers * tiles_per) (block b: XCD b % 8, slot b / 8, tiles slot, slot + G8, ..)
@@ -935,6 +939,18 @@ __device__ __forceinline__ W4Work w4_work(int K, int nmain, int ksplit, int piec
     return w;
 }
 
+// the DMA issued before MFMA q of a K-tile of gemm_bf16_tn_4w (-1: none): W instructions 0-7 as
+// d = 0-7, A instructions 0-7 as d = 8-15 (the library kernel's placement, see the body)
+constexpr int w4_dma_at(int q) {
+    return (q >= 21 && q <= 37 && (q - 21) % 4 == 0) ? (q - 21) / 4
+         : (q == 53 || q == 56 || q == 59)             ? 5 + (q - 53) / 3
+         : q == 62                                     ? 8
+         : q == 65                                     ? 9
+         : (q >= 86 && q <= 98 && (q - 86) % 3 == 0)   ? 10 + (q - 86) / 3
+         : q == 122                                    ? 15
+                                                       : -1;
+}
+
 template <int MODE, bool HINT>
 __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
@@ -954,30 +970,49 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
 
     // DMA: instruction j of wave w fills LDS row 4j + w of an operand image; lane L lands in column
     // block L / 8, chunk L % 8 = global row 128 (rho / 16) + 16 (L / 8) + rho % 16, bytes 16 (L % 8)..
-    // Instruction j's rows are those of instruction 0 plus 4j (+112 from j = 4): one per-lane offset
-    // per operand plus the wave-uniform row step of j, added into voffset at the DMA (vadd_opq); the
-    // K-tile offset goes in soffset.  Rows past the matrix fall outside the resource's range (rebased
-    // on the tile, num_records = the bytes of its remaining rows) and load 0; their outputs are
-    // discarded.  The DMA cursor (tile dk, K-tile dkt) runs two K-tiles ahead of the compute; past the
-    // block's last K-tile it re-reads that K-tile (into the buffer no later read uses), which keeps
-    // every iteration's wait counts identical.
+    // i.e. instruction j's rows are those of instruction 0 plus 4j (+112 from j = 4).  As in the
+    // library's kernel, a DMA is ONE instruction: the 16 per-lane row offsets are formed once (tile-
+    // invariant: the resources are rebased on the tile), the K-tile offset is folded into the
+    // resource base (advanced per K-tile, num_records shrunk with it), and M0 (the LDS destination)
+    // is written in the MFMA gap before the load -- no address VALU and no s_nop per DMA (r4: the
+    // per-DMA v_add + hazard nop were 2 of the 4 instructions of every DMA group).  Rows past the
+    // matrix fall outside the resource's range and load 0; their outputs are discarded.  The DMA
+    // cursor (tile dk, K-tile dkt) runs two K-tiles ahead of the compute; past the block's last
+    // K-tile it re-reads that K-tile (into the buffer no later read uses), which keeps every
+    // iteration's wait counts identical.  The DMAs are inline asm, invisible to the compiler's wait
+    // counting (its own waits only grow stricter with older loads in flight); the protocol waits are
+    // the hand-placed vmcnt below and the vmcnt(0) after each tile's epilogue.
     const unsigned ldab = (unsigned)(lda * 2), ldwb = (unsigned)(ldw * 2);
-    auto rsrc_rows = [](const bf16_t* base, long long rows, unsigned ldb) {
-        const long long bytes = rows > 0 ? rows * (long long)ldb : 0;
-        return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base), 0, (int)min(bytes, 0x7fffffffLL), 0x00020000);
+    auto rsrc4 = [](const char* base, int bytes) {      // (readfirstlane: an "s" operand)
+        const unsigned long long a = (unsigned long long)(uintptr_t)base;
+        return i32x4_t{__builtin_amdgcn_readfirstlane((int)(unsigned)a),
+                       __builtin_amdgcn_readfirstlane((int)((unsigned)(a >> 32) & 0xffffu)),
+                       __builtin_amdgcn_readfirstlane(bytes), 0x00020000};
     };
-    const unsigned vo0 = (unsigned)(16 * (lane >> 3) + wave) * 0u + 16u * (lane & 7);
-    const unsigned grow0 = (unsigned)(16 * (lane >> 3) + wave);     // row of instruction 0
-    const unsigned voa0 = grow0 * ldab + vo0, vow0 = grow0 * ldwb + vo0;
-    __amdgpu_buffer_rsrc_t ra, rw;
-    auto dma_tile = [&](int k) {
-        int tm, tn;
-        tile_of(wk.p0 + k * wk.pstep, ntm, ntn, tm, tn);
-        const int m0 = tm * 256, n0 = tn * 256;
-        ra = rsrc_rows(A + (long long)m0 * lda + wk.kb, M - m0, ldab);
-        rw = rsrc_rows(W + (long long)n0 * ldw + wk.kb, N - n0, ldwb);
+    auto rows_bytes = [](int rows, unsigned ldb) {
+        return (int)((long long)max(0, min(rows, 256)) * (long long)ldb);
     };
     auto jrow = [](int j) { return 4 * j + (j >= 4 ? 112 : 0); };
+    const unsigned grow0 = (unsigned)(16 * (lane >> 3) + wave);     // row of instruction 0
+    unsigned voa[8], vow[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        voa[j] = (grow0 + (unsigned)jrow(j)) * ldab + 16u * (lane & 7);
+        vow[j] = (grow0 + (unsigned)jrow(j)) * ldwb + 16u * (lane & 7);
+        asm volatile("" : "+v"(voa[j]), "+v"(vow[j]));     // kept, not re-formed per use
+    }
+    const char* abp = nullptr;
+    const char* wbp = nullptr;
+    int arec = 0, wrec = 0;
+    auto dma_tile = [&](int k) {
+        int tm, tn;
+        tile_of(wk.p0 + k * wk.pstep, ntm, ntn, ep.gm, tm, tn);
+        const int m0 = tm * 256, n0 = tn * 256;
+        abp = (const char*)(A + (long long)m0 * lda + wk.kb);
+        wbp = (const char*)(W + (long long)n0 * ldw + wk.kb);
+        arec = rows_bytes(M - m0, ldab);
+        wrec = rows_bytes(N - n0, ldwb);
+    };
     int dk = 0, dkt = 0;
     auto dma_advance = [&]() {
         if (++dkt == nt) {
@@ -995,13 +1030,28 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     // K-tile, so the loop body is one instance with immediate ds_read offsets
     unsigned dw = 2 * W4_OPB + wave * W4_ROWB, da = wave * W4_ROWB;
     const unsigned dw_tog = dw ^ (dw + W4_OPB), da_tog = da ^ (da + W4_OPB);
-    auto dma_w = [&](unsigned ko, int j) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (LDS_AS void*)(smem + dw + 4 * j * W4_ROWB), 16,
-                                                 vadd_opq((int)vow0, jrow(j) * (int)ldwb), ko, 0, 0);
+    const unsigned lds0 = (unsigned)(uintptr_t)smem;
+    i32x4_t rsa, rsw;                   // the current K-tile's resources (set at each DMA K-tile)
+    auto ktile_rsrc = [&](unsigned ko) {
+        rsa = rsrc4(abp + ko, arec - (int)ko);
+        rsw = rsrc4(wbp + ko, wrec - (int)ko);
     };
-    auto dma_a = [&](unsigned ko, int j) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(smem + da + 4 * j * W4_ROWB), 16,
-                                                 vadd_opq((int)voa0, jrow(j) * (int)ldab), ko, 0, 0);
+    // DMA d of a K-tile: d < 8 W instruction d, else A instruction d - 8
+    auto dma_lds = [&](int d) { return lds0 + (d < 8 ? dw + 4 * d * W4_ROWB : da + 4 * (d - 8) * W4_ROWB); };
+    // M0: set at an operand's first instruction, then stepped by one 4-row group (4 x 1056 B) --
+    // one SALU per DMA, as the library's kernel (nothing between these statements writes M0)
+    auto m0_set = [&](int d) {
+        if (d == 0 || d == 8) asm volatile("s_mov_b32 m0, %0" :: "s"(dma_lds(d)) : "m0");
+        else asm volatile("s_add_u32 m0, m0, 0x1080" ::: "m0");
+    };
+    auto dma_go = [&](int d) {
+        if (d < 8) asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" :: "v"(vow[d]), "s"(rsw) : "memory");
+        else asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" :: "v"(voa[d - 8]), "s"(rsa) : "memory");
+    };
+    auto dma_now = [&](int d) {                     // outside the pipelined body: M0, nop, load
+        asm volatile("s_mov_b32 m0, %0" :: "s"(dma_lds(d)) : "m0");
+        asm volatile("s_nop 0" ::: "memory");
+        dma_go(d);
     };
 
     // fragment bases (lane: row l % 16 of the wave's LDS rows, 16-B chunk l / 16), kept opaque so
@@ -1036,20 +1086,15 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
 
     // prologue: K-tiles 0 and 1 of the stream in flight (W then A each), then the k-step-0 fragments
     dma_tile(0);
+    ktile_rsrc(0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dma_w(0, j);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dma_a(0, j);
+    for (int d = 0; d < 16; ++d) dma_now(d);
     dma_advance();
     dw ^= dw_tog;
     da ^= da_tog;
-    {
-        const unsigned ko = (unsigned)dkt * 128u;
+    ktile_rsrc((unsigned)dkt * 128u);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) dma_w(ko, j);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) dma_a(ko, j);
-    }
+    for (int d = 0; d < 16; ++d) dma_now(d);
     dma_advance();
     dw ^= dw_tog;
     da ^= da_tog;
@@ -1064,34 +1109,33 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     // and spilled the 256 accumulators around the epilogue)
     auto ktile = [&](auto firstc) __attribute__((always_inline)) {
             constexpr bool FIRST = decltype(firstc)::value;
-            const unsigned ko = (unsigned)dkt * 128u;
+            ktile_rsrc((unsigned)dkt * 128u);
             static_for<128>([&](auto qc) __attribute__((always_inline)) {
                 constexpr int q = decltype(qc)::value;
                 if constexpr (q < 16 && (q & 1)) fw1[q >> 1] = frag(wbase + 128 * (q >> 1) + 64);
                 if constexpr (q == 17) wbase ^= wtog;                          // next buffer's W fragments
                 if constexpr (q == 20) wait_lgkm_bar();                        // W region of this buffer free
-                if constexpr (q >= 21 && q <= 37 && (q - 21) % 4 == 0) dma_w(ko, (q - 21) / 4);
                 if constexpr (q >= 23 && q <= 39 && (q - 23) % 4 == 0) fa1[(q - 23) / 4] = frag(abase + 128 * ((q - 23) / 4) + 64);
                 if constexpr (q >= 41 && q <= 45 && (q & 1)) fa1[5 + (q - 41) / 2] = frag(abase + 128 * (5 + (q - 41) / 2) + 64);
                 if constexpr (q == 47) abase ^= atog;
                 if constexpr (q == 52) wait_lgkm_bar();                        // A region of this buffer free
-                if constexpr (q == 53 || q == 56 || q == 59) dma_w(ko, 5 + (q - 53) / 3);
-                if constexpr (q == 62) dma_a(ko, 0);
-                if constexpr (q == 65) dma_a(ko, 1);
                 if constexpr (q == 69) {                                       // W of the next K-tile landed
                     fence();
                     asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
                     bar();
                 }
                 if constexpr (q >= 70 && q <= 84 && !(q & 1)) fw0[(q - 70) / 2] = frag(wbase + 128 * ((q - 70) / 2));
-                if constexpr (q >= 86 && q <= 98 && (q - 86) % 3 == 0) dma_a(ko, 2 + (q - 86) / 3);
                 if constexpr (q == 101) {                                      // A of the next K-tile landed
                     fence();
                     asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
                     bar();
                 }
                 if constexpr (q >= 102 && q <= 116 && !(q & 1)) fa0[(q - 102) / 2] = frag(abase + 128 * ((q - 102) / 2));
-                if constexpr (q == 122) dma_a(ko, 7);
+                // the 16 DMAs of K-tile t+2 (W 0-4 every 4 MFMAs from 21 after the W-free barrier, W 5-7
+                // and A 0-1 after the A-free barrier, A 2-6 between the landing waits, A 7 last), each
+                // with its M0 written one MFMA earlier
+                if constexpr (w4_dma_at(q) >= 0) dma_go(w4_dma_at(q));
+                if constexpr (w4_dma_at(q + 1) >= 0) m0_set(w4_dma_at(q + 1));
                 // MFMA q: k-step q / 64, tile (i, j) = ((q % 64) / 8, q % 8).  Inline asm with the
                 // accumulator tied in place: the 256 accumulators then fill the AGPR file exactly (the
                 // builtin let the register allocator rename them per MFMA: AGPR copies and spills)
@@ -1119,7 +1163,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
         asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
 
         int tm, tn;
-        tile_of(wk.p0 + k * wk.pstep, ntm, ntn, tm, tn);
+        tile_of(wk.p0 + k * wk.pstep, ntm, ntn, ep.gm, tm, tn);
         const int m0 = tm * 256, n0 = tn * 256;
         // output: acc[i][j][e] = C[m][n], m = m0 + 128 wm + 16 i + (lane & 15), n = n0 + 128 wn + 16 j + 4 (lane >> 4) + e
 #ifndef W4_DIAG_NOEPI
@@ -1171,7 +1215,6 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
 }
 
 
-typedef int i32x8_t __attribute__((ext_vector_type(8)));
 
 // ---------------------------------------------------------------------------------------------
 // gemm_fp8_tn_8p: the 8-phase skeleton of gemm_bf16_tn_8p for the fp8 path (config 5;
@@ -1204,7 +1247,7 @@ __global__ __launch_bounds__(512, 2) void gemm_fp8_tn_8p(
         piece = t % ksplit;
     }
     int tm, tn;
-    tile_of(pid, ntm, ntn, tm, tn);
+    tile_of(pid, ntm, ntn, ep.gm, tm, tn);
     const int m0 = tm * T8, n0 = tn * T8;
     const int kb = piece < 0 ? 0 : piece * piece_k;
     const int Kp = piece < 0 ? K : min(K - kb, piece_k);
@@ -1437,7 +1480,7 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
         piece = t % ksplit;
     }
     int tm, tn;
-    tile_of(pid, ntm, ntn, tm, tn);
+    tile_of(pid, ntm, ntn, ep.gm, tm, tn);
     const int m0 = tm * 256, n0 = tn * 256;
     const int kb = piece < 0 ? 0 : piece * piece_k;
     const int nt = (piece < 0 ? K : min(K - kb, piece_k)) / 128;
@@ -1794,6 +1837,8 @@ static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n)
     ep.hint_scale = 1.f;
     const char* ds = getenv("VS_GEMM_DESYNC");
     ep.desync = ds ? atoi(ds) : 0;
+    const char* gm = getenv("VS_GEMM_GM");
+    ep.gm = gm && atoi(gm) > 0 ? atoi(gm) : VS_GEMM_GM;
     if (epi) {
         ep.bias = (const bf16_t*)epi->bias;
         ep.res = (const bf16_t*)epi->residual;
