@@ -1010,8 +1010,8 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
         const int m0 = tm * 256, n0 = tn * 256;
         abp = (const char*)(A + (long long)m0 * lda + wk.kb);
         wbp = (const char*)(W + (long long)n0 * ldw + wk.kb);
-        arec = rows_bytes(M - m0, ldab);
-        wrec = rows_bytes(N - n0, ldwb);
+        arec = __builtin_amdgcn_readfirstlane(rows_bytes(M - m0, ldab));
+        wrec = __builtin_amdgcn_readfirstlane(rows_bytes(N - n0, ldwb));
     };
     int dk = 0, dkt = 0;
     auto dma_advance = [&]() {
@@ -1039,10 +1039,14 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     // DMA d of a K-tile: d < 8 W instruction d, else A instruction d - 8
     auto dma_lds = [&](int d) { return lds0 + (d < 8 ? dw + 4 * d * W4_ROWB : da + 4 * (d - 8) * W4_ROWB); };
     // M0: set at an operand's first instruction, then stepped by one 4-row group (4 x 1056 B) --
-    // one SALU per DMA, as the library's kernel (nothing between these statements writes M0)
+    // one SALU per DMA, as the library's kernel (nothing between these statements writes M0).
+    // m0_step_note: the step declares no "m0" clobber -- with it the hazard recognizer put an
+    // s_nop before every step that follows an MFMA (the library's kernel steps M0 right after
+    // MFMAs with no nop); the compiler is told of the M0 write by the s_mov that starts each run,
+    // and nothing in this kernel reads M0 but these DMAs
     auto m0_set = [&](int d) {
         if (d == 0 || d == 8) asm volatile("s_mov_b32 m0, %0" :: "s"(dma_lds(d)) : "m0");
-        else asm volatile("s_add_u32 m0, m0, 0x1080" ::: "m0");
+        else asm volatile("s_add_u32 m0, m0, 0x1080" ::: "memory");   // (see m0_step_note)
     };
     auto dma_go = [&](int d) {
         if (d < 8) asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" :: "v"(vow[d]), "s"(rsw) : "memory");
@@ -1462,6 +1466,7 @@ __global__ __launch_bounds__(512, 2) void gemm_fp8_tn_8p(
 constexpr int F4_ROWB = 1088;
 constexpr int F4_OPB = 32 * F4_ROWB;
 constexpr int F4_LDS = 4 * F4_OPB;            // [A b0][A b1][W b0][W b1] = 139264 B
+static_assert(4 * F4_ROWB == 0x1100, "the fp8 4w kernel's M0 step");
 __device__ __forceinline__ int f4_swz(int r) { return ((r >> 3) & 1) * 3; }
 
 template <bool WIDE>
@@ -1495,11 +1500,16 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    auto rsrc = [](const void* base) {
-        return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+    // the DMAs are inline asm, one instruction each: M0 (the LDS destination) is set at an operand's
+    // first instruction and stepped by 4 rows (4 x 1088 B) one MFMA ahead of the next, so no hazard
+    // nop sits in the MFMA stream (the bf16 kernel's r4 change, see gemm_bf16_tn_4w)
+    auto rsrc4 = [](const uint8_t* base) {
+        const unsigned long long a = (unsigned long long)(uintptr_t)base;
+        return i32x4_t{__builtin_amdgcn_readfirstlane((int)(unsigned)a),
+                       __builtin_amdgcn_readfirstlane((int)((unsigned)(a >> 32) & 0xffffu)), 0x7fffffff, 0x00020000};
     };
-    const __amdgpu_buffer_rsrc_t ra = rsrc(A + (long long)m0 * lda + kb);
-    const __amdgpu_buffer_rsrc_t rw = rsrc(W + (long long)n0 * ldw + kb);
+    const i32x4_t ra = rsrc4(A + (long long)m0 * lda + kb);
+    const i32x4_t rw = rsrc4(W + (long long)n0 * ldw + kb);
     const int alim = M - 1 - m0, wlim = N - 1 - n0;
     unsigned voa[8], vow[8];
 #pragma unroll
@@ -1512,12 +1522,23 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
     }
     unsigned dw = 2 * F4_OPB + wave * F4_ROWB, da = wave * F4_ROWB;
     const unsigned dw_tog = dw ^ (dw + F4_OPB), da_tog = da ^ (da + F4_OPB);
-    auto dma_w = [&](unsigned ko, int j) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (LDS_AS void*)(smem + dw + 4 * j * F4_ROWB), 16, vow[j], ko, 0, 0);
+    const unsigned lds0 = (unsigned)(uintptr_t)smem;
+    // DMA d: W instruction d (d < 8) or A instruction d - 8
+    auto m0_set = [&](int d) {
+        if (d == 0 || d == 8) asm volatile("s_mov_b32 m0, %0" :: "s"(lds0 + (d == 0 ? dw : da)) : "m0");
+        else asm volatile("s_add_u32 m0, m0, 0x1100" ::: "memory");   // (see m0_step_note)
     };
-    auto dma_a = [&](unsigned ko, int j) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(smem + da + 4 * j * F4_ROWB), 16, voa[j], ko, 0, 0);
+    auto dma_go = [&](unsigned ko, int d) {
+        if (d < 8) asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" :: "v"(vow[d]), "s"(rw), "s"(ko) : "memory");
+        else asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" :: "v"(voa[d - 8]), "s"(ra), "s"(ko) : "memory");
     };
+    auto dma_now = [&](unsigned ko, int d) {
+        asm volatile("s_mov_b32 m0, %0" :: "s"(lds0 + (d < 8 ? dw + 4 * d * F4_ROWB : da + 4 * (d - 8) * F4_ROWB)) : "m0");
+        asm volatile("s_nop 0" ::: "memory");
+        dma_go(ko, d);
+    };
+    auto dma_w = [&](unsigned ko, int j) { dma_now(ko, j); };
+    auto dma_a = [&](unsigned ko, int j) { dma_now(ko, 8 + j); };
 
     // fragment bases: the two 16-B halves of a lane's 32 B (logical chunks 2c, 2c+1 of row r)
     const int fr = lane & 15, fc = lane >> 4, sw = f4_swz(fr);
@@ -1601,11 +1622,7 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
                 asm volatile("s_barrier" ::: "memory");
                 fence();
             }
-            if constexpr (q >= 11 && q <= 56 && (q - 11) % 3 == 0) {
-                constexpr int d = (q - 11) / 3;
-                if constexpr (d < 8) dma_w(ko, d);
-                else dma_a(ko, d - 8);
-            }
+            if constexpr (q >= 11 && q <= 56 && (q - 11) % 3 == 0) dma_go(ko, (q - 11) / 3);
             if constexpr (q == 29) {                                                 // K-tile t+1 landed
                 fence();
                 asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -1616,6 +1633,7 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
             // MFMA q: rows 0-3 i-major, then rows 4-7 column by column
             constexpr int i = q < 32 ? (q >> 3) : 4 + ((q - 32) & 3);
             constexpr int j = q < 32 ? (q & 7) : (q - 32) >> 2;
+            if constexpr (q >= 10 && q <= 55 && (q - 10) % 3 == 0) m0_set((q - 10) / 3);   // DMA of MFMA q + 1
             asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
                          : "+a"(acc[i][j]) : "v"(fw[j]), "v"(fa[i]), "v"(unit));
             fence();
@@ -1771,11 +1789,12 @@ static bool own_wins(int m, int n, int k, int epilogue) {
         return true;
     // r4, the persistent 4-wave kernel: the fused gate-residual o-proj at every row count (59 280
     // rows: 1393 vs 1305 TF/s for the library + its epilogue pass, gemm_w4p_ab.log); VS_GEMM_OWN=0
-    // keeps the r3 routing, =2 adds the gate-residual FFN-down at any row count (1399 vs 1419)
+    // keeps the r3 routing, =2 adds the gate-residual FFN-down at any row count (1399 vs 1419),
+    // =3 the GELU FFN-up
     const char* o = getenv("VS_GEMM_OWN");
     const int lvl = o ? atoi(o) : 1;
     if (!use_4w() || lvl <= 0) return false;
-    return (resid && k <= 8192) || (lvl >= 2 && resid);
+    return (resid && k <= 8192) || (lvl >= 2 && resid) || (lvl >= 3 && epilogue == VS_EPI_GELU);
 }
 static bool lt_route(int m, int n, int k, int epilogue = VS_EPI_BIAS) {
     const char* e = getenv("VS_GEMM_BACKEND");
