@@ -82,6 +82,12 @@ int vs_gemm_split_plan(int m, int n, int k, int cus, int* out);
  * kernels, VS_E_INVALID for non-positive sizes.  Honours VS_GEMM_BACKEND.  Host-only.
  */
 int vs_gemm_route(int m, int n, int k);
+/* the same for a GEMM with epilogue `epilogue` (VS_EPI_*), bf16 (fp8 = 0, vs_gemm) or fp8 (fp8 = 1,
+ * vs_gemm_fp8): 1 = hipBLASLt + a separate epilogue pass, 0 = the MFMA kernel's fused epilogue
+ * (the host fuses a residual epilogue with the next LayerNorm only on the former route),
+ * -VS_E_INVALID for non-positive sizes or an unknown epilogue (negative: never a route).  Honours
+ * VS_GEMM_BACKEND / VS_GEMM_OWN / VS_GEMM_KERNEL (bf16) and VS_FP8_BACKEND (fp8).  Host-only. */
+int vs_gemm_route_epi(int m, int n, int k, int epilogue, int fp8);
 
 /*
  * fp8 path (config 5; AutoWrappedLinear.fp8_linear, diffsynth/vram_management/layers.py:115-151):

@@ -181,6 +181,28 @@ def test_gemm_route_rule(monkeypatch):
     assert lib.vs_gemm_route(59280, 5120, 64) == 1          # patch embedding: 4640 tiles
     assert lib.vs_gemm_route(1024, 1536, 4096) == 0         # 24 tiles, N 1536
     assert lib.vs_gemm_route(0, 1, 1) == _lib.VS_E_INVALID if hasattr(_lib, "VS_E_INVALID") else lib.vs_gemm_route(0, 1, 1) != 0
+    # vs_gemm_route_epi: r4, the gate-residual / residual GEMMs on the 4-wave kernel's fused epilogue
+    # (VS_GEMM_OWN=2 default: o-proj and FFN-down), the plain-bias q|k|v on hipBLASLt; fp8 (auto):
+    # the library only for bias-only GEMMs with N >= 2K
+    G, R, B, GL = 3, 4, 0, 1
+    monkeypatch.delenv("VS_GEMM_OWN", raising=False)
+    monkeypatch.delenv("VS_GEMM_KERNEL", raising=False)
+    monkeypatch.delenv("VS_FP8_BACKEND", raising=False)
+    assert lib.vs_gemm_route_epi(59280, 5120, 5120, G, 0) == 0      # o-proj + gate-residual
+    assert lib.vs_gemm_route_epi(59280, 5120, 5120, R, 0) == 0      # cross-attention o + residual
+    assert lib.vs_gemm_route_epi(59280, 5120, 13824, G, 0) == 0     # FFN-down + gate-residual
+    assert lib.vs_gemm_route_epi(59280, 15360, 5120, B, 0) == 1     # q|k|v
+    assert lib.vs_gemm_route_epi(59280, 5120, 5120, B, 0) == lib.vs_gemm_route(59280, 5120, 5120)
+    assert lib.vs_gemm_route_epi(59280, 15360, 5120, B, 1) == 1     # fp8 q|k|v: hipBLASLt fp8
+    assert lib.vs_gemm_route_epi(59280, 5120, 5120, G, 1) == 0      # fp8 o-proj: the MFMA kernel
+    assert lib.vs_gemm_route_epi(59280, 13824, 5120, GL, 1) == 0    # fp8 FFN-up
+    assert lib.vs_gemm_route_epi(59280, 5120, 5120, 9, 0) < 0       # invalid epilogue
+    monkeypatch.setenv("VS_GEMM_OWN", "0")
+    assert lib.vs_gemm_route_epi(59280, 5120, 5120, G, 0) == 1      # the r3 routing
+    monkeypatch.setenv("VS_FP8_BACKEND", "lt")
+    assert lib.vs_gemm_route_epi(59280, 5120, 5120, G, 1) == 1
+    monkeypatch.setenv("VS_FP8_BACKEND", "vstyler")
+    assert lib.vs_gemm_route_epi(59280, 15360, 5120, B, 1) == 0
     monkeypatch.setenv("VS_GEMM_BACKEND", "vstyler")
     assert lib.vs_gemm_route(59280, 5120, 5120) == 0
     monkeypatch.setenv("VS_GEMM_BACKEND", "lt")

@@ -1787,12 +1787,13 @@ static bool own_wins(int m, int n, int k, int epilogue) {
     if ((k >= 12288 && m <= 16384) || (epilogue == VS_EPI_GELU && k <= 8192 && m <= 8192) ||
         (resid && k <= 8192 && m <= 8192))
         return true;
-    // r4, the persistent 4-wave kernel: the fused gate-residual o-proj at every row count (59 280
-    // rows: 1393 vs 1305 TF/s for the library + its epilogue pass, gemm_w4p_ab.log); VS_GEMM_OWN=0
-    // keeps the r3 routing, =2 adds the gate-residual FFN-down at any row count (1399 vs 1419),
-    // =3 the GELU FFN-up
+    // r4, the persistent 4-wave kernel with one-instruction DMAs: the residual-epilogue GEMMs at every
+    // row count (59 280 rows: o-proj + gate-residual 1441 vs 1292 TF/s for the library + its epilogue
+    // pass, FFN-down 1475 vs 1426; profiles/r4/gemm_gm_w4_ab.log).  VS_GEMM_OWN: 0 = the r3 routing,
+    // 1 = + residual epilogues with K <= 8192, 2 (default) = + every residual epilogue, 3 = + the GELU
+    // FFN-up (1418 vs 1408 alone, -0.3 % in the step: bench_route2_ab.log)
     const char* o = getenv("VS_GEMM_OWN");
-    const int lvl = o ? atoi(o) : 1;
+    const int lvl = o ? atoi(o) : 2;
     if (!use_4w() || lvl <= 0) return false;
     return (resid && k <= 8192) || (lvl >= 2 && resid) || (lvl >= 3 && epilogue == VS_EPI_GELU);
 }
@@ -1994,6 +1995,7 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
     return VS_OK;
 }
 
+static bool fp8_lt_route(int n, int k, int epilogue);
 extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, const void* w8, long long ldw,
                            void* c, long long ldc, int m, int n, int k, int epilogue, const vs_epilogue* epi,
                            void* stream) {
@@ -2005,14 +2007,16 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
     Epi ep;
     const int rc = fill_epi(ep, epilogue, epi, m, n);
     if (rc) return rc;
-    // hipBLASLt fp8 (OCP e4m3 operands, per-token fp32 scale vector as hipBLASLt's outer B scale)
-    // + the epilogue pass: 1.3-1.6x the fp8 MFMA kernel on every 14B block shape at SP=1 and SP=8
-    // and bit-identical to it, epilogues included (profiles/r1/gemm_fp8_lt_r1j.log).
-    // VS_FP8_BACKEND=vstyler forces the MFMA kernel, which also runs when no workspace is bound.
-    // GELU as in vs_gemm: hipBLASLt's fused GELU_BIAS epilogue only with VS_LT_GELU=1.
-    const char* fb = getenv("VS_FP8_BACKEND");      // lt (default) | vstyler (the 8-phase MFMA kernel)
+    // Routes (VS_FP8_BACKEND=auto (default) | vstyler | lt).  r4: the 4-wave MFMA kernel
+    // (gemm_fp8_tn_4w, one-instruction DMAs) runs the fused-epilogue block GEMMs ahead of hipBLASLt
+    // fp8 + its epilogue pass at 59 280 rows -- o-proj + gate-residual 2483 vs 2204 TF/s, FFN-up +
+    // GELU 2676 vs 2541, FFN-down + gate-residual 2883 vs 2803 -- and behind it only on the plain-bias
+    // q|k|v projection (2807 vs 3067, profiles/r4/gemm_fp8_w4_ab.log), so auto keeps the library for
+    // bias-only GEMMs with N >= 2K (the fused q|k|v) and runs everything else on the MFMA kernel; the
+    // routes are bit-identical (integer-data tests).  The MFMA kernel also runs when no workspace is
+    // bound.  GELU as in vs_gemm: hipBLASLt's fused GELU_BIAS epilogue only with VS_LT_GELU=1.
     const char* lt_gelu = getenv("VS_LT_GELU");
-    const bool use_lt = !(fb && fb[0] == 'v');
+    const bool use_lt = fp8_lt_route(n, k, epilogue);
     if (use_lt && epilogue == VS_EPI_GELU && (lt_gelu && lt_gelu[0] == '1') &&
         vs_lt_gemm_fp8(a8, lda, scale_a, w8, ldw, c, ldc, m, n, k, ep.bias, true, (hipStream_t)stream) == VS_OK)
         return VS_OK;
@@ -2021,7 +2025,7 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
             return vs_lt_gemm_fp8(a8, lda, scale_a, w8, ldw, y, ldy, m, n, k, ep.bias, false, (hipStream_t)stream);
         }))
         return VS_OK;
-    // the fp8 8-phase MFMA kernel (K-tiles of 128 fp8)
+    // the fp8 MFMA kernels (K-tiles of 128 fp8)
     const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
     static bool attr8 = false;
     if (!attr8) {
@@ -2034,8 +2038,8 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
         part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
         if (!part) sp = KSplit{tm * tn, 0, 1, 0};
     }
-    const char* fk = getenv("VS_GEMM_KERNEL");      // the fp8 4-wave kernel: opt-in (VS_GEMM_KERNEL=4w)
-    if (fk && fk[0] == '4') {
+    const char* fk = getenv("VS_GEMM_KERNEL");      // the 4-wave kernel unless VS_GEMM_KERNEL=8p
+    if (!(fk && fk[0] == '8')) {
         static bool attr4 = false;
         if (!attr4) {
             for (const void* f : {(const void*)gemm_fp8_tn_4w<false>, (const void*)gemm_fp8_tn_4w<true>})
@@ -2079,6 +2083,17 @@ extern "C" int vs_quant_fp8_rows(const void* x, long long ldx, void* x8, long lo
 extern "C" int vs_gemm_route(int m, int n, int k) {
     if (m <= 0 || n <= 0 || k <= 0) return VS_E_INVALID;
     return lt_route(m, n, k) ? 1 : 0;
+}
+
+// the route of a GEMM with a given epilogue (the residual epilogues decide between the MFMA
+// kernel's fused epilogue and hipBLASLt's staged output + the fused residual-LayerNorm pass)
+static bool fp8_lt_route(int n, int k, int epilogue) {
+    const char* fb = getenv("VS_FP8_BACKEND");
+    return fb && fb[0] == 'v' ? false : fb && fb[0] == 'l' ? true : epilogue == VS_EPI_BIAS && n >= 2 * k;
+}
+extern "C" int vs_gemm_route_epi(int m, int n, int k, int epilogue, int fp8) {
+    if (m <= 0 || n <= 0 || k <= 0 || epilogue < VS_EPI_BIAS || epilogue > VS_EPI_RES) return -VS_E_INVALID;
+    return (fp8 ? fp8_lt_route(n, k, epilogue) : lt_route(m, n, k, epilogue)) ? 1 : 0;
 }
 
 extern "C" int vs_gemm_split_plan(int m, int n, int k, int cus, int* out) {

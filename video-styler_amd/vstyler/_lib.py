@@ -61,6 +61,7 @@ SIGNATURES = {
     "vs_attn_split_plan": [_I, _I, _I, _I, _I, _P],
     "vs_gemm_split_plan": [_I, _I, _I, _I, _P],
     "vs_gemm_route": [_I, _I, _I],
+    "vs_gemm_route_epi": [_I, _I, _I, _I, _I],
     "vs_split_workspace_bytes": [_I],
     "vs_blaslt_library": [],
     "vs_split_workspace_bind": [_I, _P, _LL, _P],

@@ -107,7 +107,7 @@ def gemm(a, w, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, g
     if k2 == 0:
         _split_ws(1, a)
         _split_ws(2, a)
-        if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES) and _lt_route(M, N, K):
+        if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES) and _lt_route(M, N, K, epilogue):
             _split_ws(3, a, M * N * 2)       # staging for the hipBLASLt route (vs_gemm decides)
     _lib.check(_lib.load().vs_gemm(a.data_ptr(), lda, w.data_ptr(), ldw, out.data_ptr(), ldc, M, N, K,
                                    int(epilogue), ep, _ptr(a2), lda2, _ptr(w2), ldw2, k2, _stream(a)))
@@ -131,10 +131,10 @@ def quant_fp8_rows(x, x8, scale):
     return x8, scale
 
 
-def _lt_route(M, N, K):
-    """vs_gemm's routing decision (vs_gemm_route): the shim binds the epilogue staging buffer for
-    GEMMs that go to hipBLASLt."""
-    return gemm_route(M, N, K)
+def _lt_route(M, N, K, epilogue=None):
+    """vs_gemm's routing decision (vs_gemm_route[_epi]): the shim binds the epilogue staging buffer
+    for GEMMs that go to hipBLASLt."""
+    return gemm_route(M, N, K, epilogue=epilogue)
 
 
 def gemm_fp8(a8, scale_a, w8, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, gate_bstride=0,
@@ -219,9 +219,13 @@ def residual_layernorm(y, x, out, eps=1e-6, epilogue=VS_EPI_GATE_RES, gate=None,
     return out
 
 
-def gemm_route(M, N, K):
-    """1 if vs_gemm sends an (M, N, K) GEMM without LoRA phase to hipBLASLt (vs_gemm_route)."""
-    return _lib.load().vs_gemm_route(int(M), int(N), int(K)) == 1
+def gemm_route(M, N, K, epilogue=None, fp8=False):
+    """True if vs_gemm (vs_gemm_fp8 with fp8=True) sends an (M, N, K) GEMM without LoRA phase and
+    with `epilogue` to hipBLASLt + a separate epilogue pass (vs_gemm_route / vs_gemm_route_epi)."""
+    if epilogue is None and not fp8:
+        return _lib.load().vs_gemm_route(int(M), int(N), int(K)) == 1
+    ep = VS_EPI_BIAS if epilogue is None else int(epilogue)
+    return _lib.load().vs_gemm_route_epi(int(M), int(N), int(K), ep, 1 if fp8 else 0) == 1
 
 
 def rmsnorm_rope(x, weight, eps=1e-6, rope=None, grid=(1, 1, 1), rows_per_batch=0, token_offset=0, head_dim=128):

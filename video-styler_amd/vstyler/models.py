@@ -56,17 +56,17 @@ def linear(lin, x, out, ws, **epi):
     return K.gemm(x, lin.weight, out, bias=lin.bias, a2=a2, w2=w2, **epi)
 
 
-def _fusable_lt(lin, M):
-    """True when `lin` on M rows runs on hipBLASLt (a plain bf16 GEMM on vs_gemm's hipBLASLt route, or
-    the fp8 path, which is always hipBLASLt unless VS_FP8_BACKEND=vstyler), i.e. when its residual
-    epilogue is a separate pass over a staged bf16(acc + bias) anyway: that pass can then fuse with
-    the LayerNorm that follows (vs_residual_layernorm) with the same rounding points.  A hot-loaded
-    LoRA keeps the MFMA kernel's fused epilogue.  VSTYLER_FUSE_RES_LN=0 disables."""
+def _fusable_lt(lin, M, epilogue):
+    """True when `lin` on M rows with the residual `epilogue` would run on hipBLASLt (vs_gemm /
+    vs_gemm_fp8's library route: vs_gemm_route_epi), i.e. when that epilogue is a separate pass over
+    a staged bf16(acc + bias) anyway: the pass then fuses with the LayerNorm that follows
+    (vs_residual_layernorm) with the same rounding points.  On the MFMA kernels the residual epilogue
+    is fused into the GEMM instead and the LayerNorm runs alone.  A hot-loaded LoRA keeps the MFMA
+    kernel's fused epilogue.  VSTYLER_FUSE_RES_LN=0 disables."""
     if getattr(lin, "lora_A", None) is not None or os.environ.get("VSTYLER_FUSE_RES_LN", "1") == "0":
         return False
-    if getattr(lin, "weight_fp8", None) is not None:
-        return not os.environ.get("VS_FP8_BACKEND", "").startswith("v")
-    return K.gemm_route(M, lin.out_features, lin.in_features)
+    fp8 = getattr(lin, "weight_fp8", None) is not None
+    return K.gemm_route(M, lin.out_features, lin.in_features, epilogue=epilogue, fp8=fp8)
 
 
 def quantize_fp8_(module):
@@ -338,7 +338,7 @@ class DiTBlock(nn.Module):
         # the fused FFN-down epilogue needs the consumer's modulation first (its own mod buffer)
         fuse = None
         if nxt is not None and only_batch is None and \
-                _fusable_lt(self.ffn[2], (tail or parts[0])["M"]) and \
+                _fusable_lt(self.ffn[2], (tail or parts[0])["M"], K.VS_EPI_GATE_RES) and \
                 os.environ.get("VSTYLER_FUSE_FFN_LN", "1") != "0":
             if isinstance(nxt, DiTBlock):
                 nslot = rc.mod_slot ^ 1
@@ -411,7 +411,7 @@ class DiTBlock(nn.Module):
         if rc.sp is not None:
             rc.sp.finish(p["xchg"], o)
         sa = self.self_attn
-        if _fusable_lt(sa.o, M):
+        if _fusable_lt(sa.o, M, K.VS_EPI_GATE_RES):
             # hipBLASLt route: bf16(o Wo^T + b) staged, then gate-residual + LN3 in one pass
             y = ws.get("res_y" + p["tag"], (M, D))
             linear(sa.o, o, y, ws)
@@ -439,7 +439,7 @@ class DiTBlock(nn.Module):
             linear(ca.v, p["ctx"], vc, ws)
         K.rmsnorm_rope(kc, ca.norm_k.weight, eps)
         K.attention(q, kc, vc, o, self.num_heads, nb)
-        if _fusable_lt(ca.o, M):
+        if _fusable_lt(ca.o, M, K.VS_EPI_RES):
             y = ws.get("res_y" + p["tag"], (M, D))
             linear(ca.o, o, y, ws)
             K.residual_layernorm(y, x, h, eps, epilogue=K.VS_EPI_RES, alpha=1.0, shift=mod[:, 3], scale=mod[:, 4],
