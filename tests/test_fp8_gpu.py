@@ -148,12 +148,13 @@ def test_gemm_fp8_hipblaslt_route_matches_mfma_kernel(epi, monkeypatch):
 
 
 def test_gemm_fp8_hipblaslt_fused_gelu(monkeypatch):
-    """The default fp8 GELU route: hipBLASLt fp8 with its fused GELU_BIAS epilogue, the GELU-tanh of
+    """The opt-in fp8 GELU route (VS_FP8_BACKEND=lt VS_LT_GELU=1; since r4 the default runs the fp8
+    FFN-up on the MFMA kernel): hipBLASLt fp8 with its fused GELU_BIAS epilogue, the GELU-tanh of
     the fp32 (x8 . w8^T) * scale + bias rounded once.  Against the fp64 GELU of that exact
     pre-activation it is as close as one rounding allows; from fp8_linear's rounding points
     (bf16(GELU(bf16(linear))), VS_LT_GELU=0) it differs by at most twice their own error."""
     K = _k()
-    monkeypatch.delenv("VS_FP8_BACKEND", raising=False)
+    monkeypatch.setenv("VS_FP8_BACKEND", "lt")
     M, N, Kd = 700, 1024, 1536
     g = torch.Generator().manual_seed(9)
     x = torch.randn(M, Kd, generator=g).to(BF16)
