@@ -55,7 +55,7 @@ def test_c5_14b_fp8_block_pair_causvid_lora_832x480x73(backend, monkeypatch):
     assert quantize_fp8_(dit) + quantize_fp8_(vace) == 20
     # the merge vs GeneralLoRALoader's bf16 merge (B scaled by alpha / rank as the kohya layout means
     # it): the rank-32 product's fp32 sums differ in order (MFMA vs torch), so a merged weight may sit
-    # one bf16 ulp away; the e4m3 re-quantisation would turn such an ulp into a rounding flip the
+    # an ulp or two away; the e4m3 re-quantisation would turn such an ulp into a rounding flip the
     # fp32/fp64 floor does not cover, so the oracle then runs on the product's merged weights
     Wm = dict(W)
     sd = dit.state_dict()
@@ -64,8 +64,15 @@ def test_c5_14b_fp8_block_pair_causvid_lora_832x480x73(backend, monkeypatch):
         la, lb = lora[f"blocks.0.{t}.lora_A.weight"], lora[f"blocks.0.{t}.lora_B.weight"]
         ref = O.lora_merge(W[key], lb, la, 1.0).float()
         got = sd[key].float()
-        ulp = torch.exp2(torch.floor(torch.log2(ref.abs().clamp_min(1e-30))) - 7)
-        assert ((got - ref).abs() <= ulp).all(), key
+        # (two roundings, bf16(B@A) then bf16(W + .): up to an ulp of the larger term each -- under
+        # cancellation many ulps of the small sum)
+        mag = torch.maximum(W[key].float().abs(), (lb.float() @ la.float()).abs())
+        ulp = torch.exp2(torch.floor(torch.log2(mag.clamp_min(1e-30))) - 7)
+        bad = (got - ref).abs() > 2 * ulp
+        if bad.any():
+            i = bad.nonzero()[:4].tolist()
+            print(key, int(bad.sum()), "beyond 2 ulps, e.g.", [(r, c, float(got[r, c]), float(ref[r, c])) for r, c in i])
+        assert not bad.any(), key
         assert (got != ref).float().mean().item() < 1e-3, key
         Wm[key] = sd[key].clone()
     lat, ctx, vc = inputs(cfg, 2)
