@@ -6,7 +6,7 @@
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p gpurun_out
-timeout -k 10 750 python -u -m pytest -v -s --timeout 600 --timeout-method thread tests/test_production_c4c5_gpu.py \
+timeout -k 10 750 python -u -m pytest -v -s --timeout 600 --timeout-method thread -m "gpu or gpu_long" tests/test_production_c4c5_gpu.py \
   > gpurun_out/prod_c4c5.log 2>&1
 rc=$?
 grep -E "^(PASSED|FAILED)|passed|failed" gpurun_out/prod_c4c5.log | tail -6

@@ -12,6 +12,8 @@ for p in (ROOT, os.path.join(ROOT, "video-styler_amd")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box via gpurun)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+    config.addinivalue_line("markers", "gpu_long: MI355X test whose oracle takes minutes (C4 block pair, "
+                                       "480x832 VAE): outside the round-end -m gpu tier, run by scripts/r4_parity.sh")
 
 
 def pytest_collection_modifyitems(config, items):
@@ -20,7 +22,7 @@ def pytest_collection_modifyitems(config, items):
         return
     skip = pytest.mark.skip(reason="no GPU in this container")
     for item in items:
-        if "gpu" in item.keywords:
+        if "gpu" in item.keywords or "gpu_long" in item.keywords:
             item.add_marker(skip)
 
 

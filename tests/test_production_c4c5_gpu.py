@@ -20,7 +20,9 @@ from gpu_util import BF16, err
 from oracle import wan_oracle as O
 from test_production_model_gpu import NOISE_X, build, floor_check, gpu_weights, inputs, oracle_both
 
-pytestmark = pytest.mark.gpu
+# C5 runs in the -m gpu tier (about 25 s); C4 (2.5 min: the fp64 oracle at S = 111 600) and the
+# 480x832 VAE (8.5 min: the oracle's fp32 and fp64 convolutions on the host) are gpu_long, run by
+# scripts/r4_parity.sh (logs: profiles/r4/prod_c4c5_run1.log)
 LORA_TARGETS = [f"{a}.{l}" for a in ("self_attn", "cross_attn") for l in "qkvo"] + ["ffn.0", "ffn.2"]
 
 
@@ -39,6 +41,7 @@ def causvid_lora(cfg, rank, alpha, seed):
     return sd
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("backend", ["lt", "vstyler"])
 def test_c5_14b_fp8_block_pair_causvid_lora_832x480x73(backend, monkeypatch):
     from vstyler import model_fn_wan_video
@@ -97,6 +100,7 @@ def test_c5_14b_fp8_block_pair_causvid_lora_832x480x73(backend, monkeypatch):
     assert rl <= NOISE_X * frl + 2e-3 and mx <= NOISE_X * fmx + 2e-2, (mx, rl, fmx, frl)
 
 
+@pytest.mark.gpu_long
 def test_c4_14b_block_pair_1280x720x121():
     from vstyler import model_fn_wan_video
     cfg = dict(O.WAN_CONFIGS["14B"], num_layers=1, vace_layers=(0,))
@@ -114,6 +118,7 @@ def test_c4_14b_block_pair_1280x720x121():
     floor_check(out, ref32, ref64, "C4 14B 1+1 blocks 1280x720x121 CFG2 (223 200 GEMM rows)")
 
 
+@pytest.mark.gpu_long
 def test_vae_tiled_encode_decode_480x832_3x3_tiles():
     from oracle import wan_vae_oracle as V
     from test_vae_gpu import _floor, _model, _within_floor
