@@ -169,6 +169,20 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
         else
             dma16(sc.vdst + (i - 4) * 1024, vvo[i - 4], sc.vr, sc.vs);
     };
+    // phase D's pieces (r4): M0 is written once before the barrier and stepped between the two PV
+    // MFMAs of the previous step, so a piece is the load alone (no s_mov + hazard s_nop per piece;
+    // the step declares no "m0" clobber -- the hazard recognizer would pad it after every MFMA --
+    // and nothing else in this kernel reads M0)
+    auto piece_go = [&](int i) __attribute__((always_inline)) {
+        if (i < 4)
+            asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" :: "v"(kvo[i]), "s"(sc.kr), "s"(sc.ks) : "memory");
+        else
+            asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" :: "v"(vvo[i - 4]), "s"(sc.vr), "s"(sc.vs) : "memory");
+    };
+    auto m0_step = [&](int i) __attribute__((always_inline)) {      // M0: piece i - 1 -> piece i
+        if (i == 4) asm volatile("s_add_u32 m0, m0, %0" :: "i"(W4_TILE - 3 * 1024) : "memory");
+        else asm volatile("s_add_u32 m0, m0, 0x400" ::: "memory");
+    };
     auto stage_next = [&]() __attribute__((always_inline)) {
         if (++li == nkv) {
             li = 0;
@@ -364,6 +378,10 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
             asm volatile("" : "+a"(o[rb][dt]));
         }
     };
+    auto mfV1 = [&](const bf16x8_t& vf, const u32x4_t (&pkv)[2][2], int ksl, int dt, int rb) __attribute__((always_inline)) {
+        o[rb][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, __builtin_bit_cast(bf16x8_t, pkv[rb][ksl]), o[rb][dt], 0, 0, 0);
+        asm volatile("" : "+a"(o[rb][dt]));
+    };
     // softmax of elements e, e+1 of one 16-value S block of row block rb: P pair -> dword
     // (e >> 1) & 3 of k-step (e >> 3) of pkd, the two p into rb's row sum
     auto smp = [&](const f32x16_t& sv, int e, u32x4_t (&pkd)[2], int rb) __attribute__((always_inline)) {
@@ -396,9 +414,11 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
             asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(sv[rb]) : "v"(kf), "a"(qf[rb][j]));
     };
     // B(T+1); the DMA of tile T+3 is issued one piece per step of phase D
-    auto sync = [&](int T) __attribute__((always_inline)) {
+    auto sync = [&](int T, auto first_c) __attribute__((always_inline)) {
         fence();
         stamp(3);
+        if constexpr (!decltype(first_c)::value)     // phase D's first piece destination (piece_go)
+            asm volatile("s_mov_b32 m0, %0" :: "s"(lds0 + ((T + 3) & 3) * W4_SLOT) : "m0");
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
         fence();
         stamp(4);
@@ -464,12 +484,19 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
             smp(s0[1], 2 * i, p0c[1], 1);
             fence();
         }
-        sync(T);
+        sync(T, first_c);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {                                   // D
-            stage_piece(i);
+            if (FIRST) stage_piece(i);
+            else piece_go(i);
             rdK(kf0[i], T + 1, 0, i);
-            if (!FIRST) mfV(vfb[i], p1, i >> 2, i & 3);
+            if (!FIRST) {
+                mfV1(vfb[i], p1, i >> 2, i & 3, 0);
+                fence();
+                if (i < 7) m0_step(i + 1);
+                fence();
+                mfV1(vfb[i], p1, i >> 2, i & 3, 1);
+            }
             fence();
 #ifdef VS_W4_STAMPS
             if (i == 3) stamp(6);
