@@ -718,7 +718,8 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
     const __amdgpu_buffer_rsrc_t rh = HINT ? rsrc(ep.hint, ep.ld_hint, true) : rsrc(C, ldc, false);
     const int vo_r = RESID ? (int)((r * ep.ld_res + n_w + ncol) * 2) : 0;
     const int vo_h = HINT ? (int)((r * ep.ld_hint + n_w + ncol) * 2) : 0;
-    constexpr int DEPTH = W4_EPI_DEPTH;        // rows of residual / hint loads in flight
+    // rows of residual / hint loads in flight (1 for the fp8 hint instantiation: its registers)
+    constexpr int DEPTH = (HINT && SCALED) ? 1 : W4_EPI_DEPTH;
     u32x4_t rs[DEPTH][4], hs[DEPTH][4];
     auto load_rows = [&](auto ic, u32x4_t (&r_)[4], u32x4_t (&h_)[4]) __attribute__((always_inline)) {
         constexpr int i = decltype(ic)::value;
@@ -1469,57 +1470,66 @@ constexpr int F4_LDS = 4 * F4_OPB;            // [A b0][A b1][W b0][W b1] = 1392
 static_assert(4 * F4_ROWB == 0x1100, "the fp8 4w kernel's M0 step");
 __device__ __forceinline__ int f4_swz(int r) { return ((r >> 3) & 1) * 3; }
 
-template <bool WIDE>
+template <bool WIDE, int MODE, bool HINT>      // MODE / HINT: the 16-B epilogue's (WIDE) mode
 __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
     const uint8_t* __restrict__ A, long long lda, const float* __restrict__ scale_a, const uint8_t* __restrict__ W,
     long long ldw, bf16_t* C, long long ldc, int M, int N, int K, Epi ep, int ntm, int ntn, int nmain, int ksplit,
-    int piece_k, float* __restrict__ part) {
+    int piece_k, float* __restrict__ part, int npers, int tiles_per) {
+#if defined(__HIP_DEVICE_COMPILE__)     // (the AGPR asm operands are not host constraints)
     extern __shared__ __attribute__((aligned(16))) char smem[];
-
-    int pid, piece = -1;
-    if ((int)blockIdx.x < nmain) {
-        pid = xcd_remap(blockIdx.x, nmain);
-    } else {
-        const int t = blockIdx.x - nmain;
-        pid = nmain + t / ksplit;
-        piece = t % ksplit;
-    }
-    int tm, tn;
-    tile_of(pid, ntm, ntn, ep.gm, tm, tn);
-    const int m0 = tm * 256, n0 = tn * 256;
-    const int kb = piece < 0 ? 0 : piece * piece_k;
-    const int nt = (piece < 0 ? K : min(K - kb, piece_k)) / 128;
+    // r4: persistent as gemm_bf16_tn_4w (w4_work: one workgroup per CU over its XCD's tile range,
+    // the DMA cursor running across tile boundaries, split pieces after)
+    const W4Work wk = w4_work(K, nmain, ksplit, piece_k, npers, tiles_per, 128);
+    const int nt = wk.nt;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1;
 
     f32x4_t acc[8][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    // the DMAs are inline asm, one instruction each: M0 (the LDS destination) is set at an operand's
-    // first instruction and stepped by 4 rows (4 x 1088 B) one MFMA ahead of the next, so no hazard
-    // nop sits in the MFMA stream (the bf16 kernel's r4 change, see gemm_bf16_tn_4w)
-    auto rsrc4 = [](const uint8_t* base) {
+    // DMA instruction j of wave w: LDS row 4j + w, global row 128 (rho / 16) + 16 (lane / 8) + rho % 16
+    // (rho = 4j + w), 16-B chunk lane % 8 taken from the swizzled source chunk; the row offsets are
+    // tile-invariant (resources rebased on the tile, num_records = its rows' bytes: rows past the
+    // matrix load 0), the K-tile offset goes in soffset.  One instruction per DMA: M0 (the LDS
+    // destination) is set at an operand's first instruction and stepped by 4 rows (4 x 1088 B) one
+    // MFMA ahead of the next (the bf16 kernel's r4 form, see gemm_bf16_tn_4w)
+    auto rsrc4 = [](const uint8_t* base, int bytes) {
         const unsigned long long a = (unsigned long long)(uintptr_t)base;
         return i32x4_t{__builtin_amdgcn_readfirstlane((int)(unsigned)a),
-                       __builtin_amdgcn_readfirstlane((int)((unsigned)(a >> 32) & 0xffffu)), 0x7fffffff, 0x00020000};
+                       __builtin_amdgcn_readfirstlane((int)((unsigned)(a >> 32) & 0xffffu)),
+                       __builtin_amdgcn_readfirstlane(bytes), 0x00020000};
     };
-    const i32x4_t ra = rsrc4(A + (long long)m0 * lda + kb);
-    const i32x4_t rw = rsrc4(W + (long long)n0 * ldw + kb);
-    const int alim = M - 1 - m0, wlim = N - 1 - n0;
     unsigned voa[8], vow[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int rho = 4 * j + wave;
-        const int g = (rho >> 4) * 128 + 16 * (lane >> 3) + (rho & 15);
+        const unsigned g = (unsigned)((rho >> 4) * 128 + 16 * (lane >> 3) + (rho & 15));
         const unsigned ch = 16u * (unsigned)((lane & 7) ^ f4_swz(rho & 15));
-        voa[j] = (unsigned)min(g, alim) * (unsigned)lda + ch;
-        vow[j] = (unsigned)min(g, wlim) * (unsigned)ldw + ch;
+        voa[j] = g * (unsigned)lda + ch;
+        vow[j] = g * (unsigned)ldw + ch;
+        asm volatile("" : "+v"(voa[j]), "+v"(vow[j]));     // kept, not re-formed per use
     }
+    i32x4_t ra, rw;
+    auto dma_tile = [&](int k) {
+        int tm, tn;
+        tile_of(wk.p0 + k * wk.pstep, ntm, ntn, ep.gm, tm, tn);
+        const int m0 = tm * 256, n0 = tn * 256;
+        ra = rsrc4(A + (long long)m0 * lda + wk.kb, (int)((long long)max(0, min(M - m0, 256)) * lda));
+        rw = rsrc4(W + (long long)n0 * ldw + wk.kb, (int)((long long)max(0, min(N - n0, 256)) * ldw));
+    };
+    int dk = 0, dkt = 0;
+    auto dma_advance = [&]() {
+        if (++dkt == nt) {
+            if (dk + 1 < wk.ntw) {
+                ++dk;
+                dkt = 0;
+                dma_tile(dk);
+            } else {
+                dkt = nt - 1;           // past the block's last K-tile: re-read it (unused buffer)
+            }
+        }
+    };
     unsigned dw = 2 * F4_OPB + wave * F4_ROWB, da = wave * F4_ROWB;
     const unsigned dw_tog = dw ^ (dw + F4_OPB), da_tog = da ^ (da + F4_OPB);
     const unsigned lds0 = (unsigned)(uintptr_t)smem;
@@ -1537,8 +1547,6 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
         asm volatile("s_nop 0" ::: "memory");
         dma_go(ko, d);
     };
-    auto dma_w = [&](unsigned ko, int j) { dma_now(ko, j); };
-    auto dma_a = [&](unsigned ko, int j) { dma_now(ko, 8 + j); };
 
     // fragment bases: the two 16-B halves of a lane's 32 B (logical chunks 2c, 2c+1 of row r)
     const int fr = lane & 15, fc = lane >> 4, sw = f4_swz(fr);
@@ -1570,43 +1578,46 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
         asm volatile("s_barrier" ::: "memory");
         fence();
     };
-    const unsigned klast = (unsigned)(nt - 1) * 128u;
-    auto kofs = [&](int t) { return min((unsigned)t * 128u, klast); };
+    // the fragments a K-tile's loop top does not read itself (A 0-3, W 0-6), of the K-tile the
+    // fragment bases point at
+    auto read_early = [&]() {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = frag(a0, a1, 128 * i);
+#pragma unroll
+        for (int j = 0; j < 7; ++j) fw[j] = frag(w0, w1, 128 * j);
+        fence();
+    };
 
-    // prologue: K-tiles 0 and 1 in flight; the fragments of tile 0 but W 7 and A 4-7 (read by the
-    // first iteration's top)
+    // prologue: K-tiles 0 and 1 of the stream in flight, then the early fragments of K-tile 0
+    dma_tile(0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dma_w(0, j);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dma_a(0, j);
+    for (int d = 0; d < 16; ++d) dma_now(0u, d);
+    dma_advance();
     dw ^= dw_tog;
     da ^= da_tog;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dma_w(kofs(1), j);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dma_a(kofs(1), j);
+    for (int d = 0; d < 16; ++d) dma_now((unsigned)dkt * 128u, d);
+    dma_advance();
     dw ^= dw_tog;
     da ^= da_tog;
     fence();
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     bar();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = frag(a0, a1, 128 * i);
-#pragma unroll
-    for (int j = 0; j < 7; ++j) fw[j] = frag(w0, w1, 128 * j);
-    fence();
+    read_early();
 
-#pragma nounroll
-    for (int t = 0; t < nt; ++t) {
-        const unsigned ko = kofs(t + 2);
-        // the previous iteration's fragment reads (compiler-visible) complete here, so the reads of
-        // W 7 and A 4-7 below (inline asm, counted by hand: used from MFMA 7 / 32) stay in flight
+    // one K-tile: top reads of this K-tile (W 7, A 4-7), one barrier (its buffer free for the DMA of
+    // the stream's K-tile two ahead, every 3 MFMAs from q = 11), vmcnt(6) + barrier at q = 29 (the
+    // next K-tile landed), then the next K-tile's early reads into the fragments that died.  FIRST:
+    // the tile's first K-tile, whose MFMAs start the accumulators from 0
+    auto ktile = [&](auto firstc) __attribute__((always_inline)) {
+        constexpr bool FIRST = decltype(firstc)::value;
+        const unsigned ko = (unsigned)dkt * 128u;
         fence();
-        __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0)
+        __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0): the early reads landed
         fence();
         static_for<64>([&](auto qc) __attribute__((always_inline)) {
             constexpr int q = decltype(qc)::value;
-            if constexpr (q == 0) fw[7] = frag_asm(w0, w1, 128 * 7);                // K-tile t, this buffer
+            if constexpr (q == 0) fw[7] = frag_asm(w0, w1, 128 * 7);                // this K-tile, this buffer
             if constexpr (q >= 1 && q <= 4) fa[3 + q] = frag_asm(a0, a1, 128 * (3 + q));
             if constexpr (q == 7) {                  // W 7 landed (the 8 reads of A 4-7 may still fly)
                 fence();
@@ -1623,7 +1634,7 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
                 fence();
             }
             if constexpr (q >= 11 && q <= 56 && (q - 11) % 3 == 0) dma_go(ko, (q - 11) / 3);
-            if constexpr (q == 29) {                                                 // K-tile t+1 landed
+            if constexpr (q == 29) {                                                 // next K-tile landed
                 fence();
                 asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
                 bar();
@@ -1634,42 +1645,64 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
             constexpr int i = q < 32 ? (q >> 3) : 4 + ((q - 32) & 3);
             constexpr int j = q < 32 ? (q & 7) : (q - 32) >> 2;
             if constexpr (q >= 10 && q <= 55 && (q - 10) % 3 == 0) m0_set((q - 10) / 3);   // DMA of MFMA q + 1
-            asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
-                         : "+a"(acc[i][j]) : "v"(fw[j]), "v"(fa[i]), "v"(unit));
+            if constexpr (FIRST)
+                asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, 0, %3, %3 op_sel_hi:[0,0,0]"
+                             : "=a"(acc[i][j]) : "v"(fw[j]), "v"(fa[i]), "v"(unit));
+            else
+                asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
+                             : "+a"(acc[i][j]) : "v"(fw[j]), "v"(fa[i]), "v"(unit));
             fence();
         });
         dw ^= dw_tog;
         da ^= da_tog;
-    }
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+        dma_advance();
+    };
 
-    // acc[i][j][e] = D[n][m]: m = m0 + 128 wm + 16 i + (lane & 15), n = n0 + 128 wn + 16 j + 4 (lane >> 4) + e
-    if (piece >= 0) {
-        float* pp = part + ((long long)(pid - nmain) * ksplit + piece) * 256 * 256;
+#pragma nounroll
+    for (int k = 0; k < wk.ntw; ++k) {
+        ktile(std::true_type{});
+#pragma nounroll
+        for (int t = 1; t < nt; ++t) ktile(std::false_type{});
+        // the accumulators leave through v_accvgpr_read (acc_rd): cover the last MFMAs' write latency
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+        int tm, tn;
+        tile_of(wk.p0 + k * wk.pstep, ntm, ntn, ep.gm, tm, tn);
+        const int m0 = tm * 256, n0 = tn * 256;
+        // acc[i][j][e] = D[n][m]: m = m0 + 128 wm + 16 i + (lane & 15), n = n0 + 128 wn + 16 j + 4 (lane >> 4) + e
+        if (wk.piece >= 0) {
+            const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+                part + ((long long)(wk.p0 - nmain) * ksplit + wk.piece) * 256 * 256, 0, 256 * 256 * 4, 0x00020000);
+            const int vo = ((128 * wm + (lane & 15)) * 256 + 128 * wn + 4 * (lane >> 4)) * 4;
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+            for (int i = 0; i < 8; ++i)
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                *reinterpret_cast<f32x4_t*>(pp + (128 * wm + 16 * i + (lane & 15)) * 256 + 128 * wn + 16 * j +
-                                            4 * (lane >> 4)) = acc[i][j];
-        return;
-    }
-    if constexpr (WIDE) {
-        tile_epilogue_w4_dispatch<true>(acc, m0 + 128 * wm, n0 + 128 * wn, lane, C, ldc, M, N, ep, scale_a);
-        return;
-    }
+                for (int j = 0; j < 8; ++j)
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        u32x4_t{__float_as_uint(acc_rd(acc[i][j][0])), __float_as_uint(acc_rd(acc[i][j][1])),
+                                __float_as_uint(acc_rd(acc[i][j][2])), __float_as_uint(acc_rd(acc[i][j][3]))},
+                        rp, vo, 16 * i * 256 * 4 + 64 * j, 0);
+        } else if constexpr (WIDE) {
+            tile_epilogue_w4<MODE, HINT, true>(acc, m0 + 128 * wm, n0 + 128 * wn, lane, C, ldc, M, N, ep, scale_a);
+        } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int m = m0 + 128 * wm + 16 * i + (lane & 15);
-        if (m >= M) continue;
-        const float sa = scale_a[m];
+            for (int i = 0; i < 8; ++i) {
+                const int m = m0 + 128 * wm + 16 * i + (lane & 15);
+                const float sa = scale_a[min(m, M - 1)];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int n = n0 + 128 * wn + 16 * j + 4 * (lane >> 4);
-            if (n >= N) continue;
-            epilogue_store(acc[i][j] * sa, m, n, C, ldc, ep);
+                for (int j = 0; j < 8; ++j) {
+                    const int n = n0 + 128 * wn + 16 * j + 4 * (lane >> 4);
+                    // (plain reads: the 8-B path, for N % 8 != 0 only, leaves the copies to the
+                    // compiler -- through acc_rd its AGPR round trips came back stale)
+                    if (m < M && n < N) epilogue_store(acc[i][j] * sa, m, n, C, ldc, ep);
+                }
+            }
         }
+        // the epilogue's loads and stores leave the counted DMA waits of the next tile exact; then
+        // the next tile's early fragments (its first K-tile has landed: the last K-tile's q = 29 wait)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (k + 1 < wk.ntw) read_early();
     }
+#endif
 }
 
 
@@ -2040,20 +2073,32 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
     }
     const char* fk = getenv("VS_GEMM_KERNEL");      // the 4-wave kernel unless VS_GEMM_KERNEL=8p
     if (!(fk && fk[0] == '8')) {
+        using KF4 = void (*)(const uint8_t*, long long, const float*, const uint8_t*, long long, bf16_t*, long long,
+                             int, int, int, Epi, int, int, int, int, int, float*, int, int);
+        // one instantiation per 16-B epilogue mode (index: mode, 5 = gate-residual + hint), 6: 8-B path
+        const KF4 kf4[7] = {gemm_fp8_tn_4w<true, VS_EPI_BIAS, false>, gemm_fp8_tn_4w<true, VS_EPI_GELU, false>,
+                            gemm_fp8_tn_4w<true, VS_EPI_SILU, false>, gemm_fp8_tn_4w<true, VS_EPI_GATE_RES, false>,
+                            gemm_fp8_tn_4w<true, VS_EPI_RES, false>, gemm_fp8_tn_4w<true, VS_EPI_GATE_RES, true>,
+                            gemm_fp8_tn_4w<false, VS_EPI_BIAS, false>};
         static bool attr4 = false;
         if (!attr4) {
-            for (const void* f : {(const void*)gemm_fp8_tn_4w<false>, (const void*)gemm_fp8_tn_4w<true>})
-                (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, F4_LDS);
+            for (const KF4 f : kf4)
+                (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, F4_LDS);
             attr4 = true;
         }
         const bool wide = n % 8 == 0 && ldc % 8 == 0 && aligned16(c) && (!ep.bias || aligned16(ep.bias)) &&
                           (!ep.res || (ep.ld_res % 8 == 0 && aligned16(ep.res))) &&
                           (!ep.gate || (ep.gate_bstride % 8 == 0 && aligned16(ep.gate))) &&
                           (!ep.hint || (ep.ld_hint % 8 == 0 && aligned16(ep.hint)));
-        hipLaunchKernelGGL(wide ? gemm_fp8_tn_4w<true> : gemm_fp8_tn_4w<false>,
-                           dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(256), F4_LDS, (hipStream_t)stream,
-                           (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c, ldc, m, n, k, ep, tm,
-                           tn, sp.nmain, sp.ksplit, sp.piece_k, part);
+        // persistent blocks (one per CU) over the first floor(nmain / CUs) * CUs tiles, as the bf16 kernel
+        const int cus = vs_cus_for_split(nullptr);
+        const int npers = (cus >= 8 && cus % 8 == 0 && sp.nmain >= cus && !getenv("VS_GEMM_NO_PERSIST")) ? cus : 0;
+        const int tiles_per = npers ? sp.nmain / npers : 0;
+        const unsigned grid = (unsigned)(npers + (sp.nmain - npers * tiles_per) + sp.ntail * sp.ksplit);
+        const KF4 kf = kf4[!wide ? 6 : (ep.mode == VS_EPI_GATE_RES && ep.hint) ? 5 : ep.mode];
+        hipLaunchKernelGGL(kf, dim3(grid), dim3(256), F4_LDS,
+                           (hipStream_t)stream, (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c,
+                           ldc, m, n, k, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part, npers, tiles_per);
     } else
     hipLaunchKernelGGL(gemm_fp8_tn_8p, dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(512), LDS8,
                        (hipStream_t)stream, (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c,
