@@ -9,9 +9,16 @@ import torch
 from vstyler import kernels as K
 
 
+# AB_FLUSH=1: overwrite a 1 GiB buffer before each timed launch (evicts L2 and the 256-MB Infinity
+# Cache, as the step's other kernels do between one weight's uses), to price a kernel's cache reuse
+FLUSH = torch.empty(1 << 29, dtype=torch.float16, device="cuda") if os.environ.get("AB_FLUSH") == "1" else None
+
+
 def timed(fn, reps=3):
     ts = []
     for _ in range(reps):
+        if FLUSH is not None:
+            FLUSH.fill_(1.0)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(); fn(); e1.record(); torch.cuda.synchronize(); ts.append(e0.elapsed_time(e1))
     return min(ts)
