@@ -182,3 +182,51 @@ def test_gemm_fp8_8p_split_tail_and_epilogue(kern, monkeypatch):
         outs.append(xo.cpu())
     monkeypatch.delenv("VS_GEMM_NO_SPLIT", raising=False)
     assert torch.equal(outs[0], ref) and torch.equal(outs[1], ref)
+
+
+def test_gemm_persistent_ragged_exact(K, monkeypatch):
+    """The persistent walk with ragged edges: 17 x 17 = 289 tiles of a 4100 x 4104 output (rows and
+    columns past the matrix in the last tile row / column, dropped by the buffer range checks), 256
+    persistent workgroups + the rest as whole tiles or split pieces; every epilogue mode bit-exact
+    vs the oracle (the 8-phase kernel runs the same shapes under its own parametrisation)."""
+    M, N, Kd, S = 4100, 4104, 1024, 2050
+    g = torch.Generator(device="cuda").manual_seed(41)
+    a, w, b = ints(M, Kd, g=g), ints(N, Kd, g=g), ints(N, g=g, lo=-8, hi=9)
+    y = (a.float() @ w.float().t() + b.float()).to(BF16)
+    out = torch.full((M, N), 7.0, dtype=BF16, device="cuda")
+    K.gemm(a, w, out, bias=b)
+    assert torch.equal(out, y)
+    res = torch.randn(M, N, generator=torch.Generator().manual_seed(42)).to(BF16)
+    gate = (0.25 * torch.randn(2, N, generator=torch.Generator().manual_seed(43))).to(BF16)
+    hint = torch.randn(M, N, generator=torch.Generator().manual_seed(44)).to(BF16)
+    x = res.cuda()
+    K.gemm(a, w, x, epilogue=K.VS_EPI_GATE_RES, bias=b, residual=x, gate=gate.cuda(), gate_bstride=N,
+           rows_per_batch=S, hint=hint.cuda(), hint_scale=0.5)
+    yc = y.cpu()
+    ref = torch.cat([O.gate_residual(res[:S], gate[0], yc[:S]), O.gate_residual(res[S:], gate[1], yc[S:])])
+    assert torch.equal(x.cpu(), O.add(ref, O.bf(hint.float() * 0.5)))
+    x = res.cuda()
+    K.gemm(a, w, x, epilogue=K.VS_EPI_RES, bias=b, residual=x, alpha=0.125)
+    assert torch.equal(x.cpu(), O.add(res, O.bf(0.125 * yc.float())))
+
+
+@pytest.mark.parametrize("kern", ["8p", "4w"])
+def test_gemm_fp8_persistent_ragged_exact(kern, monkeypatch):
+    """The fp8 kernels' persistent walk with ragged edges (289 tiles of 4100 x 4104): integer
+    operands exact in e4m3 reproduce oracle.fp8_linear bit for bit."""
+    from vstyler import kernels as K
+    monkeypatch.setenv("VS_FP8_BACKEND", "vstyler")
+    monkeypatch.setenv("VS_GEMM_KERNEL", kern)
+    M, N, Kd = 4100, 4104, 1024
+    g = torch.Generator().manual_seed(45)
+    x = torch.randint(-4, 5, (M, Kd), generator=g).to(BF16)
+    x[::7] *= 512
+    w = torch.randint(-3, 4, (N, Kd), generator=g).to(BF16)
+    b = torch.randint(-8, 9, (N,), generator=g).to(BF16)
+    ref = O.fp8_linear(x, w, b)
+    x8 = torch.empty(M, Kd, dtype=torch.uint8, device="cuda")
+    sc = torch.empty(M, dtype=torch.float32, device="cuda")
+    K.quant_fp8_rows(x.cuda(), x8, sc)
+    out = torch.empty(M, N, dtype=BF16, device="cuda")
+    K.gemm_fp8(x8, sc, w.to(torch.float8_e4m3fn).view(torch.uint8).cuda(), out, bias=b.cuda())
+    assert torch.equal(out.cpu(), ref)
