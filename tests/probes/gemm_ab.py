@@ -40,7 +40,12 @@ for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
             kw.update(residual=x, gate=gate, gate_bstride=N, rows_per_batch=(M + 1) // 2)
         out = x if epi == K.VS_EPI_GATE_RES else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 
-        def setv(v):       # <kernel>[_d<N>][_g<G>]: N = VS_GEMM_DESYNC (diagnostic), G = VS_GEMM_GM
+        def setv(v):       # <kernel>[_d<N>][_g<G>][_r<R>]: VS_GEMM_DESYNC (diagnostic), VS_GEMM_GM, VS_GEMM_ROUNDS
+            v, _, rr = v.partition("_r")
+            if rr:
+                os.environ["VS_GEMM_ROUNDS"] = rr
+            else:
+                os.environ.pop("VS_GEMM_ROUNDS", None)
             v, _, gm = v.partition("_g")
             base, _, ds = v.partition("_d")
             os.environ["VS_GEMM_BACKEND"] = "lt" if base == "lt" else "vstyler"
@@ -61,5 +66,5 @@ for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
         s = "  ".join(f"{v} {min(t[v]):.3f} ms ({fl / min(t[v]) / 1e9:.0f} TF/s)" for v in VARIANTS)
         print(f"M={M} {name:8s} N={N} K={Kd}: {s}", flush=True)
         del a, w, b, gate, x, out
-for k in ("VS_GEMM_BACKEND", "VSTYLER_GEMM_TILE", "VS_GEMM_KERNEL", "VS_GEMM_DESYNC", "VS_GEMM_GM"):
+for k in ("VS_GEMM_BACKEND", "VSTYLER_GEMM_TILE", "VS_GEMM_KERNEL", "VS_GEMM_DESYNC", "VS_GEMM_GM", "VS_GEMM_ROUNDS"):
     os.environ.pop(k, None)

@@ -44,6 +44,7 @@ struct Epi {
     int mode;
     int desync;       // diagnostic (VS_GEMM_DESYNC): the first round's blocks sleep (b % 256) / 256 x this many ~4 us units
     int gm;           // M-tiles per raster group of the 256x256 tile order (VS_GEMM_GM, default VS_GEMM_GM)
+    int rounds;       // persistent rounds of the 4-wave kernels (set per launch by the host, see w4_work)
 };
 
 // staggered start of the first round of blocks (diagnostic: do tile epilogues that coincide on
@@ -913,23 +914,32 @@ struct W4Work {
     int kb, nt;       // K offset (elements) and K-tiles per tile
     int p0, pstep;    // tile ids: p0 + k * pstep (persistent), or p0
 };
-__device__ __forceinline__ W4Work w4_work(int K, int nmain, int ksplit, int piece_k, int npers, int tiles_per, int kstep) {
+// rounds (Epi::rounds, VS_GEMM_ROUNDS): the persistent range split into `rounds` successive grids of
+// npers workgroups, each walking L = ceil(tiles_per / rounds) tiles of its XCD's range, round r the
+// r-th L-tile slab -- shorter lists drift less (the CUs of an XCD share their 4x8 block's A / W
+// slices in L2 only while K-aligned); the host passes rounds <= tiles_per with no empty round
+__device__ __forceinline__ W4Work w4_work(int K, int nmain, int ksplit, int piece_k, int npers, int tiles_per, int kstep,
+                                          int rounds) {
     W4Work w;
     const int b = blockIdx.x;
     w.piece = -1;
     w.kb = 0;
     w.nt = K / kstep;
-    if (b < npers) {
+    const int npr = npers * rounds;
+    if (b < npr) {
         const int g8 = npers >> 3;
-        w.ntw = tiles_per;
-        w.p0 = (b & 7) * (g8 * tiles_per) + (b >> 3);
+        const int r = b / npers, bb = b - r * npers;
+        const int L = (tiles_per + rounds - 1) / rounds;
+        const int k0 = r * L;
+        w.ntw = max(0, min(L, tiles_per - k0));
+        w.p0 = (bb & 7) * (g8 * tiles_per) + k0 * g8 + (bb >> 3);
         w.pstep = g8;
-    } else if (b < npers + (nmain - npers * tiles_per)) {
+    } else if (b < npr + (nmain - npers * tiles_per)) {
         w.ntw = 1;
-        w.p0 = npers * tiles_per + (b - npers);
+        w.p0 = npers * tiles_per + (b - npr);
         w.pstep = 0;
     } else {
-        const int t = b - npers - (nmain - npers * tiles_per);
+        const int t = b - npr - (nmain - npers * tiles_per);
         w.ntw = 1;
         w.p0 = nmain + t / ksplit;
         w.pstep = 0;
@@ -959,7 +969,8 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     int piece_k, float* __restrict__ part, int npers, int tiles_per) {
 #if defined(__HIP_DEVICE_COMPILE__)     // (the AGPR asm operands are not host constraints)
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const W4Work wk = w4_work(K, nmain, ksplit, piece_k, npers, tiles_per, 64);
+    const W4Work wk = w4_work(K, nmain, ksplit, piece_k, npers, tiles_per, 64, ep.rounds);
+    if (wk.ntw <= 0) return;            // (an empty round: nothing issued yet)
     const int nt = wk.nt;
     desync_start(ep);
 
@@ -1479,7 +1490,8 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // r4: persistent as gemm_bf16_tn_4w (w4_work: one workgroup per CU over its XCD's tile range,
     // the DMA cursor running across tile boundaries, split pieces after)
-    const W4Work wk = w4_work(K, nmain, ksplit, piece_k, npers, tiles_per, 128);
+    const W4Work wk = w4_work(K, nmain, ksplit, piece_k, npers, tiles_per, 128, ep.rounds);
+    if (wk.ntw <= 0) return;            // (an empty round: nothing issued yet)
     const int nt = wk.nt;
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1881,6 +1893,17 @@ static bool use_4w() {
     return !(e && e[0] == '8');
 }
 
+// persistent rounds of the 4-wave kernels (w4_work): VS_GEMM_ROUNDS (default 1), at most one per
+// tile of a workgroup's list and no empty round
+static int w4_rounds(int tiles_per) {
+    if (tiles_per <= 1) return 1;
+    const char* e = getenv("VS_GEMM_ROUNDS");
+    const int want = e && atoi(e) > 0 ? atoi(e) : 1;
+    const int r = min(want, tiles_per);
+    const int L = (tiles_per + r - 1) / r;
+    return (tiles_per + L - 1) / L;
+}
+
 static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n) {
     if (epilogue < VS_EPI_BIAS || epilogue > VS_EPI_RES) return VS_E_INVALID;
     ep = Epi{};
@@ -1892,6 +1915,7 @@ static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n)
     ep.desync = ds ? atoi(ds) : 0;
     const char* gm = getenv("VS_GEMM_GM");
     ep.gm = gm && atoi(gm) > 0 ? atoi(gm) : VS_GEMM_GM;
+    ep.rounds = 1;
     if (epi) {
         ep.bias = (const bf16_t*)epi->bias;
         ep.res = (const bf16_t*)epi->residual;
@@ -1988,7 +2012,8 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
             const int cus = vs_cus_for_split(nullptr);
             const int npers = (cus >= 8 && cus % 8 == 0 && sp.nmain >= cus && !getenv("VS_GEMM_NO_PERSIST")) ? cus : 0;
             const int tiles_per = npers ? sp.nmain / npers : 0;
-            const unsigned grid = (unsigned)(npers + (sp.nmain - npers * tiles_per) + sp.ntail * sp.ksplit);
+            ep.rounds = w4_rounds(tiles_per);
+            const unsigned grid = (unsigned)(npers * ep.rounds + (sp.nmain - npers * tiles_per) + sp.ntail * sp.ksplit);
             hipLaunchKernelGGL(kf, dim3(grid), dim3(256), W4_LDS,
                                (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw, (bf16_t*)c, ldc, m,
                                n, k, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part, npers, tiles_per);
@@ -2094,7 +2119,8 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
         const int cus = vs_cus_for_split(nullptr);
         const int npers = (cus >= 8 && cus % 8 == 0 && sp.nmain >= cus && !getenv("VS_GEMM_NO_PERSIST")) ? cus : 0;
         const int tiles_per = npers ? sp.nmain / npers : 0;
-        const unsigned grid = (unsigned)(npers + (sp.nmain - npers * tiles_per) + sp.ntail * sp.ksplit);
+        ep.rounds = w4_rounds(tiles_per);
+        const unsigned grid = (unsigned)(npers * ep.rounds + (sp.nmain - npers * tiles_per) + sp.ntail * sp.ksplit);
         const KF4 kf = kf4[!wide ? 6 : (ep.mode == VS_EPI_GATE_RES && ep.hint) ? 5 : ep.mode];
         hipLaunchKernelGGL(kf, dim3(grid), dim3(256), F4_LDS,
                            (hipStream_t)stream, (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c,
