@@ -25,7 +25,9 @@ def timed(fn, reps=3):
 
 
 SHAPES = (("qkv", 15360, 5120, K.VS_EPI_BIAS), ("o-proj", 5120, 5120, K.VS_EPI_GATE_RES),
-          ("ffn-up", 13824, 5120, K.VS_EPI_GELU), ("ffn-down", 5120, 13824, K.VS_EPI_GATE_RES))
+          ("ffn-up", 13824, 5120, K.VS_EPI_GELU), ("ffn-down", 5120, 13824, K.VS_EPI_GATE_RES),
+          ("cross-o", 5120, 5120, K.VS_EPI_RES))
+SHAPES = tuple(sh for sh in SHAPES if sh[0] in os.environ.get("AB_SHAPES", ",".join(x[0] for x in SHAPES)).split(","))
 VARIANTS = [v for v in os.environ.get("AB_VARIANTS", "vstyler,lt").split(",")]
 for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
     for name, N, Kd, epi in SHAPES:
@@ -38,7 +40,9 @@ for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
         kw = dict(epilogue=epi, bias=b)
         if epi == K.VS_EPI_GATE_RES:
             kw.update(residual=x, gate=gate, gate_bstride=N, rows_per_batch=(M + 1) // 2)
-        out = x if epi == K.VS_EPI_GATE_RES else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        if epi == K.VS_EPI_RES:
+            kw.update(residual=x)
+        out = x if epi in (K.VS_EPI_GATE_RES, K.VS_EPI_RES) else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 
         def setv(v):       # <kernel>[_d<N>][_g<G>][_r<R>]: VS_GEMM_DESYNC (diagnostic), VS_GEMM_GM, VS_GEMM_ROUNDS
             v, _, rr = v.partition("_r")

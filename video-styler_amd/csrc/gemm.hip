@@ -665,6 +665,18 @@ __device__ __forceinline__ int vadd_opq(int v, int s) {
     return r;
 }
 
+// the store's pack, one v_cvt_pk_bf16_f32 per output pair (RNE, = pack2): from the C expression the
+// compiler formed the pairs of its packed arithmetic, packed those and re-shuffled the halves
+__device__ __forceinline__ uint32_t pk_store(float lo, float hi) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((float __attribute__((ext_vector_type(2)))){lo, hi}, bf16x2_t));
+}
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2_t unpk2(uint32_t w) {
+    return f32x2_t{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+// a bf16 rounding point of a pair (= rbf of each)
+__device__ __forceinline__ f32x2_t rbf2(f32x2_t v) { return unpk2(pk_store(v.x, v.y)); }
+
 // one accumulator element AGPR -> VGPR at its point of use: left to the compiler, the copies of
 // all 256 accumulators were made at the K loop's exit (the class change from the MFMA asm's "a"
 // operands) and the overflow spilled to scratch
@@ -699,9 +711,11 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
     };
     const __amdgpu_buffer_rsrc_t rc = rsrc(C, ldc, true);
     const int vo_c = (int)((r * ldc + n_w + ncol) * 2);
-    u32x4_t bw[4];
+    // bias unpacked once per tile (the per-row unpack was 8 of the ~95 VALU per 16-B store)
+    float bvf[4][8];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) bw[p] = ep.bias ? ld16(ep.bias + min(nl + 32 * p, N - 8)) : u32x4_t{0, 0, 0, 0};
+    for (int p = 0; p < 4; ++p)
+        unpack8(ep.bias ? ld16(ep.bias + min(nl + 32 * p, N - 8)) : u32x4_t{0, 0, 0, 0}, bvf[p]);
     u32x4_t gw0[4], gw1[4];
     int b_lo = 0;
     if constexpr (MODE == VS_EPI_GATE_RES) {
@@ -743,7 +757,7 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
         if constexpr (SCALED) sa = scale_a[min(m, M - 1)];
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            float y[8], bv[8];
+            float y[8];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const float x = acc_rd(acc[i][2 * p][e]), z = acc_rd(acc[i][2 * p + 1][e]);
@@ -751,41 +765,51 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
                 y[e] = __uint_as_float(sw[0]);
                 y[4 + e] = __uint_as_float(sw[1]);
             }
-            unpack8(bw[p], bv);
+            // pair arithmetic (output pair j = y[2j], y[2j+1] = word j of the 16-B store): packed
+            // f32 adds / muls, every bf16 rounding point one v_cvt_pk_bf16_f32 of a pair plus its
+            // unpack (rbf2); a value rounded only for the store is left to the store's pack (RNE is
+            // idempotent: pack2(rbf(v)) == pack2(v) bit for bit) -- the plain-bias output and the
+            // un-hinted gate-residual sum.  Same operations and rounding points as epilogue_store_w.
+            f32x2_t y2[4];
+            uint32_t wo[4];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) y[e] = rbf((SCALED ? y[e] * sa : y[e]) + bv[e]);
-            if constexpr (MODE == VS_EPI_GELU) {
+            for (int j = 0; j < 4; ++j) {
+                f32x2_t v = f32x2_t{y[2 * j], y[2 * j + 1]};
+                if constexpr (SCALED) v = v * sa;
+                v = v + f32x2_t{bvf[p][2 * j], bvf[p][2 * j + 1]};
+                y2[j] = v;
+            }
+            if constexpr (MODE == VS_EPI_GELU || MODE == VS_EPI_SILU) {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) y[e] = gelu_tanh_f(y[e]);
-            } else if constexpr (MODE == VS_EPI_SILU) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) y[e] = silu_f(y[e]);
+                for (int j = 0; j < 4; ++j) {
+                    const f32x2_t v = rbf2(y2[j]);
+                    wo[j] = MODE == VS_EPI_GELU ? pk_store(gelu_tanh_f(v.x), gelu_tanh_f(v.y))
+                                                : pk_store(silu_f(v.x), silu_f(v.y));
+                }
             } else if constexpr (MODE == VS_EPI_GATE_RES) {
-                float rv[8], gv[8];
-                unpack8(rs[i % DEPTH][p], rv);
                 const bool hi = m / ep.rows_per_batch != b_lo;
                 const u32x4_t gsel = hi ? gw1[p] : gw0[p];
-                unpack8(gsel, gv);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) y[e] = rbf(rv[e] + rbf(gv[e] * y[e]));
-                if constexpr (HINT) {
-                    float hv[8];
-                    unpack8(hs[i % DEPTH][p], hv);
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) y[e] = y[e] + rbf(hv[e] * ep.hint_scale);
+                for (int j = 0; j < 4; ++j) {
+                    f32x2_t v = unpk2(rs[i % DEPTH][p][j]) + rbf2(unpk2(gsel[j]) * rbf2(y2[j]));
+                    if constexpr (HINT) v = rbf2(v) + rbf2(unpk2(hs[i % DEPTH][p][j]) * ep.hint_scale);
+                    wo[j] = pk_store(v.x, v.y);
                 }
             } else if constexpr (MODE == VS_EPI_RES) {
-                float rv[8];
-                unpack8(rs[i % DEPTH][p], rv);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) y[e] = rv[e] + rbf(ep.alpha * y[e]);
+                for (int j = 0; j < 4; ++j) {
+                    const f32x2_t v = unpk2(rs[i % DEPTH][p][j]) + rbf2(ep.alpha * rbf2(y2[j]));
+                    wo[j] = pk_store(v.x, v.y);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) wo[j] = pk_store(y2[j].x, y2[j].y);
             }
             // rows past M fall outside rc's range, columns past N get an offset outside it: the
             // hardware drops those stores (no per-store branch)
             const int so = vadd_opq(vo_c, (int)(16 * i * ldc * 2)) + 64 * p;
             __builtin_amdgcn_raw_buffer_store_b128(
-                u32x4_t{pack2(y[0], y[1]), pack2(y[2], y[3]), pack2(y[4], y[5]), pack2(y[6], y[7])}, rc,
-                nl + 32 * p < N ? so : 0x7ffffff0, 0, 0);
+                u32x4_t{wo[0], wo[1], wo[2], wo[3]}, rc, nl + 32 * p < N ? so : 0x7ffffff0, 0, 0);
             // one column block at a time: the scheduler would otherwise hoist the accumulator reads
             // of later blocks (AGPR -> VGPR copies) and run out of VGPRs
             __builtin_amdgcn_sched_barrier(0);
