@@ -646,6 +646,9 @@ __device__ __forceinline__ void static_for(F&& f) {
 #ifndef W4_EPI_DEPTH
 #define W4_EPI_DEPTH 2
 #endif
+#ifndef W4_EPI_DEPTH_BF16       // the bf16 un-hinted residual modes (registers for deeper prefetch)
+#define W4_EPI_DEPTH_BF16 2
+#endif
 __device__ __forceinline__ u32x4_t ld16(const bf16_t* p) { return *reinterpret_cast<const u32x4_t*>(p); }
 __device__ __forceinline__ void unpack8(const u32x4_t& w, float* v) {
 #pragma unroll
@@ -729,12 +732,16 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
         }
     }
     // (resources of absent operands point at C with an empty range: never read)
+#if defined(W4_DIAG) && (W4_DIAG & 2)   // diagnostic build: residual loads answered by the range check
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(C, 0, 0, 0x00020000);
+#else
     const __amdgpu_buffer_rsrc_t rr = RESID ? rsrc(ep.res, ep.ld_res, true) : rsrc(C, ldc, false);
+#endif
     const __amdgpu_buffer_rsrc_t rh = HINT ? rsrc(ep.hint, ep.ld_hint, true) : rsrc(C, ldc, false);
     const int vo_r = RESID ? (int)((r * ep.ld_res + n_w + ncol) * 2) : 0;
     const int vo_h = HINT ? (int)((r * ep.ld_hint + n_w + ncol) * 2) : 0;
     // rows of residual / hint loads in flight (1 for the fp8 hint instantiation: its registers)
-    constexpr int DEPTH = (HINT && SCALED) ? 1 : W4_EPI_DEPTH;
+    constexpr int DEPTH = (HINT && SCALED) ? 1 : (HINT || SCALED) ? W4_EPI_DEPTH : W4_EPI_DEPTH_BF16;
     u32x4_t rs[DEPTH][4], hs[DEPTH][4];
     auto load_rows = [&](auto ic, u32x4_t (&r_)[4], u32x4_t (&h_)[4]) __attribute__((always_inline)) {
         constexpr int i = decltype(ic)::value;
@@ -809,7 +816,13 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
             // hardware drops those stores (no per-store branch)
             const int so = vadd_opq(vo_c, (int)(16 * i * ldc * 2)) + 64 * p;
             __builtin_amdgcn_raw_buffer_store_b128(
-                u32x4_t{wo[0], wo[1], wo[2], wo[3]}, rc, nl + 32 * p < N ? so : 0x7ffffff0, 0, 0);
+                u32x4_t{wo[0], wo[1], wo[2], wo[3]}, rc,
+#if defined(W4_DIAG) && (W4_DIAG & 1)   // diagnostic build: every store dropped by the range check
+                0x7ffffff0,
+#else
+                nl + 32 * p < N ? so : 0x7ffffff0,
+#endif
+                0, 0);
             // one column block at a time: the scheduler would otherwise hoist the accumulator reads
             // of later blocks (AGPR -> VGPR copies) and run out of VGPRs
             __builtin_amdgcn_sched_barrier(0);
@@ -839,7 +852,11 @@ __device__ __forceinline__ void tile_epilogue_w4n(const AccT& acc, int m_w, int 
     };
     const __amdgpu_buffer_rsrc_t rc = rsrc(C, ldc, false);
     const int vo_c = (int)((r * ldc + n_w + ncol) * 2);
+#if defined(W4_DIAG) && (W4_DIAG & 2)   // diagnostic build: residual loads answered by the range check
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(C, 0, 0, 0x00020000);
+#else
     const __amdgpu_buffer_rsrc_t rr = RESID ? rsrc(ep.res, ep.ld_res, true) : rsrc(C, ldc, false);
+#endif
     const __amdgpu_buffer_rsrc_t rh = HINT ? rsrc(ep.hint, ep.ld_hint, true) : rsrc(C, ldc, false);
     const int vo_r = RESID ? (int)((r * ep.ld_res + n_w + ncol) * 2) : 0;
     const int vo_h = HINT ? (int)((r * ep.ld_hint + n_w + ncol) * 2) : 0;
@@ -1124,6 +1141,15 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
         fence();
     };
 
+    // The counted waits of a tile's first K-tile after an epilogue.  VMEM operations complete in
+    // issue order (loads, stores and LDS-DMA alike), and the epilogue's >= EPI_OPS loads / stores
+    // were issued after the 16 DMAs it waits on, so while any of those is pending at least EPI_OPS
+    // more are: the wait counts grow by EPI_OPS (capped at the counter's 63) and the epilogue's
+    // stores drain under the next tile's first K-tile instead of before it (r3-r4: a vmcnt(0)
+    // after every epilogue; dropping every store in a diagnostic build was worth +3.8 %, 
+    // gemm_epidiag_ab.log).  EPI_OPS = the fewest VMEM operations any epilogue path of this
+    // instantiation issues: 32 16-B stores, + 32 residual loads (the split-K piece path: 64 stores).
+    constexpr int EPI_OPS = (MODE == VS_EPI_GATE_RES || MODE == VS_EPI_RES) ? 64 : 32;
     // prologue: K-tiles 0 and 1 of the stream in flight (W then A each), then the k-step-0 fragments
     dma_tile(0);
     ktile_rsrc(0);
@@ -1142,6 +1168,15 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     bar();
     read_k0();
+    // the first tile's first K-tile counts EPI_OPS operations behind K-tile 1's DMAs as every later
+    // tile's does: as many stores the buffer range check drops (offset past num_records 0)
+    {
+        const i32x4_t rz = rsrc4((const char*)C, 0);
+        const int vz = 0;
+#pragma unroll
+        for (int d = 0; d < EPI_OPS; ++d)
+            asm volatile("buffer_store_dword %0, %0, %1, 0 offen" :: "v"(vz), "s"(rz) : "memory");
+    }
 
     // one K-tile: 128 MFMAs with, before MFMA q, the reads / DMA / barriers of this table.  FIRST:
     // the tile's first K-tile, whose k-step-0 MFMAs start the accumulators from 0 (no zeroing pass,
@@ -1149,6 +1184,8 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     // and spilled the 256 accumulators around the epilogue)
     auto ktile = [&](auto firstc) __attribute__((always_inline)) {
             constexpr bool FIRST = decltype(firstc)::value;
+            constexpr int W69 = FIRST ? (18 + EPI_OPS < 63 ? 18 + EPI_OPS : 63) : 18;
+            constexpr int W101 = FIRST ? (15 + EPI_OPS < 63 ? 15 + EPI_OPS : 63) : 15;
             ktile_rsrc((unsigned)dkt * 128u);
             static_for<128>([&](auto qc) __attribute__((always_inline)) {
                 constexpr int q = decltype(qc)::value;
@@ -1161,13 +1198,13 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
                 if constexpr (q == 52) wait_lgkm_bar();                        // A region of this buffer free
                 if constexpr (q == 69) {                                       // W of the next K-tile landed
                     fence();
-                    asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+                    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(W69) : "memory");
                     bar();
                 }
                 if constexpr (q >= 70 && q <= 84 && !(q & 1)) fw0[(q - 70) / 2] = frag(wbase + 128 * ((q - 70) / 2));
                 if constexpr (q == 101) {                                      // A of the next K-tile landed
                     fence();
-                    asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+                    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(W101) : "memory");
                     bar();
                 }
                 if constexpr (q >= 102 && q <= 116 && !(q & 1)) fa0[(q - 102) / 2] = frag(abase + 128 * ((q - 102) / 2));
@@ -1247,9 +1284,11 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
             tile_epilogue_w4<MODE, HINT, false>(acc, m0 + 128 * wm, n0 + 128 * wn, lane, C, ldc, M, N, ep, nullptr);
         }
 #endif
-        // the epilogue's loads and stores leave the counted DMA waits of the next tile exact
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (k + 1 < wk.ntw) read_k0();      // the next tile's k-step-0 fragments (its first K-tile has landed)
+        // the next tile's k-step-0 fragments (its first K-tile has landed); the epilogue's stores stay
+        // in flight (EPI_OPS above) -- after the last tile everything drains, the re-read DMAs into
+        // LDS included, before the workgroup's LDS is released
+        if (k + 1 < wk.ntw) read_k0();
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 #endif
 }
