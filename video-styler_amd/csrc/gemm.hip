@@ -646,6 +646,14 @@ __device__ __forceinline__ void static_for(F&& f) {
 #ifndef W4_EPI_DEPTH
 #define W4_EPI_DEPTH 2
 #endif
+// cache policy of the tile epilogue's output stores / residual loads (A/B knobs; gfx950 CPol bits:
+// 1 sc0, 2 nt, 16 sc1)
+#ifndef W4_OUT_CPOL
+#define W4_OUT_CPOL 2
+#endif
+#ifndef W4_RES_CPOL
+#define W4_RES_CPOL 0
+#endif
 #ifndef W4_EPI_DEPTH_BF16       // the bf16 un-hinted residual modes (registers for deeper prefetch)
 #define W4_EPI_DEPTH_BF16 2
 #endif
@@ -747,7 +755,7 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
         constexpr int i = decltype(ic)::value;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            r_[p] = __builtin_amdgcn_raw_buffer_load_b128(rr, vadd_opq(vo_r, (int)(16 * i * ep.ld_res * 2)) + 64 * p, 0, 0);
+            r_[p] = __builtin_amdgcn_raw_buffer_load_b128(rr, vadd_opq(vo_r, (int)(16 * i * ep.ld_res * 2)) + 64 * p, 0, W4_RES_CPOL);
             if constexpr (HINT) h_[p] = __builtin_amdgcn_raw_buffer_load_b128(rh, vadd_opq(vo_h, (int)(16 * i * ep.ld_hint * 2)) + 64 * p, 0, 0);
         }
     };
@@ -822,7 +830,7 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
 #else
                 nl + 32 * p < N ? so : 0x7ffffff0,
 #endif
-                0, 0);
+                0, W4_OUT_CPOL);
             // one column block at a time: the scheduler would otherwise hoist the accumulator reads
             // of later blocks (AGPR -> VGPR copies) and run out of VGPRs
             __builtin_amdgcn_sched_barrier(0);
