@@ -129,8 +129,10 @@ int vs_attn_split_plan(int batch, int sq, int skv, int heads, int cus, int* out)
 /*
  * Library scratch (kind 0: vs_attn_fwd split tail, 1: vs_gemm split tail, 2: vs_gemm's hipBLASLt
  * workspace, 3: vs_gemm epilogue staging, M*N*2 bytes of the largest staged GEMM, 4: vs_attn_fwd
- * item flags, one int per item, ZERO-FILLED by the caller when bound -- every launch leaves it zero).
- * vs_split_workspace_bytes(kind) is the size that covers every plan of kinds 0-2 and 4 (-1 for kind 3);
+ * item flags, one int per item, ZERO-FILLED by the caller when bound -- every launch leaves it zero;
+ * 5: the tile queues of vs_gemm / vs_gemm_fp8's persistent 256x256 kernels, ZERO-FILLED when bound,
+ * left zero by every launch -- without one those kernels walk static per-CU tile lists).
+ * vs_split_workspace_bytes(kind) is the size that covers every plan of kinds 0-2, 4 and 5 (-1 for kind 3);
  * vs_split_workspace_bind(kind, ptr, bytes, stream) registers a caller-owned
  * device buffer (16-B aligned) for launches of that kind on `stream` of the current device
  * (ptr = NULL unbinds).  The buffer must stay valid while bound, including in captured graphs.

@@ -378,6 +378,65 @@ def model_fn(W, cfg, latents, timestep, context, vace_context=None, vace_scale=1
     return unpatchify(x, (f, h, w), cfg["out_dim"])
 
 
+def dit_block_rows(x, ctx, t_mod, freqs, W, p, num_heads, rows, eps=1e-6):
+    """dit_block (wan_video_dit.py:214-230) evaluated for the token rows `rows` of x only.  Every op
+    of the block is token-local except self-attention's keys / values, which come from every row of
+    x (LayerNorm + modulate + k / v projections + k's RMSNorm / RoPE over all S rows); the query rows,
+    the output projection, cross-attention, the FFN and both gate-residuals run on `rows` alone.
+    Per row the arithmetic is dit_block's, so the result equals dit_block(x, ...)[:, rows]."""
+    mod = bf(W[p + "modulation"].float() + t_mod.float())
+    shift_msa, scale_msa, gate_msa, shift_mlp, scale_mlp, gate_mlp = mod.chunk(6, dim=1)
+    h = modulate(layer_norm(x, eps), shift_msa, scale_msa)
+    a = p + "self_attn."
+    hr = h[:, rows]
+    q = rope_apply(rms_norm(blk_linear(hr, W[a + "q.weight"], W[a + "q.bias"]), W[a + "norm_q.weight"], eps),
+                   freqs[rows], num_heads)
+    k = rope_apply(rms_norm(blk_linear(h, W[a + "k.weight"], W[a + "k.bias"]), W[a + "norm_k.weight"], eps),
+                   freqs, num_heads)
+    v = blk_linear(h, W[a + "v.weight"], W[a + "v.bias"])
+    o = blk_linear(attention(q, k, v, num_heads), W[a + "o.weight"], W[a + "o.bias"])
+    del h, k, v
+    xr = gate_residual(x[:, rows], gate_msa, o)
+    hr = layer_norm(xr, eps, W[p + "norm3.weight"], W[p + "norm3.bias"])
+    xr = add(xr, cross_attention(hr, ctx, W, p + "cross_attn.", num_heads, eps))
+    hr = modulate(layer_norm(xr, eps), shift_mlp, scale_mlp)
+    f = blk_linear(gelu_tanh(blk_linear(hr, W[p + "ffn.0.weight"], W[p + "ffn.0.bias"])),
+                   W[p + "ffn.2.weight"], W[p + "ffn.2.bias"])
+    return gate_residual(xr, gate_mlp, f)
+
+
+def model_fn_rows(W, cfg, latents, timestep, context, vace_context, rows, vace_scale=1.0):
+    """model_fn (wan_video_new.py:1338-1468) of a ONE-block DiT with at most one VACE block, at the
+    token rows `rows` only: the head's output tokens (B, len(rows), 4 * out_dim) before unpatchify
+    (wan_video_dit.py:347-352).  Full-size parity without the S x S attention of every row: the
+    self-attention keys / values still come from all S tokens (dit_block_rows), so at S = 111 600
+    (1280x720x121) a few hundred sampled rows cost seconds instead of minutes."""
+    D, H, eps = cfg["dim"], cfg["num_heads"], cfg["eps"]
+    assert cfg["num_layers"] == 1 and len(cfg["vace_layers"]) <= 1, "model_fn_rows: a one-block pair"
+    t, t_mod = time_embed(timestep, W, D)
+    ctx = text_embed(context, W)
+    x, (f, h, w) = patchify(latents, W["patch_embedding.weight"], W["patch_embedding.bias"])
+    freqs = rope_freqs(f, h, w, D // H)
+    hint = None
+    if vace_context is not None and cfg["vace_layers"]:
+        c, _ = patchify(vace_context, W["vace_patch_embedding.weight"], W["vace_patch_embedding.bias"])
+        c = add(linear(c, W["vace_blocks.0.before_proj.weight"], W["vace_blocks.0.before_proj.bias"]), x)
+        c = dit_block_rows(c, ctx, t_mod, freqs, W, "vace_blocks.0.", H, rows, eps)
+        hint = linear(c, W["vace_blocks.0.after_proj.weight"], W["vace_blocks.0.after_proj.bias"])
+    xr = dit_block_rows(x, ctx, t_mod, freqs, W, "blocks.0.", H, rows, eps)
+    if hint is not None and 0 in cfg["vace_layers"]:
+        xr = add(xr, bf(hint.float() * vace_scale))
+    return head(xr, t, W, eps)
+
+
+def patchify_output(out, patch=(1, 2, 2)):
+    """The inverse of unpatchify: (B, C, F, 2h, 2w) -> tokens (B, F*h*w, 4*C) in the head's column
+    order (x y z c), so product outputs can be compared at token rows."""
+    b, c, ff, hh, ww = out.shape
+    h, w = hh // patch[1], ww // patch[2]
+    return out.view(b, c, ff, 1, h, 2, w, 2).permute(0, 2, 4, 6, 3, 5, 7, 1).reshape(b, ff * h * w, 4 * c)
+
+
 def denoise(W, cfg, latents, context_pos, context_neg, vace_context=None, num_inference_steps=2,
             cfg_scale=5.0, sigma_shift=5.0, vace_scale=1.0, num_layers=None, tea_caches=None):
     """WanVideoPipeline.__call__ denoise loop, wan_video_new.py:484,515-542 (cfg_merge=False).

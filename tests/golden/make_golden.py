@@ -3,7 +3,7 @@
 The reference could not be executed here (denied) and ships no vectors, so these
 fixtures are the oracle's own outputs on seeded synthetic inputs: they pin the GPU path (and the
 oracle itself) against drift.  bf16 tensors are stored as uint16 bit patterns.
-Run:  python tests/golden/make_golden.py [tiny|c1|ops|all]
+Run:  python tests/golden/make_golden.py [tiny|c1|ops|vae480|all]
 """
 import os
 import sys
@@ -67,12 +67,53 @@ def run_ops():
     print("ops: written")
 
 
+def run_vae480():
+    """The causal VAE's tiled encode + decode at 480x832 (5 frames: two latent frames, the causal cache
+    path) with the real 3x3 grid of 30x52-latent tiles (stride 15x26, wan_video_vae.py:1103-1203) at
+    the Wan2.1 widths, random weights (seed 31): the oracle's fp32 outputs and their fp32/fp64 noise
+    floor, for tests/test_production_c4c5_gpu.py (the host convolutions take minutes, so the GPU tier
+    compares against these).  The decode is stored at every 8th output row (all frames, channels,
+    columns: every tile row and both vertical seams of each tile column)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE)))
+    from oracle import wan_vae_oracle as V
+    from vae_util import synthetic_video
+    W = V.random_vae_weights(seed=31)
+    video = synthetic_video(5, 480, 832)
+    ts, st = (30, 52), (15, 26)
+
+    def floor(a, b):
+        d = a.float() - b.float()
+        return [d.abs().max().item(), (d.norm() / b.float().norm()).item()]
+
+    def both(fn):
+        r32 = fn()
+        O.ACC_DTYPE = torch.float64
+        try:
+            r64 = fn()
+        finally:
+            O.ACC_DTYPE = torch.float32
+        return r32, r64
+    t0 = time.time()
+    enc, enc64 = both(lambda: V.tiled_encode(video, W, ts, st))
+    dec, dec64 = both(lambda: V.tiled_decode(enc, W, ts, st))
+    rows = slice(0, None, 8)
+    np.savez_compressed(os.path.join(HERE, "vae_480x832.npz"), enc=u16(enc), dec_rows8=u16(dec[..., rows, :]),
+                        noise_enc=np.array(floor(enc64, enc)),
+                        noise_dec_rows8=np.array(floor(dec64[..., rows, :], dec[..., rows, :])),
+                        video_sum=np.array(video.float().sum().item()),
+                        weight_sum=np.array(sum(v.float().sum().item() for v in W.values())))
+    print(f"vae480: enc {tuple(enc.shape)} floor {floor(enc64, enc)}, dec {tuple(dec.shape)} floor "
+          f"{floor(dec64, dec)} ({time.time() - t0:.0f} s)")
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which in ("ops", "all"):
         run_ops()
     if which in ("tiny", "all"):
         run_denoise("tiny_2step", O.WAN_CONFIGS["tiny"], 5, 128, 128, 2)
+    if which in ("vae480", "all"):
+        run_vae480()
     if which in ("c1", "all"):
         # BASELINE config 0 ("C1"): random-init 1.3B-shape DiT+VACE, 2 Euler steps, 5 frames 128x128
         run_denoise("c1_1p3b_2step", O.WAN_CONFIGS["1.3B"], 5, 128, 128, 2)

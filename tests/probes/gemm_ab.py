@@ -1,6 +1,6 @@
-"""A/B: the hand-written staggered 8-phase GEMM (vstyler), the 4-wave kernel (w4) and the hipBLASLt
-route (lt, + its epilogue pass), per 14B block GEMM with its real epilogue; interleaved rounds, one
-process (AB_VARIANTS=vstyler,w4,lt).  A third build
+"""A/B: the hand-written staggered 8-phase GEMM (8p), the 4-wave kernel with the XCD tile queues (w4)
+or the static per-CU lists (w4s) and the hipBLASLt route (lt, + its epilogue pass), per 14B block
+GEMM with its real epilogue; interleaved rounds, one process (AB_VARIANTS=w4,w4s,lt).  A third build
 can join with AB_VARIANTS=vstyler,lt,diag:<path to libvstyler.so> (not loaded here: run per build).
 usage: gemm_ab.py [M ...]"""
 import os, sys
@@ -28,7 +28,7 @@ SHAPES = (("qkv", 15360, 5120, K.VS_EPI_BIAS), ("o-proj", 5120, 5120, K.VS_EPI_G
           ("ffn-up", 13824, 5120, K.VS_EPI_GELU), ("ffn-down", 5120, 13824, K.VS_EPI_GATE_RES),
           ("cross-o", 5120, 5120, K.VS_EPI_RES))
 SHAPES = tuple(sh for sh in SHAPES if sh[0] in os.environ.get("AB_SHAPES", ",".join(x[0] for x in SHAPES)).split(","))
-VARIANTS = [v for v in os.environ.get("AB_VARIANTS", "vstyler,lt").split(",")]
+VARIANTS = [v for v in os.environ.get("AB_VARIANTS", "w4,w4s,lt").split(",")]
 for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
     for name, N, Kd, epi in SHAPES:
         g = torch.Generator(device="cuda").manual_seed(1)
@@ -44,22 +44,11 @@ for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
             kw.update(residual=x)
         out = x if epi in (K.VS_EPI_GATE_RES, K.VS_EPI_RES) else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 
-        def setv(v):       # <kernel>[_d<N>][_g<G>][_r<R>]: VS_GEMM_DESYNC (diagnostic), VS_GEMM_GM, VS_GEMM_ROUNDS
-            v, _, rr = v.partition("_r")
-            if rr:
-                os.environ["VS_GEMM_ROUNDS"] = rr
-            else:
-                os.environ.pop("VS_GEMM_ROUNDS", None)
-            v, _, gm = v.partition("_g")
-            base, _, ds = v.partition("_d")
-            os.environ["VS_GEMM_BACKEND"] = "lt" if base == "lt" else "vstyler"
+        def setv(v):       # lt | 8p (vstyler) | w4 (4-wave, XCD tile queues) | w4s (4-wave, static lists)
+            os.environ["VS_GEMM_BACKEND"] = "lt" if v == "lt" else "vstyler"
             os.environ["VSTYLER_GEMM_TILE"] = "256"
-            os.environ["VS_GEMM_KERNEL"] = "4w" if base == "w4" else "8p"
-            os.environ["VS_GEMM_DESYNC"] = ds or "0"
-            if gm:
-                os.environ["VS_GEMM_GM"] = gm
-            else:
-                os.environ.pop("VS_GEMM_GM", None)
+            os.environ["VS_GEMM_KERNEL"] = "4w" if v.startswith("w4") else "8p"
+            os.environ["VS_GEMM_QUEUE"] = "0" if v == "w4s" else "1"
         t = {v: [] for v in VARIANTS}
         for v in VARIANTS:             # warm (hipBLASLt autotune happens here)
             setv(v); K.gemm(a, w, out, **kw); torch.cuda.synchronize()
@@ -70,5 +59,5 @@ for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
         s = "  ".join(f"{v} {min(t[v]):.3f} ms ({fl / min(t[v]) / 1e9:.0f} TF/s)" for v in VARIANTS)
         print(f"M={M} {name:8s} N={N} K={Kd}: {s}", flush=True)
         del a, w, b, gate, x, out
-for k in ("VS_GEMM_BACKEND", "VSTYLER_GEMM_TILE", "VS_GEMM_KERNEL", "VS_GEMM_DESYNC", "VS_GEMM_GM", "VS_GEMM_ROUNDS"):
+for k in ("VS_GEMM_BACKEND", "VSTYLER_GEMM_TILE", "VS_GEMM_KERNEL", "VS_GEMM_QUEUE"):
     os.environ.pop(k, None)

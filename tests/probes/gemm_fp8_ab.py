@@ -19,7 +19,7 @@ def timed(fn, reps=3):
 
 SHAPES = (("qkv", 15360, 5120, K.VS_EPI_BIAS), ("o-proj", 5120, 5120, K.VS_EPI_GATE_RES),
           ("ffn-up", 13824, 5120, K.VS_EPI_GELU), ("ffn-down", 5120, 13824, K.VS_EPI_GATE_RES))
-VARIANTS = os.environ.get("AB_VARIANTS", "vstyler,lt").split(",")
+VARIANTS = os.environ.get("AB_VARIANTS", "w4,w4s,lt").split(",")
 for M in [int(v) for v in sys.argv[1:]] or (59280,):
     for name, N, Kd, epi in SHAPES:
         g = torch.Generator(device="cuda").manual_seed(1)
@@ -36,9 +36,10 @@ for M in [int(v) for v in sys.argv[1:]] or (59280,):
             kw.update(residual=x, gate=gate, gate_bstride=N, rows_per_batch=(M + 1) // 2)
         out = x if epi == K.VS_EPI_GATE_RES else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         t = {v: [] for v in VARIANTS}
-        def setv(v):      # vstyler = the 8-phase kernel, w4 = the 4-wave kernel, lt = hipBLASLt fp8
-            os.environ["VS_FP8_BACKEND"] = "vstyler" if v in ("vstyler", "w4") else v
-            os.environ["VS_GEMM_KERNEL"] = "4w" if v == "w4" else "8p"
+        def setv(v):      # 8p = the 8-phase kernel, w4 / w4s = the 4-wave kernel (tile queues / static lists), lt = hipBLASLt fp8
+            os.environ["VS_FP8_BACKEND"] = "lt" if v == "lt" else "vstyler"
+            os.environ["VS_GEMM_KERNEL"] = "4w" if v.startswith("w4") else "8p"
+            os.environ["VS_GEMM_QUEUE"] = "0" if v == "w4s" else "1"
         for v in VARIANTS:
             setv(v)
             K.gemm_fp8(a8, sc, w8, out, **kw); torch.cuda.synchronize()
@@ -52,3 +53,4 @@ for M in [int(v) for v in sys.argv[1:]] or (59280,):
         del a, w8, a8, sc, b, gate, x, out
 os.environ.pop("VS_FP8_BACKEND", None)
 os.environ.pop("VS_GEMM_KERNEL", None)
+os.environ.pop("VS_GEMM_QUEUE", None)

@@ -11,7 +11,7 @@ if which == "attn":
     o = torch.empty_like(q)
     fn = lambda: K.attention(q, k, v, o, H, B)
 else:
-    M, N, Kd = int(os.environ.get("KP_M", "59280")), 13824, 5120    # KP_M: the row count (default the SP = 1 FFN-up)
+    M, N, Kd = int(os.environ.get("KP_M", "59280")), int(os.environ.get("KP_N", "13824")), 5120    # KP_M / KP_N: rows / columns (default the SP = 1 FFN-up)
     a = torch.randn(M, Kd, device="cuda", generator=g).to(torch.bfloat16)
     w = (0.05 * torch.randn(N, Kd, device="cuda", generator=g)).to(torch.bfloat16)
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)

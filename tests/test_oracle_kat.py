@@ -137,3 +137,25 @@ def test_loader_configs_from_shapes_and_shards(tmp_path):
     sd = load_state_dict([str(tmp_path / "a-00001-of-00002.safetensors"),
                           str(tmp_path / "a-00002-of-00002.safetensors")])
     assert set(sd) == set(W) and all(torch.equal(sd[k], W[k]) for k in W)
+
+
+def test_model_fn_rows_matches_full_model_fn():
+    """O.model_fn_rows (the C4 GPU test's oracle: a one-block pair evaluated at sampled token rows,
+    keys / values from every row) equals O.model_fn at those rows, tiny config on the CPU (up to the
+    GEMM's row-blocking order: a bf16 ulp here and there)."""
+    cfg = dict(O.WAN_CONFIGS["tiny"], num_layers=1, vace_layers=(0,))
+    W = O.random_weights(cfg, seed=9)
+    lat, cp, cn, vc = O.synthetic_inputs(cfg, 9, 64, 96)
+    t = torch.tensor([600.0, 600.0]).to(torch.bfloat16)
+    ctx = torch.cat([cp, cn])
+    full = O.patchify_output(O.model_fn(W, cfg, torch.cat([lat, lat]), t, ctx, torch.cat([vc, vc]), vace_scale=0.9))
+    S = full.shape[1]
+    rows = torch.tensor([0, 5, 47, 48, S // 2, S - 1])
+    got = O.model_fn_rows(W, cfg, torch.cat([lat, lat]), t, ctx, torch.cat([vc, vc]), rows, vace_scale=0.9)
+    ref = full[:, rows]
+    d = (got.float() - ref.float())
+    assert got.shape == ref.shape
+    assert (d.norm() / ref.float().norm()).item() < 2e-3 and d.abs().max().item() < 2e-2
+    # patchify_output inverts unpatchify
+    x = torch.randn(2, 3 * 4 * 16).view(2, 3, 64).to(torch.bfloat16)
+    assert torch.equal(O.patchify_output(O.unpatchify(x.view(2, 3, 64), (3, 1, 1))), x)

@@ -442,3 +442,24 @@ def test_plan_native_comms_cpu():
     assert plan_native_comms(None) == []
     shared = NS(native=side[0], ulysses=NS(native=side[0]))
     assert plan_native_comms(shared) == [side[0]]
+
+
+def test_unbound_side_comms_guard():
+    """DenoiseStepper.capture refuses to capture while a live side-stream NativeComm is not bound to
+    the capture stream (RCCL forked into a capture from a side stream segfaulted in
+    hipStreamEndCapture), whatever plan attribute holds the communicator."""
+    from vstyler import usp
+
+    class FakeComm:                      # the attributes unbound_side_comms reads
+        def __init__(self, stream):
+            self.stream = stream
+    side, caller = FakeComm("side-stream"), FakeComm(None)
+    usp.NativeComm._live.add(side)
+    usp.NativeComm._live.add(caller)
+    try:
+        assert usp.unbound_side_comms("capture-origin") == [side]
+        side.stream = "capture-origin"   # what bind_stream does for the capture
+        assert usp.unbound_side_comms("capture-origin") == []
+    finally:
+        usp.NativeComm._live.discard(side)
+        usp.NativeComm._live.discard(caller)

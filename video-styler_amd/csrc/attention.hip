@@ -1100,11 +1100,12 @@ extern "C" long long vs_split_workspace_bytes(int kind) {
     if (kind == 1) return vs_gemm_split_workspace_bytes_impl();
     if (kind == 2) return 128LL << 20;          // hipBLASLt (stream-K partials)
     if (kind == 4) return 1LL << 20;            // attention item flags (int per item; zero-filled)
+    if (kind == 5) return 4096;                 // GEMM tile-queue words (zero-filled; gemm.hip W4Sched)
     return -1;                                  // kind 3: m * n * 2 bytes of the largest routed GEMM
 }
 
 extern "C" int vs_split_workspace_bind(int kind, void* ptr, long long bytes, void* stream) {
-    if (kind < 0 || kind > 4 || bytes < 0 || (ptr && ((uintptr_t)ptr & 15))) return VS_E_INVALID;
+    if (kind < 0 || kind > 5 || bytes < 0 || (ptr && ((uintptr_t)ptr & 15))) return VS_E_INVALID;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return VS_E_LAUNCH;
     std::mutex* mu;

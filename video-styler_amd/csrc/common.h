@@ -81,7 +81,9 @@ inline int vs_cus_for_split(const char* env_off) {
 // Split-tail scratch is caller-owned (the library never allocates): the host binds one fp32
 // workspace per (kind, device, stream) with vs_split_workspace_bind; a launch on a stream without
 // one runs unsplit.  kind 0: attention split tail, 1: GEMM split tail, 2: hipBLASLt workspace,
-// 3: bf16 staging for epilogues finished after a hipBLASLt GEMM (gate-residual / residual).
+// 3: bf16 staging for epilogues finished after a hipBLASLt GEMM (gate-residual / residual),
+// 4: attention item flags, 5: the 4-wave GEMMs' tile-queue words (4 and 5 bound zero-filled; the
+// kernels leave them zero).
 struct VsWs { float* ptr; long long bytes; };
 inline std::map<std::tuple<int, int, hipStream_t>, VsWs>& vs_ws_registry(std::mutex*& mu) {
     static std::mutex m;

@@ -42,19 +42,8 @@ struct Epi {
     float alpha;
     int rows_per_batch;
     int mode;
-    int desync;       // diagnostic (VS_GEMM_DESYNC): the first round's blocks sleep (b % 256) / 256 x this many ~4 us units
-    int gm;           // M-tiles per raster group of the 256x256 tile order (VS_GEMM_GM, default VS_GEMM_GM)
-    int rounds;       // persistent rounds of the 4-wave kernels (set per launch by the host, see w4_work)
+    int gm;           // M-tiles per raster group of the 256x256 tile order (VS_GEMM_GM)
 };
-
-// staggered start of the first round of blocks (diagnostic: do tile epilogues that coincide on
-// every CU cost more than staggered ones?)
-__device__ __forceinline__ void desync_start(const Epi& ep) {
-    if (ep.desync > 0 && blockIdx.x < 256) {
-        const int n = (int)(blockIdx.x % 256) * ep.desync / 256;
-        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-    }
-}
 
 __device__ __forceinline__ int g_off(int row, int ch) { return row * 128 + 16 * (ch ^ (row & 7)); }
 
@@ -351,7 +340,6 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_tn_8p(
     int tm, tn;
     tile_of(pid, ntm, ntn, ep.gm, tm, tn);
     const int m0 = tm * T8, n0 = tn * T8;
-    desync_start(ep);
     const int kb = piece < 0 ? 0 : piece * piece_k;
     const int Kp = piece < 0 ? K : min(K - kb, piece_k);
     const int nk1 = Kp / 64;
@@ -740,11 +728,7 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
         }
     }
     // (resources of absent operands point at C with an empty range: never read)
-#if defined(W4_DIAG) && (W4_DIAG & 2)   // diagnostic build: residual loads answered by the range check
-    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(C, 0, 0, 0x00020000);
-#else
     const __amdgpu_buffer_rsrc_t rr = RESID ? rsrc(ep.res, ep.ld_res, true) : rsrc(C, ldc, false);
-#endif
     const __amdgpu_buffer_rsrc_t rh = HINT ? rsrc(ep.hint, ep.ld_hint, true) : rsrc(C, ldc, false);
     const int vo_r = RESID ? (int)((r * ep.ld_res + n_w + ncol) * 2) : 0;
     const int vo_h = HINT ? (int)((r * ep.ld_hint + n_w + ncol) * 2) : 0;
@@ -823,14 +807,8 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
             // rows past M fall outside rc's range, columns past N get an offset outside it: the
             // hardware drops those stores (no per-store branch)
             const int so = vadd_opq(vo_c, (int)(16 * i * ldc * 2)) + 64 * p;
-            __builtin_amdgcn_raw_buffer_store_b128(
-                u32x4_t{wo[0], wo[1], wo[2], wo[3]}, rc,
-#if defined(W4_DIAG) && (W4_DIAG & 1)   // diagnostic build: every store dropped by the range check
-                0x7ffffff0,
-#else
-                nl + 32 * p < N ? so : 0x7ffffff0,
-#endif
-                0, W4_OUT_CPOL);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{wo[0], wo[1], wo[2], wo[3]}, rc,
+                                                   nl + 32 * p < N ? so : 0x7ffffff0, 0, W4_OUT_CPOL);
             // one column block at a time: the scheduler would otherwise hoist the accumulator reads
             // of later blocks (AGPR -> VGPR copies) and run out of VGPRs
             __builtin_amdgcn_sched_barrier(0);
@@ -839,165 +817,152 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
     });
 }
 
-// The same epilogue with 8-B accesses straight from the MFMA layout (lane: 4 consecutive columns
-// n_w + 16 j + 4 (lane >> 4) of each of its 8 rows): no permlane pairing, twice the store
-// instructions (W4_NARROW A/B).
-__device__ __forceinline__ u32x2_t ld8(const bf16_t* p) { return *reinterpret_cast<const u32x2_t*>(p); }
-template <int MODE, bool HINT, bool SCALED, class AccT>
-__device__ __forceinline__ void tile_epilogue_w4n(const AccT& acc, int m_w, int n_w, int lane, bf16_t* C, long long ldc,
-                                                  int M, int N, const Epi& ep, const float* __restrict__ scale_a) {
-    constexpr bool RESID = MODE == VS_EPI_GATE_RES || MODE == VS_EPI_RES;
-    const int ncol = 4 * (lane >> 4);
-    const int nl = n_w + ncol;                            // + 16 j
-    const int r = lane & 15;                              // + 16 i
-    const int rows = max(0, min(128, M - m_w));
-    // (num_records through readfirstlane: the compiler formed the clamp with its 128 in a VGPR and
-    // then wrapped every access in a waterfall loop)
-    auto rsrc = [&](const bf16_t* base, long long ld, bool load) {
-        return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base + (long long)m_w * ld), 0,
-                                                 load ? __builtin_amdgcn_readfirstlane((int)((long long)rows * ld * 2))
-                                                      : 0x7fffffff, 0x00020000);
-    };
-    const __amdgpu_buffer_rsrc_t rc = rsrc(C, ldc, false);
-    const int vo_c = (int)((r * ldc + n_w + ncol) * 2);
-#if defined(W4_DIAG) && (W4_DIAG & 2)   // diagnostic build: residual loads answered by the range check
-    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(C, 0, 0, 0x00020000);
-#else
-    const __amdgpu_buffer_rsrc_t rr = RESID ? rsrc(ep.res, ep.ld_res, true) : rsrc(C, ldc, false);
-#endif
-    const __amdgpu_buffer_rsrc_t rh = HINT ? rsrc(ep.hint, ep.ld_hint, true) : rsrc(C, ldc, false);
-    const int vo_r = RESID ? (int)((r * ep.ld_res + n_w + ncol) * 2) : 0;
-    const int vo_h = HINT ? (int)((r * ep.ld_hint + n_w + ncol) * 2) : 0;
-    int b_lo = 0;
-    if constexpr (MODE == VS_EPI_GATE_RES) b_lo = min(m_w, M - 1) / ep.rows_per_batch;
-    const int b_hi = MODE == VS_EPI_GATE_RES ? min(m_w + 127, M - 1) / ep.rows_per_batch : 0;
-    static_for<8>([&](auto ic) __attribute__((always_inline)) {
-        constexpr int i = decltype(ic)::value;
-        const int m = m_w + r + 16 * i;
-        float sa = 1.f;
-        if constexpr (SCALED) sa = scale_a[min(m, M - 1)];
-        u32x2_t rv2[8], hv2[8];
-        if constexpr (RESID) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                rv2[j] = __builtin_amdgcn_raw_buffer_load_b64(rr, vadd_opq(vo_r, (int)(16 * i * ep.ld_res * 2)) + 32 * j, 0, 0);
-                if constexpr (HINT) hv2[j] = __builtin_amdgcn_raw_buffer_load_b64(rh, vadd_opq(vo_h, (int)(16 * i * ep.ld_hint * 2)) + 32 * j, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int n = nl + 16 * j;
-            const int nc = min(n, N - 4);
-            float y[4], bv[4] = {0.f, 0.f, 0.f, 0.f};
-            if (ep.bias) loadw<4>(ep.bias + nc, bv);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float x = acc_rd(acc[i][j][e]);
-                y[e] = rbf((SCALED ? x * sa : x) + bv[e]);
-            }
-            if constexpr (MODE == VS_EPI_GELU) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) y[e] = gelu_tanh_f(y[e]);
-            } else if constexpr (MODE == VS_EPI_SILU) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) y[e] = silu_f(y[e]);
-            } else if constexpr (MODE == VS_EPI_GATE_RES) {
-                float gv[4];
-                const int bi = m / ep.rows_per_batch != b_lo ? b_hi : b_lo;
-                loadw<4>(ep.gate + (long long)bi * ep.gate_bstride + nc, gv);
-                const float rv[4] = {bflo(rv2[j][0]), bfhi(rv2[j][0]), bflo(rv2[j][1]), bfhi(rv2[j][1])};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) y[e] = rbf(rv[e] + rbf(gv[e] * y[e]));
-                if constexpr (HINT) {
-                    const float hv[4] = {bflo(hv2[j][0]), bfhi(hv2[j][0]), bflo(hv2[j][1]), bfhi(hv2[j][1])};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) y[e] = y[e] + rbf(hv[e] * ep.hint_scale);
-                }
-            } else if constexpr (MODE == VS_EPI_RES) {
-                const float rv[4] = {bflo(rv2[j][0]), bfhi(rv2[j][0]), bflo(rv2[j][1]), bfhi(rv2[j][1])};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) y[e] = rv[e] + rbf(ep.alpha * y[e]);
-            }
-            if (m < M && n < N)
-                __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack2(y[0], y[1]), pack2(y[2], y[3])}, rc,
-                                                      vo_c + 32 * j, (int)(16 * i * ldc * 2), 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    });
-}
-
-template <bool SCALED, class AccT>
-__device__ __forceinline__ void tile_epilogue_w4_dispatch(const AccT& acc, int m_w, int n_w, int lane, bf16_t* C,
-                                                          long long ldc, int M, int N, const Epi& ep,
-                                                          const float* __restrict__ scale_a) {
-#ifdef W4_ONLY_BIAS
-    tile_epilogue_w4<W4_ONLY_BIAS, false, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a);
-    return;
-#endif
-    switch (ep.mode) {
-        case VS_EPI_GELU: tile_epilogue_w4<VS_EPI_GELU, false, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a); break;
-        case VS_EPI_SILU: tile_epilogue_w4<VS_EPI_SILU, false, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a); break;
-        case VS_EPI_GATE_RES:
-            if (ep.hint) tile_epilogue_w4<VS_EPI_GATE_RES, true, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a);
-            else tile_epilogue_w4<VS_EPI_GATE_RES, false, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a);
-            break;
-        case VS_EPI_RES: tile_epilogue_w4<VS_EPI_RES, false, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a); break;
-        default: tile_epilogue_w4<VS_EPI_BIAS, false, SCALED>(acc, m_w, n_w, lane, C, ldc, M, N, ep, scale_a); break;
-    }
-}
-
 constexpr int W4_ROWB = 1056;                 // LDS row: 8 global rows x 128 B + 32 B pad
 constexpr int W4_OPB = 32 * W4_ROWB;          // one operand's K-tile image (256 rows x 64 k)
 constexpr int W4_LDS = 4 * W4_OPB;            // [A b0][A b1][W b0][W b1] = 135168 B
 static_assert(4 * W4_ROWB == 0x1080, "the 4w kernel's M0 step");
 
-// Work of one 4w block.  Blocks [0, npers) are persistent: each walks tiles_per tiles of its XCD's
-// contiguous chunk of [0, npers * tiles_per) (block b: XCD b % 8, slot b / 8, tiles slot, slot + G8, ..)
-// as ONE stream of K-tiles -- the DMA runs two K-tiles ahead straight across tile boundaries, so a
-// tile's first K-tiles land during the previous tile's last iterations and its epilogue (no prologue
-// wait, no per-tile launch).  The blocks after them run one whole tile each (up to nmain) and then
-// the split-tail K pieces of the last tiles.
-struct W4Work {
-    int ntw;          // tiles in this block's list
-    int piece;        // split-tail piece (-1: whole tiles)
-    int kb, nt;       // K offset (elements) and K-tiles per tile
-    int p0, pstep;    // tile ids: p0 + k * pstep (persistent), or p0
+// ---------------------------------------------------------------------------------------------
+// Tile schedule of the 4-wave kernels (r5): persistent workgroups fed by XCD-local tile queues.
+//
+// Blocks [0, npers) are persistent (one per CU): block b sits on XCD x = b % 8 (round-robin
+// dispatch) in slot s = b / 8 and computes tiles of its XCD's contiguous id range [x R, (x+1) R),
+// R = G8 tp (G8 = npers / 8), as ONE stream of K-tiles: the DMA runs two K-tiles ahead straight
+// across tile boundaries, so a tile's first K-tiles land during the previous tile's last K-tiles
+// and its epilogue.  A block's first two tiles are fixed (range positions s and G8 + s); after
+// them it takes tiles from its XCD's queue (head word q[x]: positions 2 G8 + t, t = 0, 1, ..), then,
+// once that has run dry, from the other XCDs' queues (probed in ring order), then from the
+// remainder pool (the nrem whole tiles past npers tp, head q[8]).
+//   r4 walked a static list (positions s, s + G8, s + 2 G8, ..).  Over a 54-tile list an XCD's CUs
+//   drifted apart, so the 32 tiles in flight on an XCD stopped being one 4 x 8 block sharing its A / W
+//   slices in L2 (FFN-up: 23.1 GB of fabric reads per dispatch against the library's 13.1,
+//   profiles/r4/pmc_fetch_rows.txt), and a CU held by a concurrent kernel (RCCL under the Ulysses
+//   overlap) delayed its whole list.  With the queue the tiles computing on an XCD are always about
+//   the 32 most recently taken ids, and a CU that is slow or held simply takes fewer.
+// The next tile id is known one tile ahead: wave 0 takes it during tile k's epilogue (its atomic
+// issued at the epilogue's start and its value used at the end, under the stores), writes it to an
+// LDS word, and every wave reads that word in tile k+1's first K-tile behind a barrier -- before the
+// DMA cursor crosses into tile k+2 at the end of K-tile nt - 3 (nt >= 3, host-checked).  The last
+// persistent block to finish (exit count q[9]) zeroes the queue words, so every launch finds them
+// zero (workspace kind 5: bound zeroed, one per stream, so graph replays and concurrent streams are
+// safe).  Without a bound queue the same walk runs the static list and the nrem whole tiles get
+// blocks of their own.  The blocks after those run the split-tail K pieces of the last tiles.
+// ---------------------------------------------------------------------------------------------
+constexpr int WQ_LINE = 32;                   // queue words 128 B apart (a line each)
+constexpr int WQ_BYTES = 10 * WQ_LINE * 4;    // 8 XCD heads, the remainder head, the exit count
+struct W4Sched {
+    unsigned* q;      // queue words (null: static lists)
+    int npers;        // persistent blocks (a multiple of 8, or 0)
+    int tp;           // tiles per slot of an XCD range (>= 2 with a queue)
+    int nrem;         // whole tiles past npers * tp
 };
-// rounds (Epi::rounds, VS_GEMM_ROUNDS): the persistent range split into `rounds` successive grids of
-// npers workgroups, each walking L = ceil(tiles_per / rounds) tiles of its XCD's range, round r the
-// r-th L-tile slab -- shorter lists drift less (the CUs of an XCD share their 4x8 block's A / W
-// slices in L2 only while K-aligned); the host passes rounds <= tiles_per with no empty round
-__device__ __forceinline__ W4Work w4_work(int K, int nmain, int ksplit, int piece_k, int npers, int tiles_per, int kstep,
-                                          int rounds) {
+struct W4Work {
+    int first, second;  // the block's first two tile ids (-1: none)
+    int piece;          // split-tail piece (-1: whole tiles)
+    int kb, nt;         // K offset (elements) and K-tiles per tile
+};
+__device__ __forceinline__ W4Work w4_work(const W4Sched& sc, int K, int nmain, int ksplit, int piece_k, int kstep) {
     W4Work w;
     const int b = blockIdx.x;
     w.piece = -1;
     w.kb = 0;
     w.nt = K / kstep;
-    const int npr = npers * rounds;
-    if (b < npr) {
-        const int g8 = npers >> 3;
-        const int r = b / npers, bb = b - r * npers;
-        const int L = (tiles_per + rounds - 1) / rounds;
-        const int k0 = r * L;
-        w.ntw = max(0, min(L, tiles_per - k0));
-        w.p0 = (bb & 7) * (g8 * tiles_per) + k0 * g8 + (bb >> 3);
-        w.pstep = g8;
-    } else if (b < npr + (nmain - npers * tiles_per)) {
-        w.ntw = 1;
-        w.p0 = npers * tiles_per + (b - npr);
-        w.pstep = 0;
+    w.second = -1;
+    const int nstat = sc.q ? 0 : sc.nrem;          // remainder tiles with blocks of their own
+    if (b < sc.npers) {
+        const int g8 = sc.npers >> 3, base = (b & 7) * g8 * sc.tp, s = b >> 3;
+        w.first = base + s;
+        if (sc.tp >= 2) w.second = base + g8 + s;
+    } else if (b < sc.npers + nstat) {
+        w.first = sc.npers * sc.tp + (b - sc.npers);
     } else {
-        const int t = b - npr - (nmain - npers * tiles_per);
-        w.ntw = 1;
-        w.p0 = nmain + t / ksplit;
-        w.pstep = 0;
+        const int t = b - sc.npers - nstat;
+        w.first = nmain + t / ksplit;
         w.piece = t % ksplit;
         w.kb = w.piece * piece_k;
         w.nt = min(K - w.kb, piece_k) / kstep;
     }
     return w;
 }
+__device__ __forceinline__ unsigned wq_add(unsigned* p) {
+    return __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The tile taking of one persistent block (wave 0; see the schedule above).  issue(): the atomic on
+// the XCD's head, lane 0 only, at the start of an epilogue; finish<W>(): the tile id (-1: none
+// left), wave-uniform, at its end.  The head atomic is inline asm that sets EXEC to lane 0 itself:
+// as a compiler-visible atomic, the compiler's wait before its value is used was a vmcnt(0) (it
+// cannot count across the epilogue's branches), i.e. the epilogue's stores drained before the next
+// tile -- the per-tile wait r4 removed (gemm_drain_ab.log) -- and its atomic optimizer consumed the
+// value right after the atomic (Makefile).  finish<W>() waits vmcnt(W) instead: VMEM operations
+// complete in issue order and the caller has issued >= W of them since issue() (the epilogue's),
+// so the atomic has returned.  The steal / remainder atomics are ordinary ones (rare: once the own
+// queue has run dry).
+struct W4Grab {
+    const W4Sched& sc;
+    int k = 2;                  // static list: position of the next tile
+    bool local = true;          // the XCD's own queue may still hold tiles
+    bool steal = true;          // another XCD's queue may
+    unsigned t0 = 0;
+    __device__ __forceinline__ explicit W4Grab(const W4Sched& s) : sc(s) {}
+    __device__ __forceinline__ void issue() {
+        if (!sc.q || !local) return;
+        unsigned long long sv;
+        asm volatile("s_mov_b64 %1, exec\n\t"
+                     "s_mov_b64 exec, 1\n\t"
+                     "global_atomic_add %0, %2, %3, %4 sc0\n\t"
+                     "s_mov_b64 exec, %1"
+                     : "=&v"(t0), "=&s"(sv)
+                     : "v"(0), "v"(1u), "s"(sc.q + (blockIdx.x & 7) * WQ_LINE)
+                     : "memory");
+    }
+    template <int W>
+    __device__ __forceinline__ int finish(int lane) {
+        const int g8 = sc.npers >> 3, x = blockIdx.x & 7;
+        if (!sc.q) {
+            const int id = k < sc.tp ? x * g8 * sc.tp + k * g8 + (blockIdx.x >> 3) : -1;
+            ++k;
+            return id;
+        }
+        const unsigned qlen = (unsigned)(g8 * (sc.tp - 2));
+        if (local) {
+            unsigned t;
+            asm volatile("s_waitcnt vmcnt(%1)\n\tv_readfirstlane_b32 %0, %2" : "=s"(t) : "n"(W), "v"(t0) : "memory");
+            if (t < qlen) return x * g8 * sc.tp + 2 * g8 + (int)t;
+            local = false;
+        }
+        // other XCDs' queues: lanes 0-6 probe heads x+1 .. x+7, the first live one in ring order is
+        // taken from (a lost race just probes again; heads only grow, so this ends)
+        for (int it = 0; steal && it < 16; ++it) {
+            unsigned h = qlen;
+            if (lane < 7) h = __hip_atomic_load(sc.q + ((x + 1 + lane) & 7) * WQ_LINE, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long live = __ballot(lane < 7 && h < qlen);
+            if (!live) {
+                steal = false;
+                break;
+            }
+            const int v = (x + 1 + (int)__builtin_ctzll(live)) & 7;
+            unsigned t = 0;
+            if (lane == 0) t = wq_add(sc.q + v * WQ_LINE);
+            t = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
+            if (t < qlen) return v * g8 * sc.tp + 2 * g8 + (int)t;
+        }
+        steal = false;
+        if (sc.nrem > 0) {
+            unsigned u = 0;
+            if (lane == 0) u = wq_add(sc.q + 8 * WQ_LINE);
+            u = (unsigned)__builtin_amdgcn_readfirstlane((int)u);
+            if (u < (unsigned)sc.nrem) return sc.npers * sc.tp + (int)u;
+        }
+        return -1;
+    }
+    // after the block's last tile: the last persistent block to finish zeroes the queue words
+    __device__ __forceinline__ void done(int tid) {
+        if (!sc.q || (int)blockIdx.x >= sc.npers || tid != 0) return;
+        if (wq_add(sc.q + 9 * WQ_LINE) == (unsigned)sc.npers - 1)
+            for (int i = 0; i < 10; ++i) __hip_atomic_store(sc.q + i * WQ_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+};
 
 // the DMA issued before MFMA q of a K-tile of gemm_bf16_tn_4w (-1: none): W instructions 0-7 as
 // d = 0-7, A instructions 0-7 as d = 8-15 (the library kernel's placement, see the body)
@@ -1015,13 +980,11 @@ template <int MODE, bool HINT>
 __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     const bf16_t* __restrict__ A, long long lda, const bf16_t* __restrict__ W, long long ldw,
     bf16_t* C, long long ldc, int M, int N, int K, Epi ep, int ntm, int ntn, int nmain, int ksplit,
-    int piece_k, float* __restrict__ part, int npers, int tiles_per) {
+    int piece_k, float* __restrict__ part, W4Sched sc) {
 #if defined(__HIP_DEVICE_COMPILE__)     // (the AGPR asm operands are not host constraints)
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const W4Work wk = w4_work(K, nmain, ksplit, piece_k, npers, tiles_per, 64, ep.rounds);
-    if (wk.ntw <= 0) return;            // (an empty round: nothing issued yet)
+    const W4Work wk = w4_work(sc, K, nmain, ksplit, piece_k, 64);
     const int nt = wk.nt;
-    desync_start(ep);
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1038,11 +1001,12 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     // is written in the MFMA gap before the load -- no address VALU and no s_nop per DMA (r4: the
     // per-DMA v_add + hazard nop were 2 of the 4 instructions of every DMA group).  Rows past the
     // matrix fall outside the resource's range and load 0; their outputs are discarded.  The DMA
-    // cursor (tile dk, K-tile dkt) runs two K-tiles ahead of the compute; past the block's last
-    // K-tile it re-reads that K-tile (into the buffer no later read uses), which keeps every
-    // iteration's wait counts identical.  The DMAs are inline asm, invisible to the compiler's wait
-    // counting (its own waits only grow stricter with older loads in flight); the protocol waits are
-    // the hand-placed vmcnt below and the vmcnt(0) after each tile's epilogue.
+    // cursor (K-tile dkt of the tile it is in) runs two K-tiles ahead of the compute; past the
+    // block's last K-tile it re-reads that K-tile (into the buffer no later read uses), which keeps
+    // every iteration's wait counts identical.  The DMAs are inline asm, invisible to the compiler's
+    // wait counting (its own waits only grow stricter with older loads in flight); the protocol
+    // waits are the hand-placed vmcnt below (EPI_OPS: the epilogue's stores drain under the next
+    // tile's first K-tile) and the vmcnt(0) after the block's last tile.
     const unsigned ldab = (unsigned)(lda * 2), ldwb = (unsigned)(ldw * 2);
     auto rsrc4 = [](const char* base, int bytes) {      // (readfirstlane: an "s" operand)
         const unsigned long long a = (unsigned long long)(uintptr_t)base;
@@ -1065,27 +1029,34 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     const char* abp = nullptr;
     const char* wbp = nullptr;
     int arec = 0, wrec = 0;
-    auto dma_tile = [&](int k) {
+    auto dma_tile = [&](int id) {
         int tm, tn;
-        tile_of(wk.p0 + k * wk.pstep, ntm, ntn, ep.gm, tm, tn);
+        tile_of(id, ntm, ntn, ep.gm, tm, tn);
         const int m0 = tm * 256, n0 = tn * 256;
         abp = (const char*)(A + (long long)m0 * lda + wk.kb);
         wbp = (const char*)(W + (long long)n0 * ldw + wk.kb);
         arec = __builtin_amdgcn_readfirstlane(rows_bytes(M - m0, ldab));
         wrec = __builtin_amdgcn_readfirstlane(rows_bytes(N - n0, ldwb));
     };
-    int dk = 0, dkt = 0;
+    // tiles: cur (computing), nxt (the next one, read from the LDS word in cur's first K-tile) and
+    // dnext (where the DMA cursor goes when it leaves cur; -1: re-read)
+    int cur = wk.first, nxt = wk.second, dnext = wk.second;
+    int dkt = 0;
     auto dma_advance = [&]() {
         if (++dkt == nt) {
-            if (dk + 1 < wk.ntw) {
-                ++dk;
+            if (dnext >= 0) {
                 dkt = 0;
-                dma_tile(dk);
+                dma_tile(dnext);
+                dnext = -1;
             } else {
                 dkt = nt - 1;
             }
         }
     };
+    W4Grab grab(sc);
+    const unsigned slot = (unsigned)(uintptr_t)smem + W4_LDS;     // the next tile id (LDS word)
+    auto slot_ref = [&]() -> volatile LDS_AS int& { return *(volatile LDS_AS int*)(uintptr_t)slot; };
+    int slotv = 0;
     // LDS-DMA destinations (wave-uniform byte offsets of the wave's first row in the current
     // buffer) and the per-lane fragment bases; both toggle between the two buffers by XOR once per
     // K-tile, so the loop body is one instance with immediate ds_read offsets
@@ -1159,8 +1130,9 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     // instantiation issues: 32 16-B stores, + 32 residual loads (the split-K piece path: 64 stores).
     constexpr int EPI_OPS = (MODE == VS_EPI_GATE_RES || MODE == VS_EPI_RES) ? 64 : 32;
     // prologue: K-tiles 0 and 1 of the stream in flight (W then A each), then the k-step-0 fragments
-    dma_tile(0);
+    dma_tile(cur);
     ktile_rsrc(0);
+    if (tid == 0) slot_ref() = wk.second;     // read in the first tile's first K-tile
 #pragma unroll
     for (int d = 0; d < 16; ++d) dma_now(d);
     dma_advance();
@@ -1200,10 +1172,15 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
                 if constexpr (q < 16 && (q & 1)) fw1[q >> 1] = frag(wbase + 128 * (q >> 1) + 64);
                 if constexpr (q == 17) wbase ^= wtog;                          // next buffer's W fragments
                 if constexpr (q == 20) wait_lgkm_bar();                        // W region of this buffer free
+                if constexpr (FIRST && q == 21) slotv = slot_ref();           // the next tile (behind q 20)
                 if constexpr (q >= 23 && q <= 39 && (q - 23) % 4 == 0) fa1[(q - 23) / 4] = frag(abase + 128 * ((q - 23) / 4) + 64);
                 if constexpr (q >= 41 && q <= 45 && (q & 1)) fa1[5 + (q - 41) / 2] = frag(abase + 128 * (5 + (q - 41) / 2) + 64);
                 if constexpr (q == 47) abase ^= atog;
                 if constexpr (q == 52) wait_lgkm_bar();                        // A region of this buffer free
+                if constexpr (FIRST && q == 53) {
+                    nxt = __builtin_amdgcn_readfirstlane(slotv);
+                    dnext = nxt;
+                }
                 if constexpr (q == 69) {                                       // W of the next K-tile landed
                     fence();
                     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(W69) : "memory");
@@ -1239,7 +1216,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     };
 
 #pragma nounroll
-    for (int k = 0; k < wk.ntw; ++k) {
+    for (;;) {
         ktile(std::true_type{});
 #pragma nounroll
         for (int t = 1; t < nt; ++t) ktile(std::false_type{});
@@ -1248,16 +1225,17 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
         asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
 
         int tm, tn;
-        tile_of(wk.p0 + k * wk.pstep, ntm, ntn, ep.gm, tm, tn);
+        tile_of(cur, ntm, ntn, ep.gm, tm, tn);
         const int m0 = tm * 256, n0 = tn * 256;
+        // the tile after nxt: wave 0's queue atomic goes out under this epilogue
+        if (nxt >= 0 && wave == 0) grab.issue();
         // output: acc[i][j][e] = C[m][n], m = m0 + 128 wm + 16 i + (lane & 15), n = n0 + 128 wn + 16 j + 4 (lane >> 4) + e
-#ifndef W4_DIAG_NOEPI
         if (wk.piece >= 0) {
             // fp32 partial tile through one buffer resource: a per-lane offset, the row block i in
             // soffset and the column block j in the immediate (64 precomputed 64-bit addresses,
             // hoisted out of the tile loop by the compiler, were spilled)
             const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-                part + ((long long)(wk.p0 - nmain) * ksplit + wk.piece) * 256 * 256, 0, 256 * 256 * 4, 0x00020000);
+                part + ((long long)(cur - nmain) * ksplit + wk.piece) * 256 * 256, 0, 256 * 256 * 4, 0x00020000);
             const int vo = ((128 * wm + (lane & 15)) * 256 + 128 * wn + 4 * (lane >> 4)) * 4;
 #pragma unroll
             for (int i = 0; i < 8; ++i)
@@ -1273,31 +1251,24 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
             // odd-g lane with 32p + 16 + 4(g-1) .. +7; loads issued ahead (tile_epilogue_w4).  One
             // epilogue mode per kernel instantiation (the runtime switch's six bodies beside the
             // 256 live accumulators overflowed the register file)
-#ifdef W4_NARROW
-            tile_epilogue_w4n<MODE, HINT, false>(acc, m0 + 128 * wm, n0 + 128 * wn, lane, C, ldc, M, N, ep, nullptr);
-#else
-            tile_epilogue_w4<MODE, HINT, false>(acc, m0 + 128 * wm, n0 + 128 * wn, lane, C, ldc, M, N, ep, nullptr);
-#endif
-        }
-#else
-        if (W4_DIAG_NOEPI == 1 && wk.piece >= 0) {
-            float* pp = part + ((long long)(wk.p0 - nmain) * ksplit + wk.piece) * 256 * 256;
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    *reinterpret_cast<f32x4_t*>(pp + (128 * wm + 16 * i + (lane & 15)) * 256 + 128 * wn + 16 * j +
-                                                4 * (lane >> 4)) = acc[i][j];
-        } else if (W4_DIAG_NOEPI == 2) {
             tile_epilogue_w4<MODE, HINT, false>(acc, m0 + 128 * wm, n0 + 128 * wn, lane, C, ldc, M, N, ep, nullptr);
         }
-#endif
+        if (nxt < 0) break;
+        // the id of the tile after nxt into the LDS word (read in nxt's first K-tile, behind its
+        // q = 20 barrier; the readers of the previous id passed this K-tile's q = 52 barrier long ago)
+        if (wave == 0) {
+            const int id = grab.finish<(EPI_OPS < 63 ? EPI_OPS : 63)>(lane);   // (>= EPI_OPS issued since)
+            if (lane == 0) slot_ref() = id;
+        }
+        cur = nxt;
         // the next tile's k-step-0 fragments (its first K-tile has landed); the epilogue's stores stay
-        // in flight (EPI_OPS above) -- after the last tile everything drains, the re-read DMAs into
-        // LDS included, before the workgroup's LDS is released
-        if (k + 1 < wk.ntw) read_k0();
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // in flight (EPI_OPS above)
+        read_k0();
     }
+    // after the last tile everything drains, the re-read DMAs into LDS included, before the
+    // workgroup's LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    grab.done(tid);
 #endif
 }
 
@@ -1556,13 +1527,12 @@ template <bool WIDE, int MODE, bool HINT>      // MODE / HINT: the 16-B epilogue
 __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
     const uint8_t* __restrict__ A, long long lda, const float* __restrict__ scale_a, const uint8_t* __restrict__ W,
     long long ldw, bf16_t* C, long long ldc, int M, int N, int K, Epi ep, int ntm, int ntn, int nmain, int ksplit,
-    int piece_k, float* __restrict__ part, int npers, int tiles_per) {
+    int piece_k, float* __restrict__ part, W4Sched sc) {
 #if defined(__HIP_DEVICE_COMPILE__)     // (the AGPR asm operands are not host constraints)
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    // r4: persistent as gemm_bf16_tn_4w (w4_work: one workgroup per CU over its XCD's tile range,
-    // the DMA cursor running across tile boundaries, split pieces after)
-    const W4Work wk = w4_work(K, nmain, ksplit, piece_k, npers, tiles_per, 128, ep.rounds);
-    if (wk.ntw <= 0) return;            // (an empty round: nothing issued yet)
+    // persistent as gemm_bf16_tn_4w (w4_work / W4Grab: one workgroup per CU fed by its XCD's tile
+    // queue, the DMA cursor running across tile boundaries, split pieces after)
+    const W4Work wk = w4_work(sc, K, nmain, ksplit, piece_k, 128);
     const int nt = wk.nt;
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1594,25 +1564,32 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
         asm volatile("" : "+v"(voa[j]), "+v"(vow[j]));     // kept, not re-formed per use
     }
     i32x4_t ra, rw;
-    auto dma_tile = [&](int k) {
+    auto dma_tile = [&](int id) {
         int tm, tn;
-        tile_of(wk.p0 + k * wk.pstep, ntm, ntn, ep.gm, tm, tn);
+        tile_of(id, ntm, ntn, ep.gm, tm, tn);
         const int m0 = tm * 256, n0 = tn * 256;
         ra = rsrc4(A + (long long)m0 * lda + wk.kb, (int)((long long)max(0, min(M - m0, 256)) * lda));
         rw = rsrc4(W + (long long)n0 * ldw + wk.kb, (int)((long long)max(0, min(N - n0, 256)) * ldw));
     };
-    int dk = 0, dkt = 0;
+    // tiles: cur (computing), nxt (the next one, from the LDS word in cur's first K-tile), dnext
+    // (where the DMA cursor goes when it leaves cur; -1: re-read), as in gemm_bf16_tn_4w
+    int cur = wk.first, nxt = wk.second, dnext = wk.second;
+    int dkt = 0;
     auto dma_advance = [&]() {
         if (++dkt == nt) {
-            if (dk + 1 < wk.ntw) {
-                ++dk;
+            if (dnext >= 0) {
                 dkt = 0;
-                dma_tile(dk);
+                dma_tile(dnext);
+                dnext = -1;
             } else {
                 dkt = nt - 1;           // past the block's last K-tile: re-read it (unused buffer)
             }
         }
     };
+    W4Grab grab(sc);
+    const unsigned slot = (unsigned)(uintptr_t)smem + F4_LDS;     // the next tile id (LDS word)
+    auto slot_ref = [&]() -> volatile LDS_AS int& { return *(volatile LDS_AS int*)(uintptr_t)slot; };
+    int slotv = 0;
     unsigned dw = 2 * F4_OPB + wave * F4_ROWB, da = wave * F4_ROWB;
     const unsigned dw_tog = dw ^ (dw + F4_OPB), da_tog = da ^ (da + F4_OPB);
     const unsigned lds0 = (unsigned)(uintptr_t)smem;
@@ -1672,7 +1649,8 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
     };
 
     // prologue: K-tiles 0 and 1 of the stream in flight, then the early fragments of K-tile 0
-    dma_tile(0);
+    dma_tile(cur);
+    if (tid == 0) slot_ref() = wk.second;     // read in the first tile's first K-tile
 #pragma unroll
     for (int d = 0; d < 16; ++d) dma_now(0u, d);
     dma_advance();
@@ -1717,10 +1695,15 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
                 fence();
             }
             if constexpr (q >= 11 && q <= 56 && (q - 11) % 3 == 0) dma_go(ko, (q - 11) / 3);
+            if constexpr (FIRST && q == 11) slotv = slot_ref();           // the next tile (behind q 10)
             if constexpr (q == 29) {                                                 // next K-tile landed
                 fence();
                 asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
                 bar();
+            }
+            if constexpr (FIRST && q == 30) {
+                nxt = __builtin_amdgcn_readfirstlane(slotv);
+                dnext = nxt;
             }
             if constexpr (q >= 32 && q <= 35) fa[q - 32] = frag(a0, a1, 128 * (q - 32));
             if constexpr (q >= 36 && q <= 60 && (q - 36) % 4 == 0) fw[(q - 36) / 4] = frag(w0, w1, 128 * ((q - 36) / 4));
@@ -1742,19 +1725,20 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
     };
 
 #pragma nounroll
-    for (int k = 0; k < wk.ntw; ++k) {
+    for (;;) {
         ktile(std::true_type{});
 #pragma nounroll
         for (int t = 1; t < nt; ++t) ktile(std::false_type{});
         // the accumulators leave through v_accvgpr_read (acc_rd): cover the last MFMAs' write latency
         asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
         int tm, tn;
-        tile_of(wk.p0 + k * wk.pstep, ntm, ntn, ep.gm, tm, tn);
+        tile_of(cur, ntm, ntn, ep.gm, tm, tn);
         const int m0 = tm * 256, n0 = tn * 256;
+        if (nxt >= 0 && wave == 0) grab.issue();            // the tile after nxt, under the epilogue
         // acc[i][j][e] = D[n][m]: m = m0 + 128 wm + 16 i + (lane & 15), n = n0 + 128 wn + 16 j + 4 (lane >> 4) + e
         if (wk.piece >= 0) {
             const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-                part + ((long long)(wk.p0 - nmain) * ksplit + wk.piece) * 256 * 256, 0, 256 * 256 * 4, 0x00020000);
+                part + ((long long)(cur - nmain) * ksplit + wk.piece) * 256 * 256, 0, 256 * 256 * 4, 0x00020000);
             const int vo = ((128 * wm + (lane & 15)) * 256 + 128 * wn + 4 * (lane >> 4)) * 4;
 #pragma unroll
             for (int i = 0; i < 8; ++i)
@@ -1780,11 +1764,17 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
                 }
             }
         }
-        // the epilogue's loads and stores leave the counted DMA waits of the next tile exact; then
-        // the next tile's early fragments (its first K-tile has landed: the last K-tile's q = 29 wait)
+        // the epilogue's loads and stores leave the counted DMA waits of the next tile exact
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (k + 1 < wk.ntw) read_early();
+        if (nxt < 0) break;
+        if (wave == 0) {                // the id of the tile after nxt into the LDS word
+            const int id = grab.finish<0>(lane);
+            if (lane == 0) slot_ref() = id;
+        }
+        cur = nxt;
+        read_early();   // the next tile's early fragments (its first K-tile landed: the last q = 29 wait)
     }
+    grab.done(tid);
 #endif
 }
 
@@ -1964,15 +1954,24 @@ static bool use_4w() {
     return !(e && e[0] == '8');
 }
 
-// persistent rounds of the 4-wave kernels (w4_work): VS_GEMM_ROUNDS (default 1), at most one per
-// tile of a workgroup's list and no empty round
-static int w4_rounds(int tiles_per) {
-    if (tiles_per <= 1) return 1;
-    const char* e = getenv("VS_GEMM_ROUNDS");
-    const int want = e && atoi(e) > 0 ? atoi(e) : 1;
-    const int r = min(want, tiles_per);
-    const int L = (tiles_per + r - 1) / r;
-    return (tiles_per + L - 1) / L;
+// the schedule of a 4-wave launch (W4Sched): one persistent block per CU when the main tiles fill
+// every CU and a tile has >= 3 K-tiles (the tile-id hand-off, see the schedule's comment), fed by the
+// XCD tile queues when the stream has a queue workspace (kind 5) bound (VS_GEMM_QUEUE=0: the static
+// lists, A/B)
+static W4Sched w4_sched(int nmain, int nt, hipStream_t stream) {
+    W4Sched s{nullptr, 0, 0, 0};
+    const int cus = vs_cus_for_split(nullptr);
+    if (cus >= 8 && cus % 8 == 0 && nmain >= cus && nt >= 3) {
+        s.npers = cus;
+        s.tp = nmain / cus;
+    }
+    s.nrem = nmain - s.npers * s.tp;
+    const char* e = getenv("VS_GEMM_QUEUE");
+    if (s.npers && s.tp >= 2 && !(e && e[0] == '0')) s.q = (unsigned*)vs_split_workspace(5, WQ_BYTES, stream);
+    return s;
+}
+static unsigned w4_grid(const W4Sched& s, const KSplit& sp) {
+    return (unsigned)(s.npers + (s.q ? 0 : s.nrem) + sp.ntail * sp.ksplit);
 }
 
 static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n) {
@@ -1982,11 +1981,7 @@ static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n)
     ep.rows_per_batch = m;
     ep.alpha = 1.f;
     ep.hint_scale = 1.f;
-    const char* ds = getenv("VS_GEMM_DESYNC");
-    ep.desync = ds ? atoi(ds) : 0;
-    const char* gm = getenv("VS_GEMM_GM");
-    ep.gm = gm && atoi(gm) > 0 ? atoi(gm) : VS_GEMM_GM;
-    ep.rounds = 1;
+    ep.gm = VS_GEMM_GM;
     if (epi) {
         ep.bias = (const bf16_t*)epi->bias;
         ep.res = (const bf16_t*)epi->residual;
@@ -2067,7 +2062,7 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
         }
         if (k2 == 0 && wide && use_4w()) {
             using K4 = void (*)(const bf16_t*, long long, const bf16_t*, long long, bf16_t*, long long, int, int, int,
-                                Epi, int, int, int, int, int, float*, int, int);
+                                Epi, int, int, int, int, int, float*, W4Sched);
             // (a static table's constant initializer left the kernels' host stubs un-instantiated)
             const K4 kern4[6] = {gemm_bf16_tn_4w<VS_EPI_BIAS, false>, gemm_bf16_tn_4w<VS_EPI_GELU, false>,
                                         gemm_bf16_tn_4w<VS_EPI_SILU, false>, gemm_bf16_tn_4w<VS_EPI_GATE_RES, false>,
@@ -2075,19 +2070,14 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
             static bool attr4 = false;
             if (!attr4) {
                 for (const K4 f : kern4)
-                    (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS);
+                    (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS + 16);
                 attr4 = true;
             }
             const K4 kf = kern4[(ep.mode == VS_EPI_GATE_RES && ep.hint) ? 5 : ep.mode];
-            // persistent blocks (one per CU) over the first floor(nmain / CUs) * CUs tiles
-            const int cus = vs_cus_for_split(nullptr);
-            const int npers = (cus >= 8 && cus % 8 == 0 && sp.nmain >= cus && !getenv("VS_GEMM_NO_PERSIST")) ? cus : 0;
-            const int tiles_per = npers ? sp.nmain / npers : 0;
-            ep.rounds = w4_rounds(tiles_per);
-            const unsigned grid = (unsigned)(npers * ep.rounds + (sp.nmain - npers * tiles_per) + sp.ntail * sp.ksplit);
-            hipLaunchKernelGGL(kf, dim3(grid), dim3(256), W4_LDS,
+            const W4Sched sc = w4_sched(sp.nmain, k / 64, (hipStream_t)stream);
+            hipLaunchKernelGGL(kf, dim3(w4_grid(sc, sp)), dim3(256), W4_LDS + 16,
                                (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw, (bf16_t*)c, ldc, m,
-                               n, k, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part, npers, tiles_per);
+                               n, k, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part, sc);
             VS_CHECK_LAUNCH();
         } else {
         hipLaunchKernelGGL(k2 ? (wide ? gemm_bf16_tn_8p<true, true> : gemm_bf16_tn_8p<true, false>)
@@ -2170,7 +2160,7 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
     const char* fk = getenv("VS_GEMM_KERNEL");      // the 4-wave kernel unless VS_GEMM_KERNEL=8p
     if (!(fk && fk[0] == '8')) {
         using KF4 = void (*)(const uint8_t*, long long, const float*, const uint8_t*, long long, bf16_t*, long long,
-                             int, int, int, Epi, int, int, int, int, int, float*, int, int);
+                             int, int, int, Epi, int, int, int, int, int, float*, W4Sched);
         // one instantiation per 16-B epilogue mode (index: mode, 5 = gate-residual + hint), 6: 8-B path
         const KF4 kf4[7] = {gemm_fp8_tn_4w<true, VS_EPI_BIAS, false>, gemm_fp8_tn_4w<true, VS_EPI_GELU, false>,
                             gemm_fp8_tn_4w<true, VS_EPI_SILU, false>, gemm_fp8_tn_4w<true, VS_EPI_GATE_RES, false>,
@@ -2179,23 +2169,19 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
         static bool attr4 = false;
         if (!attr4) {
             for (const KF4 f : kf4)
-                (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, F4_LDS);
+                (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, F4_LDS + 16);
             attr4 = true;
         }
         const bool wide = n % 8 == 0 && ldc % 8 == 0 && aligned16(c) && (!ep.bias || aligned16(ep.bias)) &&
                           (!ep.res || (ep.ld_res % 8 == 0 && aligned16(ep.res))) &&
                           (!ep.gate || (ep.gate_bstride % 8 == 0 && aligned16(ep.gate))) &&
                           (!ep.hint || (ep.ld_hint % 8 == 0 && aligned16(ep.hint)));
-        // persistent blocks (one per CU) over the first floor(nmain / CUs) * CUs tiles, as the bf16 kernel
-        const int cus = vs_cus_for_split(nullptr);
-        const int npers = (cus >= 8 && cus % 8 == 0 && sp.nmain >= cus && !getenv("VS_GEMM_NO_PERSIST")) ? cus : 0;
-        const int tiles_per = npers ? sp.nmain / npers : 0;
-        ep.rounds = w4_rounds(tiles_per);
-        const unsigned grid = (unsigned)(npers * ep.rounds + (sp.nmain - npers * tiles_per) + sp.ntail * sp.ksplit);
+        // persistent blocks fed by the XCD tile queues, as the bf16 kernel (w4_sched)
+        const W4Sched sc = w4_sched(sp.nmain, k / 128, (hipStream_t)stream);
         const KF4 kf = kf4[!wide ? 6 : (ep.mode == VS_EPI_GATE_RES && ep.hint) ? 5 : ep.mode];
-        hipLaunchKernelGGL(kf, dim3(grid), dim3(256), F4_LDS,
+        hipLaunchKernelGGL(kf, dim3(w4_grid(sc, sp)), dim3(256), F4_LDS + 16,
                            (hipStream_t)stream, (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c,
-                           ldc, m, n, k, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part, npers, tiles_per);
+                           ldc, m, n, k, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part, sc);
     } else
     hipLaunchKernelGGL(gemm_fp8_tn_8p, dim3((unsigned)(sp.nmain + sp.ntail * sp.ksplit)), dim3(512), LDS8,
                        (hipStream_t)stream, (const uint8_t*)a8, lda, scale_a, (const uint8_t*)w8, ldw, (bf16_t*)c,

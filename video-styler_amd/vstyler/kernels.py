@@ -23,7 +23,7 @@ _SPLIT_WS = {}
 
 def _split_ws(kind, t, nbytes=None):
     """Bind library scratch of `kind` (0 attention split tail, 1 GEMM split tail, 2 hipBLASLt
-    workspace, 3 epilogue staging of `nbytes`, 4 attention item flags) for the current stream of t's device from the torch
+    workspace, 3 epilogue staging of `nbytes`, 4 attention item flags, 5 GEMM tile queues) for the current stream of t's device from the torch
     allocator (vs_split_workspace_bind: the library never allocates).  Re-bound larger when a
     bigger one is needed; never inside a graph capture (the library then takes its fallback)."""
     stream = _stream(t)
@@ -37,8 +37,9 @@ def _split_ws(kind, t, nbytes=None):
         return
     if torch.cuda.is_current_stream_capturing():
         return
-    # kind 4 (attention item flags) must be zero when bound; the library keeps it zero
-    buf = (torch.zeros if kind == 4 else torch.empty)(nbytes, dtype=torch.uint8, device=t.device)
+    # kinds 4 (attention item flags) and 5 (GEMM tile queues) must be zero when bound; the library
+    # keeps them zero
+    buf = (torch.zeros if kind in (4, 5) else torch.empty)(nbytes, dtype=torch.uint8, device=t.device)
     _lib.check(_lib.load().vs_split_workspace_bind(kind, buf.data_ptr(), nbytes, stream))
     _SPLIT_WS[key] = buf
 
@@ -107,6 +108,7 @@ def gemm(a, w, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, g
     if k2 == 0:
         _split_ws(1, a)
         _split_ws(2, a)
+        _split_ws(5, a)
         if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES) and _lt_route(M, N, K, epilogue):
             _split_ws(3, a, M * N * 2)       # staging for the hipBLASLt route (vs_gemm decides)
     _lib.check(_lib.load().vs_gemm(a.data_ptr(), lda, w.data_ptr(), ldw, out.data_ptr(), ldc, M, N, K,
@@ -147,6 +149,7 @@ def gemm_fp8(a8, scale_a, w8, out, epilogue=VS_EPI_BIAS, bias=None, residual=Non
         raise ValueError(f"gemm_fp8 shape mismatch a8={tuple(a8.shape)} w8={tuple(w8.shape)} out={tuple(out.shape)}")
     ep = _epilogue(bias, residual, gate, gate_bstride, hint, hint_scale, alpha, rows_per_batch)
     _split_ws(1, a8)                                                    # split tail of the MFMA kernel
+    _split_ws(5, a8)                                                    # its tile queues
     if not os.environ.get("VS_FP8_BACKEND", "").startswith("v"):   # hipBLASLt route (vs_gemm_fp8's own test)
         _split_ws(2, a8)
         if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES):

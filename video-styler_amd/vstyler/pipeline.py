@@ -287,11 +287,16 @@ class DenoiseStepper:
     def capture(self):
         g = torch.cuda.CUDAGraph()
         err = None
-        try:
-            with torch.cuda.graph(g, stream=self.stream):
-                self._run()
-        except Exception as e:      # e.g. a collective backend that cannot be captured: stay eager
-            err = e
+        from .usp import unbound_side_comms
+        stray = unbound_side_comms(self.stream)
+        if stray:                   # RCCL forked into the capture from a side stream: never capture
+            err = RuntimeError(f"{len(stray)} side-stream communicator(s) not bound to the capture stream")
+        else:
+            try:
+                with torch.cuda.graph(g, stream=self.stream):
+                    self._run()
+            except Exception as e:      # e.g. a collective backend that cannot be captured: stay eager
+                err = e
         # the decision is collective: with several ranks replaying graphs whose collectives must
         # pair up, one rank falling back to eager steps while the others replay would deadlock or
         # mismatch, so every rank keeps its graph only if every rank captured one

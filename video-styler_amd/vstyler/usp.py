@@ -11,6 +11,7 @@ carries the output back; layout transforms are the vs_ulysses_permute kernel.  R
 S % p == 0 and heads % p == 0 (asserted instead of the reference's silent zero padding).
 """
 import ctypes
+import weakref
 import os
 
 import torch
@@ -117,10 +118,15 @@ class NativeComm:
         if stream not in ("caller", "side"):
             raise ValueError(f"VSTYLER_SP_COMM_STREAM must be 'caller' or 'side', not {stream!r}")
         self.stream = None if stream == "caller" else torch.cuda.Stream()
+        NativeComm._live.add(self)
+
+    _live = weakref.WeakSet()           # every communicator of the process (unbound_side_comms)
 
     @property
     def capturable(self):
-        """On the caller's stream, or on a side stream the step's capture binds to its origin."""
+        """On the caller's stream, or on a side stream the step's capture binds to its origin --
+        DenoiseStepper.capture refuses to capture while any live side-stream communicator is not
+        bound to the capture stream (unbound_side_comms), whatever plan attribute holds it."""
         return True
 
     def bind_stream(self, stream):
@@ -333,6 +339,13 @@ class UlyssesGroup:
 
 
 _WS_BY_DEV = {}
+
+
+def unbound_side_comms(stream):
+    """The live side-stream NativeComm objects whose collectives would NOT run on `stream` (a graph
+    capture's origin): RCCL forked into a capture from any other stream segfaulted in
+    hipStreamEndCapture (NativeComm's comment), so a capture must see this list empty."""
+    return [c for c in list(NativeComm._live) if c.stream is not None and c.stream != stream]
 
 
 def plan_native_comms(plan):
