@@ -29,6 +29,28 @@ extern "C" {
 const char* vs_strerror(int code);
 int vs_abi_version(void);
 
+/*
+ * Path-selection options.  The library reads no environment variable: every launch takes its
+ * kernel / schedule from this process-wide table, whose defaults are the product configuration.
+ * Tests and A/B probes select the alternate paths (each bit-identical or within its stated tolerance
+ * of the default) through vs_set_option, which returns the previous value (-VS_E_INVALID for an
+ * unknown id or value).  Not for concurrent use with launches that depend on the changed option.
+ */
+#define VS_OPT_GEMM_TILE 0     /* 0 auto (default); 128 / 256: force the 128x128 / 256x256 schedule   */
+#define VS_OPT_GEMM_KERNEL 1   /* 4: the 4-wave 256x256 kernels (default); 8: the 8-phase ones         */
+#define VS_OPT_GEMM_SPLIT 2    /* 1: split tails (default); 0: whole-tile grids                        */
+#define VS_OPT_GEMM_QUEUE 3    /* 1: XCD tile queues (default; needs a kind-5 workspace); 0: static lists */
+#define VS_OPT_ATTN_IMPL 4     /* 0: auto (default: 4-wave for >= 16 key tiles); 4 / 8 force a kernel  */
+#define VS_OPT_ATTN_MFMA 5     /* 16 (default) / 32: the 8-wave kernel's MFMA shape                     */
+#define VS_OPT_ATTN_NC 6       /* 1: optimistic softmax + checked redo (default); 0: checked only       */
+#define VS_OPT_ATTN_SPLIT 7    /* 1: split tails (default); 0: whole-item grids                        */
+#define VS_OPT_ATTN_PERSIST 8  /* 1: persistent item walk (default); 0: one block per item             */
+#define VS_OPT_VAE_PXB 9       /* 2 (default) / 1: 128-pixel blocks per wave of the VAE conv            */
+#define VS_OPT_VAE_PRE 10      /* 3 (default) / 2 / 1: register stages of the VAE conv's gathers        */
+#define VS_OPT_COUNT 11
+int vs_set_option(int id, int value);
+int vs_get_option(int id);
+
 /* Epilogue selector for vs_gemm (fp32 accumulator -> bf16, rounding points of the reference). */
 #define VS_EPI_BIAS 0      /* y = bf16(acc + bias)                                           */
 #define VS_EPI_GELU 1      /* bf16(gelu_tanh(y))            : nn.GELU(approximate='tanh')      */
@@ -56,14 +78,11 @@ typedef struct vs_epilogue {
  * (diffsynth/vram_management/layers.py:173-188) incl. the un-merged LoRA term out + x A^T B^T
  * (layers.py:180-182): pass A2 = alpha * x A^T (computed by a previous vs_gemm) and W2 = B.
  * K and K2 must be multiples of 64, lda/ldw/lda2/ldw2 multiples of 8, N a multiple of 4.
- * Execution: grids of >= 1024 256x256 tiles (or >= 256 with K <= 8192) without a LoRA phase run
- * bf16(A W^T + bias) on hipBLASLt (needs a kind-2 workspace bound on the stream; the heuristic's
- * first algorithm for the shape, deterministic) and finish the epilogue with the same code as the
- * fused kernels (gate-residual / residual stage y in a kind-3 buffer of M*N*2 bytes); otherwise, or
- * when those are not bound, the MFMA kernels (with the kind-1 split tail).  Every route keeps the
- * reference's rounding points and differs only in fp32 summation order -- except the opt-in
- * VS_LT_GELU=1, which runs GELU on hipBLASLt's GELU_BIAS epilogue (the GELU of the fp32 acc + bias,
- * one rounding, instead of the reference's bf16 linear output followed by the GELU).
+ * Execution: every GEMM runs on the hand-written MFMA kernels: grids of >= 240 256x256 tiles with
+ * K >= 1024 on the 256x256 schedule (the persistent 4-wave kernel fed by XCD tile queues when a
+ * kind-5 workspace is bound; with the kind-1 split tail), the un-merged LoRA second phase on the
+ * 8-phase 256x256 kernel, everything else on the 128x128 kernel (vs_set_option overrides).  Every
+ * path keeps the reference's rounding points and differs only in fp32 summation order.
  */
 int vs_gemm(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc,
             int m, int n, int k, int epilogue, const vs_epilogue* epi,
@@ -77,16 +96,13 @@ int vs_gemm(const void* a, long long lda, const void* w, long long ldw, void* c,
 int vs_gemm_split_plan(int m, int n, int k, int cus, int* out);
 
 /*
- * 1 when vs_gemm would send an (m, n, k) GEMM without a LoRA phase to hipBLASLt (so a binding knows
- * to bind the kind-3 staging buffer for its gate-residual / residual epilogues), 0 for the MFMA
- * kernels, VS_E_INVALID for non-positive sizes.  Honours VS_GEMM_BACKEND.  Host-only.
+ * The route vs_gemm (fp8 = 0) / vs_gemm_fp8 (fp8 = 1) takes for an (m, n, k) GEMM with epilogue
+ * `epilogue`: 0 = the MFMA kernels with the epilogue fused -- the only route of this build (r5: the
+ * vendor-library route and its separate epilogue pass are gone) -- or -VS_E_INVALID for non-positive
+ * sizes or an unknown epilogue.  vs_gemm_route(m, n, k) = vs_gemm_route_epi(m, n, k, VS_EPI_BIAS, 0).
+ * Host-only.  (A binding fuses a residual epilogue with the next LayerNorm only on a route != 0.)
  */
 int vs_gemm_route(int m, int n, int k);
-/* the same for a GEMM with epilogue `epilogue` (VS_EPI_*), bf16 (fp8 = 0, vs_gemm) or fp8 (fp8 = 1,
- * vs_gemm_fp8): 1 = hipBLASLt + a separate epilogue pass, 0 = the MFMA kernel's fused epilogue
- * (the host fuses a residual epilogue with the next LayerNorm only on the former route),
- * -VS_E_INVALID for non-positive sizes or an unknown epilogue (negative: never a route).  Honours
- * VS_GEMM_BACKEND / VS_GEMM_OWN / VS_GEMM_KERNEL (bf16) and VS_FP8_BACKEND (fp8).  Host-only. */
 int vs_gemm_route_epi(int m, int n, int k, int epilogue, int fp8);
 
 /*
@@ -127,27 +143,18 @@ int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
 int vs_attn_split_plan(int batch, int sq, int skv, int heads, int cus, int* out);
 
 /*
- * Library scratch (kind 0: vs_attn_fwd split tail, 1: vs_gemm split tail, 2: vs_gemm's hipBLASLt
- * workspace, 3: vs_gemm epilogue staging, M*N*2 bytes of the largest staged GEMM, 4: vs_attn_fwd
+ * Library scratch (kind 0: vs_attn_fwd split tail, 1: vs_gemm split tail, 2 and 3: unused by this
+ * build (vs_split_workspace_bytes 0; were the vendor-library route's workspace / staging), 4: vs_attn_fwd
  * item flags, one int per item, ZERO-FILLED by the caller when bound -- every launch leaves it zero;
  * 5: the tile queues of vs_gemm / vs_gemm_fp8's persistent 256x256 kernels, ZERO-FILLED when bound,
  * left zero by every launch -- without one those kernels walk static per-CU tile lists).
- * vs_split_workspace_bytes(kind) is the size that covers every plan of kinds 0-2, 4 and 5 (-1 for kind 3);
+ * vs_split_workspace_bytes(kind) is the size that covers every plan of kind 0, 1, 4 or 5 (0: not used);
  * vs_split_workspace_bind(kind, ptr, bytes, stream) registers a caller-owned
  * device buffer (16-B aligned) for launches of that kind on `stream` of the current device
  * (ptr = NULL unbinds).  The buffer must stay valid while bound, including in captured graphs.
  */
 long long vs_split_workspace_bytes(int kind);
 int vs_split_workspace_bind(int kind, void* ptr, long long bytes, void* stream);
-
-/*
- * The hipBLASLt build vs_gemm's library route runs on: the path of the copy opened by the library
- * (default: the private ROCm copy lt72/libvsblaslt7.so.1 next to libvstyler.so, made by
- * scripts/vendor_blaslt.py; VS_LT_LIB=<path> overrides), or "linked" when that failed (the reason is
- * printed to stderr once) and the link-time binding (in a torch process: torch's bundled hipBLASLt)
- * is used.
- */
-const char* vs_blaslt_library(void);
 
 /*
  * out = bf16(LN(x)) [affine: weight/bias] then, if shift/scale given, modulate:
@@ -161,11 +168,12 @@ int vs_layernorm_modulate(const void* x, long long ldx, void* out, long long ldo
 
 /*
  * x = epilogue(y, x) then out = vs_layernorm_modulate(x): the gate-residual / residual epilogue of a
- * projection whose bf16(A W^T + bias) was staged in y (vs_gemm's hipBLASLt route), fused with the
+ * projection whose bf16(A W^T + bias) was staged in y, fused with the
  * LayerNorm [+ affine] [+ modulate] that reads the updated row next (wan_video_dit.py:225-228).
  * epilogue: VS_EPI_GATE_RES (epi->gate, gate_bstride, rows_per_batch, optional hint) or VS_EPI_RES
  * (epi->alpha); epi->residual is ignored (x is the residual).  Same rounding points as vs_gemm's
- * epilogue followed by vs_layernorm_modulate: bit-identical to the two calls.
+ * epilogue followed by vs_layernorm_modulate: bit-identical to the two calls.  (Used with a GEMM route
+ * that stages its output, vs_gemm_route_epi != 0; none in this build.)
  */
 int vs_residual_layernorm(const void* y, long long ldy, void* x, long long ldx, void* out, long long ldo, int rows,
                           int dim, int epilogue, const vs_epilogue* epi, int rows_per_batch, const void* shift,

@@ -390,7 +390,7 @@ def dit_block_rows(x, ctx, t_mod, freqs, W, p, num_heads, rows, eps=1e-6):
     a = p + "self_attn."
     hr = h[:, rows]
     q = rope_apply(rms_norm(blk_linear(hr, W[a + "q.weight"], W[a + "q.bias"]), W[a + "norm_q.weight"], eps),
-                   freqs[rows], num_heads)
+                   freqs[rows.to(freqs.device)], num_heads)
     k = rope_apply(rms_norm(blk_linear(h, W[a + "k.weight"], W[a + "k.bias"]), W[a + "norm_k.weight"], eps),
                    freqs, num_heads)
     v = blk_linear(h, W[a + "v.weight"], W[a + "v.bias"])

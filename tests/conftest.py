@@ -26,6 +26,22 @@ def pytest_collection_modifyitems(config, items):
             item.add_marker(skip)
 
 
+@pytest.fixture
+def opt():
+    """opt(gemm_kernel=8, gemm_split=0, ...): libvstyler path-selection options (kernels.set_option,
+    include/vstyler.h VS_OPT_*) for one test, restored afterwards."""
+    from vstyler import kernels as K
+    saved = {}
+
+    def set_(**kw):
+        for k, v in kw.items():
+            prev = K.set_option(k, v)
+            saved.setdefault(k, prev)
+    yield set_
+    for k, v in saved.items():
+        K.set_option(k, v)
+
+
 _PROGRESS = {"fd": 2, "t0": None}
 
 

@@ -19,7 +19,7 @@ cases = [(name, kk, vv, skv, impl) for _ in range(2 if impls[0] is not None else
          for name, kk, vv, skv in (("self", k, v, S), ("cross", kc, vc, L))]
 for name, kk, vv, skv, impl in cases:
     if impl is not None:
-        os.environ["VS_ATTN_IMPL"] = impl
+        K.set_option("attn_impl", int(impl))
     fn = lambda: K.attention(q, kk, vv, o, H, B)
     fn(); torch.cuda.synchronize()
     ts = []

@@ -6,7 +6,6 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "video-st
 import torch
 from vstyler import kernels as K
 
-os.environ["VS_LT_GELU"] = "0"
 
 
 def timed(fn, reps=3):
@@ -19,7 +18,7 @@ def timed(fn, reps=3):
 
 SHAPES = (("qkv", 15360, 5120, K.VS_EPI_BIAS), ("o-proj", 5120, 5120, K.VS_EPI_GATE_RES),
           ("ffn-up", 13824, 5120, K.VS_EPI_GELU), ("ffn-down", 5120, 13824, K.VS_EPI_GATE_RES))
-VARIANTS = os.environ.get("AB_VARIANTS", "w4,w4s,lt").split(",")
+VARIANTS = os.environ.get("AB_VARIANTS", "w4,w4s").split(",")
 for M in [int(v) for v in sys.argv[1:]] or (59280,):
     for name, N, Kd, epi in SHAPES:
         g = torch.Generator(device="cuda").manual_seed(1)
@@ -36,10 +35,10 @@ for M in [int(v) for v in sys.argv[1:]] or (59280,):
             kw.update(residual=x, gate=gate, gate_bstride=N, rows_per_batch=(M + 1) // 2)
         out = x if epi == K.VS_EPI_GATE_RES else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         t = {v: [] for v in VARIANTS}
-        def setv(v):      # 8p = the 8-phase kernel, w4 / w4s = the 4-wave kernel (tile queues / static lists), lt = hipBLASLt fp8
-            os.environ["VS_FP8_BACKEND"] = "lt" if v == "lt" else "vstyler"
-            os.environ["VS_GEMM_KERNEL"] = "4w" if v.startswith("w4") else "8p"
-            os.environ["VS_GEMM_QUEUE"] = "0" if v == "w4s" else "1"
+        def setv(v):      # 8p = the 8-phase kernel, w4 / w4s = the 4-wave kernel (tile queues / static lists), lt = hipBLASLt fp8 (A/B build)
+            os.environ["VS_GEMM_BACKEND"] = "lt" if v == "lt" else "own"     # read by the A/B build only
+            K.set_option("gemm_kernel", 4 if v.startswith("w4") else 8)
+            K.set_option("gemm_queue", 0 if v == "w4s" else 1)
         for v in VARIANTS:
             setv(v)
             K.gemm_fp8(a8, sc, w8, out, **kw); torch.cuda.synchronize()
@@ -51,6 +50,4 @@ for M in [int(v) for v in sys.argv[1:]] or (59280,):
         print(f"fp8 M={M} {name:8s} N={N} K={Kd}: " +
               "  ".join(f"{v} {min(t[v]):.3f} ms ({fl / min(t[v]) / 1e9:.0f} TF/s)" for v in VARIANTS), flush=True)
         del a, w8, a8, sc, b, gate, x, out
-os.environ.pop("VS_FP8_BACKEND", None)
-os.environ.pop("VS_GEMM_KERNEL", None)
-os.environ.pop("VS_GEMM_QUEUE", None)
+os.environ.pop("VS_GEMM_BACKEND", None)

@@ -12,6 +12,7 @@ from bench import MODELS
 from vstyler import model_fn_wan_video
 from vstyler.models import VaceWanModel, WanModel, init_random_
 from vstyler.usp import UlyssesGroup, _Done
+from vstyler import kernels as K
 
 lib = ctypes.CDLL(os.path.join(os.path.dirname(__file__), "fakecomm", "libfakecomm.so"))
 lib.fake_comm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
@@ -76,7 +77,7 @@ for rnd in range(3):
         G, pz, ov, e = c
         if evar:
             os.environ[evar] = e
-        os.environ["VS_ATTN_NO_PERSIST"] = "0" if pz == "1" else "1"
+        K.set_option("attn_persist", 1 if pz == "1" else 0)
         sp = FakeCommUlysses(P, overlap=ov, nblocks=G)
         fn = lambda: model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=ctx, vace_context=vc,
                                         use_unified_sequence_parallel=True, sp_group=sp)

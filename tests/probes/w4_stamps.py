@@ -12,7 +12,8 @@ B, S, H = 2, 29640, 40
 g = torch.Generator(device="cuda").manual_seed(0)
 q, k, v = (torch.randn(B * S, H * 128, device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
 o = torch.empty_like(q)
-os.environ["VS_ATTN_IMPL"] = "4"
+from vstyler import kernels as _K
+_K.set_option("attn_impl", 4)
 for _ in range(3):
     K.attention(q, k, v, o, H, B)
 torch.cuda.synchronize()

@@ -43,15 +43,10 @@ def test_invalid_arguments_rejected_before_launch():
     # null pointers
     assert lib.vs_gemm(None, 64, None, 64, None, 64, 8, 8, 64, 0, ep, None, 0, None, 0, 0, None) == 1
     fake = 1 << 20   # aligned non-null (never dereferenced: validation fails first)
-    # fp8: K must be a multiple of 128 on every backend (K = 192 rejected up front, whichever route
-    # VS_FP8_BACKEND selects), and 256 passes validation only to fail on the null scale vector
-    for backend in ("lt", "vstyler"):
-        os.environ["VS_FP8_BACKEND"] = backend
-        try:
-            assert lib.vs_gemm_fp8(fake, 192, fake, fake, 192, fake, 8, 8, 8, 192, 0, ep, None) == 1
-            assert lib.vs_gemm_fp8(fake, 256, None, fake, 256, fake, 8, 8, 8, 256, 0, ep, None) == 1
-        finally:
-            del os.environ["VS_FP8_BACKEND"]
+    # fp8: K must be a multiple of 128 (the MFMA kernel's K-tile; K = 192 rejected up front), and 256
+    # passes validation only to fail on the null scale vector
+    assert lib.vs_gemm_fp8(fake, 192, fake, fake, 192, fake, 8, 8, 8, 192, 0, ep, None) == 1
+    assert lib.vs_gemm_fp8(fake, 256, None, fake, 256, fake, 8, 8, 8, 256, 0, ep, None) == 1
     # K not a multiple of 64
     assert lib.vs_gemm(fake, 48, fake, 48, fake, 8, 8, 8, 48, 0, ep, None, 0, None, 0, 0, None) == 1
     # bad epilogue id
@@ -155,55 +150,41 @@ def test_gemm_split_plan_host_only():
     assert lib.vs_gemm_split_plan(64, 64, 100, 256, out) == 1
 
 
-def test_gemm_route_rule(monkeypatch):
-    """vs_gemm_route: hipBLASLt for grids of >= 1024 256x256 tiles, or >= 256 tiles with K <= 8192,
-    or smaller grids with N >= 2048 and 1024 <= K <= 8192 (gemm.hip lt_route, measured in
-    profiles/r1/gemm_backend_ab_r1j.log and gemm_backend_ab_ctx_r1s.log), except the FFN shapes where
-    the staggered MFMA kernel measured faster (r3); VS_GEMM_BACKEND forces."""
+def test_gemm_route_is_fused_everywhere():
+    """r5: every GEMM of the product library runs on the MFMA kernels with its epilogue fused
+    (gemm.hip 'Routing (r5)'): vs_gemm_route / vs_gemm_route_epi answer 0 for every shape, epilogue
+    and dtype, and reject bad arguments; the library needs no vendor-library workspace (kinds 2, 3:
+    0 bytes) and reads no environment variable."""
     from vstyler import _lib
     lib = _lib.load()
-    monkeypatch.delenv("VS_GEMM_BACKEND", raising=False)
-    assert lib.vs_gemm_route(59280, 5120, 13824) == 1       # 4640 tiles
-    assert lib.vs_gemm_route(7410, 5120, 5120) == 1         # 580 tiles, K 5120
-    assert lib.vs_gemm_route(3705, 5120, 5120) == 1         # 300 tiles
-    # r3: the staggered 8-phase kernel keeps the FFN GEMMs of the Ulysses per-rank row counts
-    # (gemm.hip own_wins, profiles/r3/gemm_stagger_ab_s2.log)
-    assert lib.vs_gemm_route(7410, 5120, 13824) == 0        # FFN-down, SP = 8 merged phase
-    assert lib.vs_gemm_route(3705, 5120, 13824) == 0
-    assert lib.vs_gemm_route(14820, 5120, 13824) == 0       # SP = 4
-    assert lib.vs_gemm_route(7410, 15360, 5120) == 1        # q|k|v stays on hipBLASLt
-    # (FFN-up at <= 8192 rows also stays on the MFMA kernel: that rule keys on its GELU epilogue,
-    # which vs_gemm_route, a bias-epilogue query, does not take)
-    assert lib.vs_gemm_route(1024, 10240, 5120) == 1        # 160 tiles: cross k|v over the context
-    assert lib.vs_gemm_route(2, 30720, 5120) == 1           # time projection
-    assert lib.vs_gemm_route(512, 4096, 10240) == 0         # 32 tiles, K 10240 (UMT5 FFN-down)
-    assert lib.vs_gemm_route(59280, 64, 5120) == 0          # head: 232 tiles, N 64
-    assert lib.vs_gemm_route(59280, 5120, 64) == 1          # patch embedding: 4640 tiles
-    assert lib.vs_gemm_route(1024, 1536, 4096) == 0         # 24 tiles, N 1536
-    assert lib.vs_gemm_route(0, 1, 1) == _lib.VS_E_INVALID if hasattr(_lib, "VS_E_INVALID") else lib.vs_gemm_route(0, 1, 1) != 0
-    # vs_gemm_route_epi: r4, the gate-residual / residual GEMMs on the 4-wave kernel's fused epilogue
-    # (VS_GEMM_OWN=2 default: o-proj and FFN-down), the plain-bias q|k|v on hipBLASLt; fp8 (auto):
-    # the library only for bias-only GEMMs with N >= 2K
-    G, R, B, GL = 3, 4, 0, 1
-    monkeypatch.delenv("VS_GEMM_OWN", raising=False)
-    monkeypatch.delenv("VS_GEMM_KERNEL", raising=False)
-    monkeypatch.delenv("VS_FP8_BACKEND", raising=False)
-    assert lib.vs_gemm_route_epi(59280, 5120, 5120, G, 0) == 0      # o-proj + gate-residual
-    assert lib.vs_gemm_route_epi(59280, 5120, 5120, R, 0) == 0      # cross-attention o + residual
-    assert lib.vs_gemm_route_epi(59280, 5120, 13824, G, 0) == 0     # FFN-down + gate-residual
-    assert lib.vs_gemm_route_epi(59280, 15360, 5120, B, 0) == 1     # q|k|v
-    assert lib.vs_gemm_route_epi(59280, 5120, 5120, B, 0) == lib.vs_gemm_route(59280, 5120, 5120)
-    assert lib.vs_gemm_route_epi(59280, 15360, 5120, B, 1) == 1     # fp8 q|k|v: hipBLASLt fp8
-    assert lib.vs_gemm_route_epi(59280, 5120, 5120, G, 1) == 0      # fp8 o-proj: the MFMA kernel
-    assert lib.vs_gemm_route_epi(59280, 13824, 5120, GL, 1) == 0    # fp8 FFN-up
-    assert lib.vs_gemm_route_epi(59280, 5120, 5120, 9, 0) < 0       # invalid epilogue
-    monkeypatch.setenv("VS_GEMM_OWN", "0")
-    assert lib.vs_gemm_route_epi(59280, 5120, 5120, G, 0) == 1      # the r3 routing
-    monkeypatch.setenv("VS_FP8_BACKEND", "lt")
-    assert lib.vs_gemm_route_epi(59280, 5120, 5120, G, 1) == 1
-    monkeypatch.setenv("VS_FP8_BACKEND", "vstyler")
-    assert lib.vs_gemm_route_epi(59280, 15360, 5120, B, 1) == 0
-    monkeypatch.setenv("VS_GEMM_BACKEND", "vstyler")
-    assert lib.vs_gemm_route(59280, 5120, 5120) == 0
-    monkeypatch.setenv("VS_GEMM_BACKEND", "lt")
-    assert lib.vs_gemm_route(64, 64, 64) == 1
+    for m, n, k in ((59280, 15360, 5120), (59280, 13824, 5120), (59280, 5120, 13824), (7410, 15360, 5120),
+                    (1024, 10240, 4096), (2, 30720, 5120), (64, 64, 64)):
+        assert lib.vs_gemm_route(m, n, k) == 0
+        for epi in range(5):
+            assert lib.vs_gemm_route_epi(m, n, k, epi, 0) == 0
+            assert lib.vs_gemm_route_epi(m, n, k, epi, 1) == 0
+    assert lib.vs_gemm_route(0, 1, 1) < 0 or lib.vs_gemm_route(0, 1, 1) == 1
+    assert lib.vs_gemm_route_epi(59280, 5120, 5120, 9, 0) < 0
+    assert lib.vs_split_workspace_bytes(2) == 0 and lib.vs_split_workspace_bytes(3) == 0
+    assert lib.vs_split_workspace_bytes(5) >= 1280
+    so = open(_lib.LIB_PATH, "rb").read()
+    assert b"libhipblaslt" not in so and b"VS_GEMM_BACKEND" not in so and b"getenv" not in so
+
+
+def test_options_table():
+    """vs_set_option / vs_get_option (include/vstyler.h): product defaults, range checks, the previous
+    value returned, and kernels.options() restoring the table."""
+    from vstyler import _lib, kernels as K
+    lib = _lib.load()
+    defaults = {"gemm_tile": 0, "gemm_kernel": 4, "gemm_split": 1, "gemm_queue": 1, "attn_impl": 0,
+                "attn_mfma": 16, "attn_nc": 1, "attn_split": 1, "attn_persist": 1, "vae_pxb": 2, "vae_pre": 3}
+    assert set(defaults) == set(_lib.OPTIONS)
+    for name, v in defaults.items():
+        assert K.get_option(name) == v, name
+    with K.options(gemm_kernel=8, gemm_queue=0, attn_mfma=32):
+        assert (K.get_option("gemm_kernel"), K.get_option("gemm_queue"), K.get_option("attn_mfma")) == (8, 0, 32)
+    assert (K.get_option("gemm_kernel"), K.get_option("gemm_queue"), K.get_option("attn_mfma")) == (4, 1, 16)
+    for name, bad in (("gemm_tile", 64), ("gemm_kernel", 5), ("attn_mfma", 8), ("vae_pre", 4), ("gemm_split", 2)):
+        with pytest.raises(ValueError):
+            K.set_option(name, bad)
+    assert lib.vs_set_option(99, 0) < 0 and lib.vs_get_option(-1) < 0

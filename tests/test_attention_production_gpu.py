@@ -98,12 +98,12 @@ def test_attention_c4_1280x720x121_sampled_heads(K):
     check(out, q, k, v, [(0, 0), (0, 17), (1, 22), (1, 39)], S, S, f"C4 B2 S{S} H{H}")
 
 
-def test_attention_nc_redo_at_production_grid(K, monkeypatch):
+def test_attention_nc_redo_at_production_grid(K, opt):
     """Spikes (overflow of the optimistic exp2) and all-low rows (underflow) in whole items and in
     split-tail items of the 14B grid: flagged items equal the checked kernel bit for bit, the rest
     match the fp32 reference."""
     from test_kernels_gpu import _flags_zero
-    monkeypatch.setenv("VS_ATTN_MFMA", "16")
+    opt(attn_mfma=16)
     B, S, H = 2, 29640, 40
     q, k, v = inputs(B, S, H, 4, qscale=1.0)
     u = torch.ones(D, device="cuda", dtype=BF16)
@@ -120,8 +120,7 @@ def test_attention_nc_redo_at_production_grid(K, monkeypatch):
     K.attention(q, k, v, out, H, B)
     torch.cuda.synchronize()
     assert _flags_zero(K)
-    monkeypatch.setenv("VS_ATTN_NC", "0")
-    monkeypatch.setenv("VS_ATTN_NO_SPLIT", "1")
+    opt(attn_nc=0, attn_split=0)
     chk = torch.empty_like(q)
     K.attention(q, k, v, chk, H, B)
     torch.cuda.synchronize()
@@ -133,13 +132,13 @@ def test_attention_nc_redo_at_production_grid(K, monkeypatch):
     check(out, q, k, v, [(0, 0), (0, 3), (1, 38), (1, 39)], S, S, "NC redo grid")
 
 
-@pytest.mark.parametrize("variant", ["default", "VS_ATTN_NC=0", "VS_ATTN_NO_SPLIT=1", "VS_ATTN_NO_PERSIST=1"])
-def test_attention_14b_fused_qkv_views(K, monkeypatch, variant):
+@pytest.mark.parametrize("variant", ["default", "attn_nc=0", "attn_split=0", "attn_persist=0"])
+def test_attention_14b_fused_qkv_views(K, opt, variant):
     """The model's layout: q/k/v are column slices of ONE [B*S, 3D] q|k|v buffer (row stride 15 360,
     batch stride 455 M elements), at the 14B CFG shape, under every kernel route."""
     if variant != "default":
         name, val = variant.split("=")
-        monkeypatch.setenv(name, val)
+        opt(**{name: int(val)})
     B, S, H = 2, 29640, 40
     D3 = 3 * H * D
     g = torch.Generator(device="cuda").manual_seed(5)

@@ -52,9 +52,8 @@ def test_gemm_fp8_integer_exact(M, N, Kd):
 
 
 @pytest.mark.parametrize("epi", ["bias", "gelu", "gate_res"])
-def test_gemm_fp8_random_epilogues(epi, monkeypatch):
+def test_gemm_fp8_random_epilogues(epi):
     K = _k()
-    monkeypatch.setenv("VS_LT_GELU", "0")       # the reference's rounding points (fused GELU: below)
     M, N, Kd = 700, 1024, 1536
     g = torch.Generator().manual_seed(3)
     x = torch.randn(M, Kd, generator=g).to(BF16)
@@ -113,13 +112,13 @@ def test_model_fn_fp8_tiny_vs_oracle():
 
 
 @pytest.mark.parametrize("epi", ["bias", "gelu", "gate_res", "res"])
-def test_gemm_fp8_hipblaslt_route_matches_mfma_kernel(epi, monkeypatch):
-    """vs_gemm_fp8's default route (hipBLASLt fp8 with the per-token scale as its outer B-scale
-    vector, then the epilogue pass) against the fp8 MFMA kernel (VS_FP8_BACKEND=vstyler), on random
-    data: bit-identical for every epilogue (profiles/r1/gemm_fp8_lt_r1j.log measures the same at
-    the 14B shapes)."""
+def test_gemm_fp8_schedules_agree(epi, opt):
+    """vs_gemm_fp8's schedules on random data: the 4-wave kernel with the XCD tile queues (default) and
+    with the static lists bit-identical (same per-tile summation order), the 8-phase kernel (another
+    MFMA shape, another order) within fp32 summation noise -- for every epilogue (r5: the
+    vendor-library fp8 route these were compared with is gone)."""
     K = _k()
-    M, N, Kd = 1500, 2048, 2560
+    M, N, Kd = 12300, 2048, 2560          # 49 x 8 = 392 tiles: the persistent walk + queue
     g = torch.Generator(device="cuda").manual_seed(7)
     x = torch.randn(M, Kd, device="cuda", generator=g).to(BF16)
     w8 = (0.05 * torch.randn(N, Kd, device="cuda", generator=g)).to(torch.float8_e4m3fn).view(torch.uint8)
@@ -129,10 +128,9 @@ def test_gemm_fp8_hipblaslt_route_matches_mfma_kernel(epi, monkeypatch):
     x8 = torch.empty(M, Kd, dtype=torch.uint8, device="cuda")
     sc = torch.empty(M, dtype=torch.float32, device="cuda")
     K.quant_fp8_rows(x, x8, sc)
-    monkeypatch.setenv("VS_LT_GELU", "0")       # the two-pass GELU route on both backends
     outs = []
-    for be in ("lt", "vstyler"):
-        monkeypatch.setenv("VS_FP8_BACKEND", be)
+    for o in (dict(gemm_kernel=4, gemm_queue=1), dict(gemm_kernel=4, gemm_queue=0), dict(gemm_kernel=8)):
+        opt(**o)
         out = res0.clone() if epi in ("gate_res", "res") else torch.empty(M, N, dtype=BF16, device="cuda")
         kw = dict(bias=b)
         if epi == "gelu":
@@ -145,41 +143,5 @@ def test_gemm_fp8_hipblaslt_route_matches_mfma_kernel(epi, monkeypatch):
         torch.cuda.synchronize()
         outs.append(out)
     assert torch.equal(outs[0], outs[1])
-
-
-def test_gemm_fp8_hipblaslt_fused_gelu(monkeypatch):
-    """The opt-in fp8 GELU route (VS_FP8_BACKEND=lt VS_LT_GELU=1; since r4 the default runs the fp8
-    FFN-up on the MFMA kernel): hipBLASLt fp8 with its fused GELU_BIAS epilogue, the GELU-tanh of
-    the fp32 (x8 . w8^T) * scale + bias rounded once.  Against the fp64 GELU of that exact
-    pre-activation it is as close as one rounding allows; from fp8_linear's rounding points
-    (bf16(GELU(bf16(linear))), VS_LT_GELU=0) it differs by at most twice their own error."""
-    K = _k()
-    monkeypatch.setenv("VS_FP8_BACKEND", "lt")
-    M, N, Kd = 700, 1024, 1536
-    g = torch.Generator().manual_seed(9)
-    x = torch.randn(M, Kd, generator=g).to(BF16)
-    w8 = (0.03 * torch.randn(N, Kd, generator=g)).to(torch.float8_e4m3fn)
-    b = (0.1 * torch.randn(N, generator=g)).to(BF16)
-    x8 = torch.empty(M, Kd, dtype=torch.uint8, device="cuda")
-    sc = torch.empty(M, dtype=torch.float32, device="cuda")
-    K.quant_fp8_rows(x.cuda(), x8, sc)
-    xd = x8.cpu().view(torch.float8_e4m3fn).double() * sc.cpu().double()[:, None]
-    pre = xd @ w8.double().t() + b.double()
-
-    def gelu64(v):
-        return 0.5 * v * (1 + torch.tanh(0.7978845608028654 * (v + 0.044715 * v ** 3)))
-    outs = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("VS_LT_GELU", mode)
-        out = torch.empty(M, N, dtype=BF16, device="cuda")
-        K.gemm_fp8(x8, sc, w8.view(torch.uint8).cuda(), out, epilogue=K.VS_EPI_GELU, bias=b.cuda())
-        outs[mode] = out.cpu()
-    fused, two = outs["1"], outs["0"]
-    ex = gelu64(pre)
-    frac = (fused != ex.to(BF16)).float().mean().item()
-    assert frac < 0.03, frac
-    rel = lambda v: ((v.double() - ex).norm() / ex.norm()).item()   # noqa: E731
-    assert rel(fused) <= rel(two), (rel(fused), rel(two))
-    # the two-pass route's own error against the exact GELU bounds the difference
-    assert (fused.double() - two.double()).abs().max().item() <= \
-        2 * (two.double() - ex).abs().max().item() + 2.0 ** -14
+    rel = ((outs[2].float() - outs[0].float()).norm() / outs[0].float().norm()).item()
+    assert rel < 2e-3, rel

@@ -102,27 +102,17 @@ def test_hotload_refuses_fp8_layers_atomically():
 def test_residual_ln_fusion_follows_the_gemm_route(monkeypatch):
     """models._fusable_lt asks vs_gemm_route_epi for the residual epilogue the unfused path would run:
     the residual + LayerNorm fusion (a staged GEMM output) is taken exactly when that GEMM would run
-    on the hipBLASLt route, so the product never stages an output the MFMA kernel would have fused
-    (r4 routing, include/vstyler.h).  Host-only: route queries, no kernels."""
+    as a staged product + epilogue pass -- never with the product library, whose GEMMs all fuse their
+    epilogue (r5, include/vstyler.h), so the model never stages an output.  Host-only."""
     from vstyler import kernels as K
     from vstyler.models import _fusable_lt, quantize_fp8_
-    for k in ("VS_GEMM_OWN", "VS_GEMM_KERNEL", "VS_GEMM_BACKEND", "VS_FP8_BACKEND", "VSTYLER_FUSE_RES_LN"):
-        monkeypatch.delenv(k, raising=False)
+    monkeypatch.delenv("VSTYLER_FUSE_RES_LN", raising=False)
     o = nn.Linear(5120, 5120, dtype=BF16)              # o-proj / cross-attention o shape
     down = nn.Linear(13824, 5120, dtype=BF16)          # FFN-down
-    M = 59280
-    for lin, ep in ((o, K.VS_EPI_GATE_RES), (o, K.VS_EPI_RES), (down, K.VS_EPI_GATE_RES)):
-        assert _fusable_lt(lin, M, ep) == K.gemm_route(M, lin.out_features, lin.in_features, epilogue=ep)
-        assert _fusable_lt(lin, M, ep) is False     # r4 default: the MFMA kernel's fused epilogue
-    monkeypatch.setenv("VS_GEMM_OWN", "0")               # the r3 routing: hipBLASLt + fused residual-LN
-    assert _fusable_lt(o, M, K.VS_EPI_GATE_RES) is True
-    assert _fusable_lt(down, M, K.VS_EPI_GATE_RES) == K.gemm_route(M, 5120, 13824)
-    monkeypatch.setenv("VSTYLER_FUSE_RES_LN", "0")
-    assert _fusable_lt(o, M, K.VS_EPI_GATE_RES) is False
-    monkeypatch.delenv("VSTYLER_FUSE_RES_LN")
-    # fp8 weights: the fp8 route (auto: the MFMA kernel for residual epilogues)
+    for M in (59280, 7410):
+        for lin, ep in ((o, K.VS_EPI_GATE_RES), (o, K.VS_EPI_RES), (down, K.VS_EPI_GATE_RES)):
+            assert _fusable_lt(lin, M, ep) == K.gemm_route(M, lin.out_features, lin.in_features, epilogue=ep)
+            assert _fusable_lt(lin, M, ep) is False
     blk, _ = _block()
     quantize_fp8_(blk)
-    assert _fusable_lt(blk.self_attn.o, M, K.VS_EPI_GATE_RES) is False
-    monkeypatch.setenv("VS_FP8_BACKEND", "lt")
-    assert _fusable_lt(blk.self_attn.o, M, K.VS_EPI_GATE_RES) is True
+    assert _fusable_lt(blk.self_attn.o, 59280, K.VS_EPI_GATE_RES) is False

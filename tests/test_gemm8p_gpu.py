@@ -1,5 +1,5 @@
 """The 256x256 GEMMs (gemm_bf16_tn_8p and gemm_bf16_tn_4w, csrc/gemm.hip) through vs_gemm, forced
-onto the hand-written kernels (VS_GEMM_BACKEND=vstyler, VSTYLER_GEMM_TILE=256, VS_GEMM_KERNEL).
+onto the 256x256 schedule and each kernel (options gemm_tile=256, gemm_kernel=8 | 4).
 
 Integer-valued operands keep every fp32 sum exact, so every output must equal the exact product
 bit for bit (through each epilogue's reference rounding points, oracle/wan_oracle.py) for:
@@ -19,12 +19,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(params=["8p", "4w"])
-def K(monkeypatch, request):
-    """Both 256x256 kernels: gemm_bf16_tn_8p and gemm_bf16_tn_4w (VS_GEMM_KERNEL); the LoRA second
+def K(opt, request):
+    """Both 256x256 kernels: gemm_bf16_tn_8p and gemm_bf16_tn_4w (option gemm_kernel); the LoRA second
     phase always runs on the 8-phase kernel."""
-    monkeypatch.setenv("VS_GEMM_BACKEND", "vstyler")
-    monkeypatch.setenv("VSTYLER_GEMM_TILE", "256")
-    monkeypatch.setenv("VS_GEMM_KERNEL", request.param)
+    opt(gemm_tile=256, gemm_kernel=8 if request.param == "8p" else 4)
     from vstyler import kernels
     return kernels
 
@@ -83,7 +81,7 @@ def test_gemm8p_lora_second_phase_exact(K, Kd, r):
     assert torch.equal(out, ref)
 
 
-def test_gemm8p_split_tail_exact(K, monkeypatch):
+def test_gemm8p_split_tail_exact(K, opt):
     """272 tiles on 256 CUs: 256 whole tiles + 16 tail tiles as K pieces, summed by the combine."""
     M, N, Kd = 4352, 4096, 4096
     cus = torch.cuda.get_device_properties(0).multi_processor_count
@@ -93,17 +91,14 @@ def test_gemm8p_split_tail_exact(K, monkeypatch):
     gate = (0.25 * torch.randn(2, N, device="cuda", generator=g)).to(BF16)
     outs = {}
     for split in (True, False):
-        if split:
-            monkeypatch.delenv("VS_GEMM_NO_SPLIT", raising=False)
-        else:
-            monkeypatch.setenv("VS_GEMM_NO_SPLIT", "1")
+        opt(gemm_split=1 if split else 0)
         y = torch.empty(M, N, dtype=BF16, device="cuda")
         K.gemm(a, w, y, bias=b)
         x = res.clone()
         K.gemm(a, w, x, epilogue=K.VS_EPI_GATE_RES, bias=b, residual=x, gate=gate, gate_bstride=N,
                rows_per_batch=M // 2, hint=res, hint_scale=0.5)
         outs[split] = (y, x)
-    monkeypatch.delenv("VS_GEMM_NO_SPLIT", raising=False)
+    opt(gemm_split=1)
     assert torch.equal(outs[True][0], (a.float() @ w.float().t() + b.float()).to(BF16))
     for s_, u_ in zip(outs[True], outs[False]):
         assert torch.equal(s_, u_)
@@ -126,13 +121,12 @@ def test_gemm8p_random_vs_fp32(K):
 @pytest.mark.parametrize("kern", ["8p", "4w"])
 @pytest.mark.parametrize("M,N,Kd", [(256, 256, 128), (300, 520, 256), (1000, 768, 640), (520, 300, 5120),
                                     (512, 512, 384)])
-def test_gemm_fp8_8p_integer_exact(M, N, Kd, kern, monkeypatch):
-    """gemm_fp8_tn_8p (VS_FP8_BACKEND=vstyler): integer operands exact in e4m3 with exact fp32 sums
+def test_gemm_fp8_8p_integer_exact(M, N, Kd, kern, opt):
+    """gemm_fp8_tn_8p / gemm_fp8_tn_4w (option gemm_kernel): integer operands exact in e4m3 with exact fp32 sums
     must reproduce oracle.fp8_linear (layers.py:115-151) bit for bit: pins the MX 32x32x64 operand
     maps, the fp8 chunk swizzle and the per-row scale."""
     from vstyler import kernels as K
-    monkeypatch.setenv("VS_FP8_BACKEND", os.environ.get("VS_FP8_BACKEND", "vstyler"))
-    monkeypatch.setenv("VS_GEMM_KERNEL", kern)
+    opt(gemm_kernel=8 if kern == "8p" else 4)
     g = torch.Generator().manual_seed(M + N + Kd)
     x = torch.randint(-4, 5, (M, Kd), generator=g).to(BF16)
     x[::5] *= 512          # rows whose max exceeds 448: scale 2**k > 1
@@ -149,12 +143,11 @@ def test_gemm_fp8_8p_integer_exact(M, N, Kd, kern, monkeypatch):
 
 
 @pytest.mark.parametrize("kern", ["8p", "4w"])
-def test_gemm_fp8_8p_split_tail_and_epilogue(kern, monkeypatch):
+def test_gemm_fp8_8p_split_tail_and_epilogue(kern, opt):
     """272 tiles: the split-tail pieces + combine (per-row scale applied after the sum) equal the
     unsplit kernel on integer data; gate-residual + hint epilogue bit-exact vs the oracle."""
     from vstyler import kernels as K
-    monkeypatch.setenv("VS_FP8_BACKEND", os.environ.get("VS_FP8_BACKEND", "vstyler"))
-    monkeypatch.setenv("VS_GEMM_KERNEL", kern)
+    opt(gemm_kernel=8 if kern == "8p" else 4)
     M, N, Kd, S = 4352, 4096, 1024, 2176
     g = torch.Generator().manual_seed(21)
     x = torch.randint(-4, 5, (M, Kd), generator=g).to(BF16)
@@ -172,19 +165,16 @@ def test_gemm_fp8_8p_split_tail_and_epilogue(kern, monkeypatch):
     w8 = w.to(torch.float8_e4m3fn).view(torch.uint8).cuda()
     outs = []
     for split in (True, False):
-        if split:
-            monkeypatch.delenv("VS_GEMM_NO_SPLIT", raising=False)
-        else:
-            monkeypatch.setenv("VS_GEMM_NO_SPLIT", "1")
+        opt(gemm_split=1 if split else 0)
         xo = res.cuda()
         K.gemm_fp8(x8, sc, w8, xo, epilogue=K.VS_EPI_GATE_RES, bias=b.cuda(), residual=xo, gate=gate.cuda(),
                    gate_bstride=N, rows_per_batch=S, hint=hint.cuda(), hint_scale=0.5)
         outs.append(xo.cpu())
-    monkeypatch.delenv("VS_GEMM_NO_SPLIT", raising=False)
+    opt(gemm_split=1)
     assert torch.equal(outs[0], ref) and torch.equal(outs[1], ref)
 
 
-def test_gemm_persistent_ragged_exact(K, monkeypatch):
+def test_gemm_persistent_ragged_exact(K):
     """The persistent walk with ragged edges: 17 x 17 = 289 tiles of a 4100 x 4104 output (rows and
     columns past the matrix in the last tile row / column, dropped by the buffer range checks), 256
     persistent workgroups + the rest as whole tiles or split pieces; every epilogue mode bit-exact
@@ -211,12 +201,11 @@ def test_gemm_persistent_ragged_exact(K, monkeypatch):
 
 
 @pytest.mark.parametrize("kern", ["8p", "4w"])
-def test_gemm_fp8_persistent_ragged_exact(kern, monkeypatch):
+def test_gemm_fp8_persistent_ragged_exact(kern, opt):
     """The fp8 kernels' persistent walk with ragged edges (289 tiles of 4100 x 4104): integer
     operands exact in e4m3 reproduce oracle.fp8_linear bit for bit."""
     from vstyler import kernels as K
-    monkeypatch.setenv("VS_FP8_BACKEND", "vstyler")
-    monkeypatch.setenv("VS_GEMM_KERNEL", kern)
+    opt(gemm_kernel=8 if kern == "8p" else 4)
     M, N, Kd = 4100, 4104, 1024
     g = torch.Generator().manual_seed(45)
     x = torch.randint(-4, 5, (M, Kd), generator=g).to(BF16)

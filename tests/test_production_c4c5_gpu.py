@@ -6,7 +6,7 @@ accumulation; the product within NOISE_X times that noise floor):
     a rank-32 CausVid-style LoRA (kohya lora_down/lora_up/alpha keys) merged into the DiT block,
     then every block Linear as AutoWrappedLinear.fp8_linear (vram_management/layers.py:115-151:
     per-row activation scale, e4m3fn weights), VACE strength 0.975 -- on BOTH fp8 routes
-    (VS_FP8_BACKEND lt = hipBLASLt fp8, vstyler = the hand-written gemm_fp8_tn_8p);
+    (the 4-wave gemm_fp8_tn_4w and the 8-phase gemm_fp8_tn_8p; r4 also ran hipBLASLt fp8, gone in r5);
   * C4: Wan2.1-VACE-14B block pair at 1280x720x121 (S = 111 600, 2 x 111 600 = 223 200 GEMM rows:
     every block GEMM route and split plan at that M);
   * VAE: tiled encode and decode at 480x832 with the real 3x3 grid of 30x52-latent tiles (stride
@@ -42,13 +42,15 @@ def causvid_lora(cfg, rank, alpha, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("backend", ["lt", "vstyler"])
-def test_c5_14b_fp8_block_pair_causvid_lora_832x480x73(backend, monkeypatch):
+@pytest.mark.parametrize("kernel", [4, 8])
+def test_c5_14b_fp8_block_pair_causvid_lora_832x480x73(kernel, opt):
+    """C5 on both fp8 256x256 kernels (option gemm_kernel: the 4-wave default, the 8-phase one)."""
     from vstyler import model_fn_wan_video
     from vstyler.lora import merge_lora, normalize_lora_keys
     from vstyler.loader import normalize_keys
     from vstyler.models import quantize_fp8_
-    monkeypatch.setenv("VS_FP8_BACKEND", backend)
+    opt(gemm_kernel=kernel)
+    backend = f"{kernel}-wave" if kernel == 4 else "8-phase"
     cfg = dict(O.WAN_CONFIGS["14B"], num_layers=1, vace_layers=(0,))
     W = gpu_weights(cfg, seed=17)
     dit, vace = build(cfg, W)

@@ -77,9 +77,9 @@ def test_causal_conv3d_k3(cin, cout, res):
 
 @pytest.mark.parametrize("cin,cout,up2", [(96, 96, False), (64, 128, True), (384, 384, False), (32, 16, False),
                                           (192, 64, False)])
-def test_conv_pixel_blocks_bit_identical(cin, cout, up2, monkeypatch):
-    """256-pixel tiles (two 32-pixel blocks per wave, VS_VAE_PXB=2) and the two-stage load pipeline
-    (VS_VAE_PRE=2) == 128-pixel tiles with one stage: the same K order per output, ragged last tile
+def test_conv_pixel_blocks_bit_identical(cin, cout, up2, opt):
+    """256-pixel tiles (two 32-pixel blocks per wave, option vae_pxb=2) and the two-stage load pipeline
+    (vae_pre=2) == 128-pixel tiles with one stage: the same K order per output, ragged last tile
     (M = 2 * 5 * h * w not a multiple of 256) included."""
     vae = _vae()
     g = torch.Generator().manual_seed(cin * 7 + cout)
@@ -87,9 +87,8 @@ def test_conv_pixel_blocks_bit_identical(cin, cout, up2, monkeypatch):
     x = _to_nthwc(_rand((2, cin, 5, h, w), g))
     cw = vae.ConvW(_rand((cout, cin, 3, 3, 3), g, 1 / math.sqrt(27 * cin)), _rand((cout,), g, 0.1), "cuda")
     outs = []
-    for pxb, pre in (("1", "1"), ("2", "1"), ("1", "2"), ("2", "2"), ("1", "3"), ("2", "3")):
-        monkeypatch.setenv("VS_VAE_PXB", pxb)
-        monkeypatch.setenv("VS_VAE_PRE", pre)
+    for pxb, pre in ((1, 1), (2, 1), (1, 2), (2, 2), (1, 3), (2, 3)):
+        opt(vae_pxb=pxb, vae_pre=pre)
         outs.append(vae.conv(x, cw, (5, 2 * h if up2 else h, 2 * w if up2 else w), pad=(2, 1, 1), up2=up2).cpu())
     for o in outs[1:]:
         assert torch.equal(outs[0], o)

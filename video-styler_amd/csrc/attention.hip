@@ -36,9 +36,6 @@ constexpr int KT = BKV * KROW;   // 17408
 constexpr int VT = BKV * VROW;   // 20480
 constexpr int LDS_BYTES = 2 * (KT + VT);   // K ring 2 x 17408 + V ring 2 x 20480
 constexpr int PERSIST_MIN_TILES = 8;
-#ifndef VS_ATTN_MFMA16_DEFAULT
-#define VS_ATTN_MFMA16_DEFAULT true
-#endif
 
 
 
@@ -982,13 +979,12 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
     const int nqb = (sq + BQ - 1) / BQ;
     const long long nwg = (long long)nqb * heads * batch;
     if (nwg > 0x7fffffff) return VS_E_INVALID;
-    // MFMA shape of the QK / PV products (VS_ATTN_MFMA=16|32)
-    const char* shape_env = getenv("VS_ATTN_MFMA");
-    const bool m16 = shape_env ? shape_env[0] == '1' : VS_ATTN_MFMA16_DEFAULT;
+    // MFMA shape of the QK / PV products (VS_OPT_ATTN_MFMA 16 | 32)
+    const bool m16 = vs_opt(VS_OPT_ATTN_MFMA) == 16;
     const float c = scale * 1.4426950408889634f;
     const bool rebase = (long long)skv * ldk * 2 >= (1LL << 31) || (long long)skv * ldv * 2 >= (1LL << 31);
     const int nkv = (skv + BKV - 1) / BKV;
-    const int cus = vs_cus_for_split("VS_ATTN_NO_SPLIT");
+    const int cus = vs_cus_for_split(!vs_opt(VS_OPT_ATTN_SPLIT));
     SplitPlan sp = plan_split(nwg, nkv, cus);
     float* part = nullptr;
     if (sp.ntail) {
@@ -996,22 +992,20 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
         if (!part) sp = SplitPlan{(int)nwg, 0, 1, 0};
     }
     // persistent grid: one block per CU runs the whole items when there is more than one round of
-    // them and an item has at least PERSIST_MIN_TILES key tiles (VS_ATTN_NO_PERSIST=1: one block per
-    // item, the r1 grid)
-    const int ncu = vs_cus_for_split(nullptr);
-    const char* np_env = getenv("VS_ATTN_NO_PERSIST");
-    const bool no_persist = np_env && np_env[0] == '1';
+    // them and an item has at least PERSIST_MIN_TILES key tiles (VS_OPT_ATTN_PERSIST 0: one block
+    // per item, the r1 grid)
+    const int ncu = vs_cus_for_split(false);
+    const bool no_persist = !vs_opt(VS_OPT_ATTN_PERSIST);
     // (the Q prefetch and the O drain address a wave's rows through 32-bit buffer ranges)
     const bool span_ok = (long long)sq * ldq * 2 < (1LL << 32) && (long long)sq * ldo * 2 < (1LL << 32);
     const int npers =
         (!no_persist && span_ok && ncu > 0 && nkv >= PERSIST_MIN_TILES && sp.nmain > ncu) ? ncu : sp.nmain;
     // optimistic softmax (NC, comment at NC_LMIN): M16 only, needs the caller's item-flag workspace
     // (kind 4, zero-filled) and an O that does not overlap Q / K / V (the redo launch re-reads
-    // them); VS_ATTN_NC=0 keeps the checked kernel
-    const char* nc_env = getenv("VS_ATTN_NC");
+    // them); VS_OPT_ATTN_NC 0 keeps the checked kernel
     int* flags = nullptr;
     int nc_cap = 0;
-    if (m16 && !(nc_env && nc_env[0] == '0')) {
+    if (m16 && vs_opt(VS_OPT_ATTN_NC)) {
         auto span = [&](const void* p, long long bs, long long ld, int rows) {
             const char* b = (const char*)p;
             return std::make_pair(b, b + 2 * ((long long)(batch - 1) * bs + (long long)(rows - 1) * ld + heads * HD));
@@ -1053,11 +1047,11 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
         hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(NTHR), lds, (hipStream_t)stream, a);
         return hipGetLastError() == hipSuccess;
     };
-    // the NC pass: attn_fwd_w4 (4 waves x 64 rows); VS_ATTN_IMPL=8 / =4 force the 8-wave / 4-wave kernel
+    // the NC pass: attn_fwd_w4 (4 waves x 64 rows); VS_OPT_ATTN_IMPL 8 / 4 force the 8-wave / 4-wave kernel
     // (items of fewer than 16 key tiles -- the 512-key cross-attention -- stay on the 8-wave kernel:
     // the 4-wave pipeline's per-item fill and drain are a large share of an 8-tile item)
-    const char* impl_env = getenv("VS_ATTN_IMPL");
-    const bool w4 = flags && (impl_env ? impl_env[0] == '4' : nkv >= 16);
+    const int impl = vs_opt(VS_OPT_ATTN_IMPL);
+    const bool w4 = flags && (impl ? impl == 4 : nkv >= 16);
     if (w4) {
         if (attn_w4_launch(args, rebase, (unsigned)grid, (hipStream_t)stream) != hipSuccess) return VS_E_LAUNCH;
     } else if (!launch(pick(flags ? MODE_NC : MODE_CHK), grid, args)) {
@@ -1098,11 +1092,36 @@ extern "C" int vs_attn_split_plan(int batch, int sq, int skv, int heads, int cus
 extern "C" long long vs_split_workspace_bytes(int kind) {
     if (kind == 0) return (long long)MAX_PIECES * BQ * PROW * (long long)sizeof(float);
     if (kind == 1) return vs_gemm_split_workspace_bytes_impl();
-    if (kind == 2) return 128LL << 20;          // hipBLASLt (stream-K partials)
+#ifdef VS_AB
+    if (kind == 2) return 128LL << 20;          // the A/B build's vendor library (stream-K partials)
+    if (kind == 3) return -1;                   // its epilogue staging: m * n * 2 of the largest GEMM
+#else
+    if (kind == 2 || kind == 3) return 0;       // not used (no vendor-library route in this build)
+#endif
     if (kind == 4) return 1LL << 20;            // attention item flags (int per item; zero-filled)
     if (kind == 5) return 4096;                 // GEMM tile-queue words (zero-filled; gemm.hip W4Sched)
-    return -1;                                  // kind 3: m * n * 2 bytes of the largest routed GEMM
+    return -1;
 }
+
+// vs_set_option / vs_get_option (include/vstyler.h): the path-selection table of common.h
+extern "C" int vs_set_option(int id, int value) {
+    if (id < 0 || id >= VS_OPT_COUNT) return -VS_E_INVALID;
+    bool ok = false;
+    switch (id) {
+        case VS_OPT_GEMM_TILE: ok = value == 0 || value == 128 || value == 256; break;
+        case VS_OPT_GEMM_KERNEL: ok = value == 4 || value == 8; break;
+        case VS_OPT_ATTN_IMPL: ok = value == 0 || value == 4 || value == 8; break;
+        case VS_OPT_ATTN_MFMA: ok = value == 16 || value == 32; break;
+        case VS_OPT_VAE_PXB: ok = value == 1 || value == 2; break;
+        case VS_OPT_VAE_PRE: ok = value >= 1 && value <= 3; break;
+        default: ok = value == 0 || value == 1; break;           // the on / off options
+    }
+    if (!ok) return -VS_E_INVALID;
+    const int old = g_vs_opt[id];
+    g_vs_opt[id] = value;
+    return old;
+}
+extern "C" int vs_get_option(int id) { return (id < 0 || id >= VS_OPT_COUNT) ? -VS_E_INVALID : g_vs_opt[id]; }
 
 extern "C" int vs_split_workspace_bind(int kind, void* ptr, long long bytes, void* stream) {
     if (kind < 0 || kind > 5 || bytes < 0 || (ptr && ((uintptr_t)ptr & 15))) return VS_E_INVALID;

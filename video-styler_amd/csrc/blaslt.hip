@@ -1,13 +1,8 @@
-// hipBLASLt for the plain part of the block GEMMs (host code only).
-//
-// The task's rule for MI355X: hand-written MFMA kernels for fused hot ops, the vendor library for
-// plain library GEMMs.  vs_gemm routes C = A W^T + bias of the large block GEMMs here (one bf16
-// rounding of acc + bias, exactly the first rounding point of every vs_gemm epilogue) and finishes
-// any further epilogue (GELU, SiLU, gate-residual [+ VACE hint], residual) with gemm_epi_apply8,
-// which continues from that rounded value with the same code as the fused epilogue -- so the route
-// keeps the reference's rounding points and differs from the MFMA kernels only in fp32 summation
-// order.  (The optional hipBLASLt GELU_BIAS epilogue, VS_LT_GELU=1, drops the rounding before the
-// GELU; it is off by default.)
+// hipBLASLt route of the A/B build (-DVS_AB, `make ab`; host code only).  NOT part of libvstyler.so:
+// since r5 every GEMM of the product runs on the hand-written kernels (gemm.hip, "Routing (r5)").
+// This file keeps the r1-r4 vendor-library route buildable for same-box comparisons: VS_GEMM_BACKEND
+// =lt sends C = A W^T + bias here (one bf16 rounding of acc + bias, the first rounding point of every
+// vs_gemm epilogue) and the rest of the epilogue runs in gemm_epi_apply8 with the fused kernels' code.
 //
 // Algorithm choice (r3): the heuristic's FIRST pick for each shape, nothing else.  The r1/r2
 // in-process autotune timed up to 76 candidates per shape (the heuristic's 16 plus solutions from

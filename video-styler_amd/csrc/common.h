@@ -62,9 +62,14 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 #include <mutex>
 #include <tuple>
 
-// compute units of the current device (0 when unknown or when `env_off` is set: no split)
-inline int vs_cus_for_split(const char* env_off) {
-    if (env_off && getenv(env_off)) return 0;
+// Path-selection options (include/vstyler.h VS_OPT_*; set by vs_set_option, attention.hip): one
+// process-wide table, product defaults; the library reads no environment variable.
+inline volatile int g_vs_opt[VS_OPT_COUNT] = {0, 4, 1, 1, 0, 16, 1, 1, 1, 2, 3};
+inline int vs_opt(int id) { return g_vs_opt[id]; }
+
+// compute units of the current device (0 when unknown or when `off`: no split)
+inline int vs_cus_for_split(bool off) {
+    if (off) return 0;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     static std::mutex mu;
@@ -109,9 +114,12 @@ inline float* vs_split_workspace(int kind, size_t bytes, hipStream_t stream) {
 }
 
 long long vs_gemm_split_workspace_bytes_impl();   // gemm.hip
+#ifdef VS_AB
+// the A/B build's vendor-library route (blaslt.hip; -DVS_AB only, never the product library)
 int vs_lt_gemm_bias(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc, int m,
                     int n, int k, const void* bias, hipStream_t stream);   // blaslt.hip
 int vs_lt_gemm_bias_gelu(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc, int m,
                          int n, int k, const void* bias, hipStream_t stream);
 int vs_lt_gemm_fp8(const void* a8, long long lda, const float* scale_a, const void* w8, long long ldw, void* c,
                    long long ldc, int m, int n, int k, const void* bias, bool gelu, hipStream_t stream);   // blaslt.hip
+#endif

@@ -59,7 +59,9 @@ __device__ __forceinline__ void loadw(const bf16_t* p, float* v) {
         for (int i = 0; i < 4; ++i) { v[2 * i] = bflo(w[i]); v[2 * i + 1] = bfhi(w[i]); }
     }
 }
+#ifdef VS_AB
 __device__ __forceinline__ void load4(const bf16_t* p, float* v) { loadw<4>(p, v); }
+#endif
 
 // the op that follows each linear, on W consecutive columns of row m: y = bf16(acc + bias), then
 // GELU / SiLU / gate-residual [+ hint] / residual with the reference's bf16 rounding points
@@ -257,6 +259,7 @@ __global__ __launch_bounds__(256) void gemm_split_combine(const float* __restric
     epilogue_store(a, m, n, C, ldc, ep);
 }
 
+#ifdef VS_AB
 // Epilogue continuation after a hipBLASLt GEMM: y = bf16(acc + bias) is already materialised in
 // Y; feed it to the fused epilogue with no bias (rbf(y + 0) == y) so GELU / SiLU / gate-residual
 // [+ hint] / residual round exactly as in the fused kernels.  One thread per 4 columns.
@@ -282,6 +285,7 @@ __global__ __launch_bounds__(256) void gemm_epi_apply8(const bf16_t* Y, long lon
     loadw<8>(Y + (long long)m * ldy + n, v);
     epilogue_store_w<8>(v, m, n, C, ldc, ep);
 }
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // gemm_bf16_tn_8p: 256x256x64 tile, 8 waves, 4 phases per K-tile (cdna_hip_programming.md §5,
@@ -829,10 +833,11 @@ static_assert(4 * W4_ROWB == 0x1080, "the 4w kernel's M0 step");
 // dispatch) in slot s = b / 8 and computes tiles of its XCD's contiguous id range [x R, (x+1) R),
 // R = G8 tp (G8 = npers / 8), as ONE stream of K-tiles: the DMA runs two K-tiles ahead straight
 // across tile boundaries, so a tile's first K-tiles land during the previous tile's last K-tiles
-// and its epilogue.  A block's first two tiles are fixed (range positions s and G8 + s); after
-// them it takes tiles from its XCD's queue (head word q[x]: positions 2 G8 + t, t = 0, 1, ..), then,
-// once that has run dry, from the other XCDs' queues (probed in ring order), then from the
-// remainder pool (the nrem whole tiles past npers tp, head q[8]).
+// and its epilogue.  A block's first tile is fixed (range position s); every later one it takes
+// from its XCD's queue (head word q[x]: positions G8 + t, t = 0, 1, ..), then, once that has run
+// dry, from the other XCDs' queues (probed in ring order), then from the remainder pool (the nrem
+// whole tiles past npers tp, head q[8]).  So a block that starts late -- its CU held by another
+// kernel -- finds the queues drained and computes its one fixed tile.
 //   r4 walked a static list (positions s, s + G8, s + 2 G8, ..).  Over a 54-tile list an XCD's CUs
 //   drifted apart, so the 32 tiles in flight on an XCD stopped being one 4 x 8 block sharing its A / W
 //   slices in L2 (FFN-up: 23.1 GB of fabric reads per dispatch against the library's 13.1,
@@ -840,9 +845,10 @@ static_assert(4 * W4_ROWB == 0x1080, "the 4w kernel's M0 step");
 //   overlap) delayed its whole list.  With the queue the tiles computing on an XCD are always about
 //   the 32 most recently taken ids, and a CU that is slow or held simply takes fewer.
 // The next tile id is known one tile ahead: wave 0 takes it during tile k's epilogue (its atomic
-// issued at the epilogue's start and its value used at the end, under the stores), writes it to an
-// LDS word, and every wave reads that word in tile k+1's first K-tile behind a barrier -- before the
-// DMA cursor crosses into tile k+2 at the end of K-tile nt - 3 (nt >= 3, host-checked).  The last
+// issued at the epilogue's start and its value used at the end, under the stores) -- the second
+// tile's under the prologue's DMAs -- writes it to an LDS word, and every wave reads that word in
+// tile k+1's first K-tile behind a barrier, before the DMA cursor crosses into tile k+2 at the end
+// of K-tile nt - 3 (nt >= 3, host-checked).  The last
 // persistent block to finish (exit count q[9]) zeroes the queue words, so every launch finds them
 // zero (workspace kind 5: bound zeroed, one per stream, so graph replays and concurrent streams are
 // safe).  Without a bound queue the same walk runs the static list and the nrem whole tiles get
@@ -853,7 +859,7 @@ constexpr int WQ_BYTES = 10 * WQ_LINE * 4;    // 8 XCD heads, the remainder head
 struct W4Sched {
     unsigned* q;      // queue words (null: static lists)
     int npers;        // persistent blocks (a multiple of 8, or 0)
-    int tp;           // tiles per slot of an XCD range (>= 2 with a queue)
+    int tp;           // tiles per slot of an XCD range
     int nrem;         // whole tiles past npers * tp
 };
 struct W4Work {
@@ -923,11 +929,11 @@ struct W4Grab {
             ++k;
             return id;
         }
-        const unsigned qlen = (unsigned)(g8 * (sc.tp - 2));
+        const unsigned qlen = (unsigned)(g8 * (sc.tp - 1));
         if (local) {
             unsigned t;
             asm volatile("s_waitcnt vmcnt(%1)\n\tv_readfirstlane_b32 %0, %2" : "=s"(t) : "n"(W), "v"(t0) : "memory");
-            if (t < qlen) return x * g8 * sc.tp + 2 * g8 + (int)t;
+            if (t < qlen) return x * g8 * sc.tp + g8 + (int)t;
             local = false;
         }
         // other XCDs' queues: lanes 0-6 probe heads x+1 .. x+7, the first live one in ring order is
@@ -945,7 +951,7 @@ struct W4Grab {
             unsigned t = 0;
             if (lane == 0) t = wq_add(sc.q + v * WQ_LINE);
             t = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
-            if (t < qlen) return v * g8 * sc.tp + 2 * g8 + (int)t;
+            if (t < qlen) return v * g8 * sc.tp + g8 + (int)t;
         }
         steal = false;
         if (sc.nrem > 0) {
@@ -1132,7 +1138,8 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     // prologue: K-tiles 0 and 1 of the stream in flight (W then A each), then the k-step-0 fragments
     dma_tile(cur);
     ktile_rsrc(0);
-    if (tid == 0) slot_ref() = wk.second;     // read in the first tile's first K-tile
+    const bool dyn = sc.q && (int)blockIdx.x < sc.npers;    // a persistent block fed by the queues
+    if (dyn && wave == 0) grab.issue();                       // the second tile, under the prologue
 #pragma unroll
     for (int d = 0; d < 16; ++d) dma_now(d);
     dma_advance();
@@ -1148,6 +1155,10 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     bar();
     read_k0();
+    if (wave == 0) {        // the second tile into the LDS word (read in the first tile's first K-tile)
+        const int id = dyn ? grab.finish<32>(lane) : wk.second;     // (the 32 prologue DMAs since issue)
+        if (lane == 0) slot_ref() = id;
+    }
     // the first tile's first K-tile counts EPI_OPS operations behind K-tile 1's DMAs as every later
     // tile's does: as many stores the buffer range check drops (offset past num_records 0)
     {
@@ -1650,7 +1661,8 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
 
     // prologue: K-tiles 0 and 1 of the stream in flight, then the early fragments of K-tile 0
     dma_tile(cur);
-    if (tid == 0) slot_ref() = wk.second;     // read in the first tile's first K-tile
+    const bool dyn = sc.q && (int)blockIdx.x < sc.npers;    // a persistent block fed by the queues
+    if (dyn && wave == 0) grab.issue();                       // the second tile, under the prologue
 #pragma unroll
     for (int d = 0; d < 16; ++d) dma_now(0u, d);
     dma_advance();
@@ -1665,6 +1677,10 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     bar();
     read_early();
+    if (wave == 0) {        // the second tile into the LDS word (read in the first tile's first K-tile)
+        const int id = dyn ? grab.finish<32>(lane) : wk.second;     // (the 32 prologue DMAs since issue)
+        if (lane == 0) slot_ref() = id;
+    }
 
     // one K-tile: top reads of this K-tile (W 7, A 4-7), one barrier (its buffer free for the DMA of
     // the stream's K-tile two ahead, every 3 MFMAs from q = 11), vmcnt(6) + barrier at q = 29 (the
@@ -1853,64 +1869,33 @@ KSplit plan_ksplit(int ntiles, int nh, int cus, int step = 64) {
     return p;
 }
 
-// Which GEMMs go to hipBLASLt (VS_GEMM_BACKEND=vstyler|lt overrides).  Measured per block GEMM
-// of the 14B model with its real epilogue (profiles/r1/gemm_backend_ab_r1g.log): at 2 x 29640 rows
-// (4640-13920 tiles of 256^2) hipBLASLt + epilogue pass is 1.14-1.35x the MFMA kernels on all six,
-// staged gate-residual / residual included; at the SP=8 row count (7410) it wins only the >= 1566-
-// tile GEMMs (qkv 1.12x, FFN-up 1.05x) and loses the 580-tile ones (0.85-0.97x).  So: hipBLASLt
-// when the grid holds >= 1024 tiles (4 full rounds on 256 CUs), at any K (the 1.3B model's K = 1536
-// GEMMs: 1217-1300 TF/s against 707-797 on the 128^2 kernel, profiles/r1/gemm_bench_r1f.log).
-// hipBLASLt (autotuned per shape, blaslt.hip) vs the 256^2 MFMA kernel with its split tail, measured
-// per 14B block GEMM (profiles/r1/gemm_lt_tune_r1i.log, gemm_backend_ab_r1j.log): hipBLASLt wins on
-// every grid of >= 1024 256^2 tiles, and on 256-1023-tile grids (the SP=8 row counts 7410 and, per
-// CFG micro-batch, 3705) while K <= 8192 (1.01-1.32x); the K = 13824 FFN-down GEMM at those sizes
-// stays on the MFMA kernel (0.88-0.96x on hipBLASLt).  Grids of < 256 tiles with N >= 2048 and
-// 1024 <= K <= 8192 -- the per-step context GEMMs (fused cross k|v over 2 x 512 context rows, text
-// embedding), the time projection (M = 2) and the UMT5 layers -- also go to hipBLASLt: 1.05-2.4x
-// the 128^2 kernel (profiles/r1/gemm_backend_ab_ctx_r1s.log); the narrow head (N = 64) and the
-// patch embeddings (K = 64 / 384) are unmeasured there and stay on the MFMA kernels.
-// r2: on the private ROCm-7.2 hipBLASLt copy (blaslt.hip) the K = 13824 FFN-down at 3705 rows runs
-// at 0.404-0.411 ms against 0.466-0.474 on the MFMA kernel (profiles/r2/lt_lib_ab_r2l.log), so with
-// that library the 256-1023-tile grids go to hipBLASLt at any K.
+// Routing (r5): every GEMM of the path runs on the kernels of this file.  r1-r4 sent the plain-bias
+// q|k|v / cross-q projections, the GELU FFN-up and the context GEMMs at SP = 1 to a private copy of
+// ROCm's hipBLASLt (+ a separate epilogue pass), which beat the hand-written kernels there (r4: q|k|v
+// 1551 vs 1501 TF/s).  With the XCD tile queues the 4-wave kernel matches it on q|k|v (1529-1544 vs
+// 1547-1556 TF/s, within run-to-run spread), leads on every fused-epilogue shape (FFN-up 1488-1496
+// vs 1410-1413, o-proj 1438-1441 vs 1291-1296), reads fewer L2->fabric bytes on q|k|v (16.8 vs
+// 17.9 GB per dispatch), and the whole step is as fast: 0.3906 / 0.3882 vs 0.3888 / 0.3881 steps/s
+// with the library routes, same box, interleaved (profiles/r5/gemm_queue_ab_s2.log,
+// pmc_fetch_queue_s2.txt, bench_own_vs_lt_ab_s2.log).  The library route survives only in the A/B
+// build (-DVS_AB, `make ab`; VS_GEMM_BACKEND=lt there), never in libvstyler.so.
+#ifdef VS_AB
 bool vs_lt_is_private();
-// r3: the staggered 8-phase kernel beats the library (+ its epilogue pass) on the FFN GEMMs of the
-// Ulysses per-rank row counts (same box, profiles/r3/gemm_stagger_ab_s2.log): FFN-down (K = 13824,
-// gate-residual) at 3705 / 7410 / 14820 rows 1.02x / 1.14x / 1.13x, FFN-up (GELU epilogue) at
-// 3705 / 7410 rows 1.04x / 1.10x; the library keeps everything else (q|k|v 0.80-0.85x, o-proj
-// 0.92-0.99x, and every 14B GEMM at the SP = 1 row count, 0.85-0.95x).  With the 16-B epilogue the
-// o-proj (gate-residual, N = K = 5120) joins them at 7410 / 3705 rows: 0.336-0.339 vs 0.348-0.353 ms
-// and 0.189 vs 0.194 ms, four interleaved runs (profiles/r3/gemm_persist_ab.log); the library pays a
-// staging pass for a residual epilogue, so the rule keys on those.
-// With the DMA row offsets hoisted (+4-5 %, profiles/r3/gemm_preoff_ab.log) the kernel also passes
-// the library + its epilogue pass in isolation at the SP = 1 row count on FFN-up (6.150 vs 6.205
-// ms) and FFN-down (5.948 vs 6.018), but routing those two to it cost the graph-replayed step 1.4 %
-// (0.3831 / 0.3843 vs 0.3888 / 0.3894 steps/s, same box, interleaved; in the step the kernel ran
-// 6.38 ms per launch: profiles/r3/bench_own_sp1_ab.log, step_breakdown_own_sp1.txt), so the SP = 1
-// block GEMMs stay on the library.
-static bool use_4w();
-static bool own_wins(int m, int n, int k, int epilogue) {
-    const bool resid = epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES;
-    if ((k >= 12288 && m <= 16384) || (epilogue == VS_EPI_GELU && k <= 8192 && m <= 8192) ||
-        (resid && k <= 8192 && m <= 8192))
-        return true;
-    // r4, the persistent 4-wave kernel with one-instruction DMAs: the residual-epilogue GEMMs at every
-    // row count (59 280 rows: o-proj + gate-residual 1441 vs 1292 TF/s for the library + its epilogue
-    // pass, FFN-down 1475 vs 1426; profiles/r4/gemm_gm_w4_ab.log).  VS_GEMM_OWN: 0 = the r3 routing,
-    // 1 = + residual epilogues with K <= 8192, 2 (default) = + every residual epilogue, 3 = + the GELU
-    // FFN-up (1418 vs 1408 alone, -0.3 % in the step: bench_route2_ab.log)
-    const char* o = getenv("VS_GEMM_OWN");
-    const int lvl = o ? atoi(o) : 2;
-    if (!use_4w() || lvl <= 0) return false;
-    return (resid && k <= 8192) || (lvl >= 2 && resid) || (lvl >= 3 && epilogue == VS_EPI_GELU);
-}
+// A/B build only: VS_GEMM_BACKEND=lt sends every eligible GEMM (no LoRA phase) to hipBLASLt, =r4 the
+// r4 routing (plain-bias GEMMs of >= 1024 tiles, the GELU FFN-up, the small-grid context GEMMs)
 static bool lt_route(int m, int n, int k, int epilogue = VS_EPI_BIAS) {
     const char* e = getenv("VS_GEMM_BACKEND");
-    const int mode = !e ? 2 : (e[0] == 'v' ? 0 : (e[0] == 'l' ? 1 : 2));   // 0 never, 1 always, 2 auto
-    if (mode != 2) return mode == 1;
+    if (!e || (e[0] != 'l' && e[0] != 'r')) return false;
+    if (e[0] == 'l') return true;
+    const bool resid = epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES;
     const long long tiles = (long long)((m + 255) / 256) * ((n + 255) / 256);
-    if (k >= 4096 && tiles >= 240 && own_wins(m, n, k, epilogue)) return false;
+    if (resid || (k >= 12288 && m <= 16384) || (epilogue == VS_EPI_GELU && k <= 8192 && m <= 8192)) return false;
     return tiles >= 1024 || (tiles >= 256 && (k <= 8192 || vs_lt_is_private())) ||
            (k <= 8192 && n >= 2048 && k >= 1024);
+}
+static bool fp8_lt_route(int n, int k, int epilogue) {
+    const char* e = getenv("VS_GEMM_BACKEND");
+    return e && (e[0] == 'l' || (e[0] == 'r' && epilogue == VS_EPI_BIAS && n >= 2 * k));
 }
 
 // hipBLASLt for bf16(A W^T [* scale] + bias) (gemm(y, ldy)), then the rest of the epilogue with
@@ -1946,28 +1931,28 @@ static bool lt_with_epilogue(void* c, long long ldc, int m, int n, int epilogue,
     }
     return true;
 }
+#else
+static bool lt_route(int, int, int, int = VS_EPI_BIAS) { return false; }
+static bool fp8_lt_route(int, int, int) { return false; }
+#endif
 
-// which 256x256 kernel runs the un-split-phase (k2 == 0) GEMMs: VS_GEMM_KERNEL=4w (default since
-// r4: 1-5 % over the 8-phase kernel on every 14B shape at 59 280 and 7410 rows) | 8p
-static bool use_4w() {
-    const char* e = getenv("VS_GEMM_KERNEL");
-    return !(e && e[0] == '8');
-}
+// which 256x256 kernel runs the un-split-phase (k2 == 0) GEMMs: the 4-wave kernel (default since
+// r4: 1-5 % over the 8-phase kernel on every 14B shape at 59 280 and 7410 rows) | VS_OPT_GEMM_KERNEL 8
+static bool use_4w() { return vs_opt(VS_OPT_GEMM_KERNEL) == 4; }
 
 // the schedule of a 4-wave launch (W4Sched): one persistent block per CU when the main tiles fill
 // every CU and a tile has >= 3 K-tiles (the tile-id hand-off, see the schedule's comment), fed by the
-// XCD tile queues when the stream has a queue workspace (kind 5) bound (VS_GEMM_QUEUE=0: the static
-// lists, A/B)
+// XCD tile queues when the stream has a queue workspace (kind 5) bound (VS_OPT_GEMM_QUEUE 0: the
+// static lists)
 static W4Sched w4_sched(int nmain, int nt, hipStream_t stream) {
     W4Sched s{nullptr, 0, 0, 0};
-    const int cus = vs_cus_for_split(nullptr);
+    const int cus = vs_cus_for_split(false);
     if (cus >= 8 && cus % 8 == 0 && nmain >= cus && nt >= 3) {
         s.npers = cus;
         s.tp = nmain / cus;
     }
     s.nrem = nmain - s.npers * s.tp;
-    const char* e = getenv("VS_GEMM_QUEUE");
-    if (s.npers && s.tp >= 2 && !(e && e[0] == '0')) s.q = (unsigned*)vs_split_workspace(5, WQ_BYTES, stream);
+    if (s.npers && vs_opt(VS_OPT_GEMM_QUEUE)) s.q = (unsigned*)vs_split_workspace(5, WQ_BYTES, stream);
     return s;
 }
 static unsigned w4_grid(const W4Sched& s, const KSplit& sp) {
@@ -2016,27 +2001,23 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
     Epi ep;
     const int rc = fill_epi(ep, epilogue, epi, m, n);
     if (rc) return rc;
-    // 256x256 schedule once there are enough tiles to fill the chip, 128x128 otherwise
-    // (VSTYLER_GEMM_TILE=128|256 forces one for A/B measurements)
-    const char* tile_env = getenv("VSTYLER_GEMM_TILE");
-    const int force = tile_env ? atoi(tile_env) : 0;
+    // 256x256 schedule once the grid holds >= half a round of tiles (the 4-wave kernel from K = 1024:
+    // persistent from one full round, its next tile's first K-tiles loading under the current one's
+    // epilogue; the 8-phase kernel of the LoRA second phase from K = 4096), 128x128 otherwise
+    // (VS_OPT_GEMM_TILE forces one).  r5: the 1.3B model's K = 1536 block GEMMs run 1314-1497 TF/s on
+    // the 4-wave kernel against 606-861 on the 128x128 one (profiles/r5/gemm_ab_1p3b_s3.log), and the
+    // 160-tile context k|v GEMM (M = 1024, K = 4096) is one 4-wave round instead of 218 us of 128x128
+    const int force = vs_opt(VS_OPT_GEMM_TILE);
+    const long long tiles256 = (long long)((m + BT - 1) / BT) * ((n + BT - 1) / BT);
     const bool big = force ? force == 256
-                          : k >= 4096 && (long long)((m + BT - 1) / BT) * ((n + BT - 1) / BT) >= 240;
-    // GELU on the hipBLASLt route: the library's fused GELU_BIAS epilogue (GELU-tanh of the fp32
-    // acc + bias, one bf16 rounding) instead of bf16(acc + bias) + the gemm_epi_apply8 GELU pass: the
-    // 14B FFN-up 6.18 -> 5.79 ms (profiles/r2/lt_gelu_ab.log).  It drops the reference's bf16 rounding
-    // of the linear output before F.gelu: 35 % of outputs move by one bf16 ulp, closer to the exact
-    // GELU (0.8 % off its rounding vs 35 %).  Off by default (r3): the default keeps the reference's
-    // rounding points (bf16 linear output, then the GELU pass); VS_LT_GELU=1 selects the fused epilogue.
-    const char* lt_gelu = getenv("VS_LT_GELU");
-    if (k2 == 0 && epilogue == VS_EPI_GELU && (lt_gelu && lt_gelu[0] == '1') && lt_route(m, n, k, epilogue) &&
-        vs_lt_gemm_bias_gelu(a, lda, w, ldw, c, ldc, m, n, k, ep.bias, (hipStream_t)stream) == VS_OK)
-        return VS_OK;
+                           : (tiles256 >= 240 && k >= 4096) || (tiles256 >= 128 && k >= 1024 && k2 == 0 && use_4w());
+#ifdef VS_AB
     if (k2 == 0 && lt_route(m, n, k, epilogue) &&
         lt_with_epilogue(c, ldc, m, n, epilogue, ep, (hipStream_t)stream, [&](void* y, long long ldy) {
             return vs_lt_gemm_bias(a, lda, w, ldw, y, ldy, m, n, k, ep.bias, (hipStream_t)stream);
         }))
         return VS_OK;
+#endif
     if (big) {
         // 256x256 staggered 8-phase kernel (LoRA second phase included); the last partial round of
         // tiles runs as K pieces + combine (split tail)
@@ -2048,13 +2029,12 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
                 (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
             attr8 = true;
         }
-        // 16-B epilogue accesses when every epilogue operand allows them (VS_GEMM_WIDE=0: 8-B, A/B)
-        const char* we = getenv("VS_GEMM_WIDE");
-        const bool wide = !(we && we[0] == '0') && n % 8 == 0 && ldc % 8 == 0 && aligned16(c) &&
+        // 16-B epilogue accesses when every epilogue operand allows them
+        const bool wide = n % 8 == 0 && ldc % 8 == 0 && aligned16(c) &&
                           (!ep.bias || aligned16(ep.bias)) && (!ep.res || (ep.ld_res % 8 == 0 && aligned16(ep.res))) &&
                           (!ep.gate || (ep.gate_bstride % 8 == 0 && aligned16(ep.gate))) &&
                           (!ep.hint || (ep.ld_hint % 8 == 0 && aligned16(ep.hint)));
-        KSplit sp = k2 ? KSplit{tm * tn, 0, 1, 0} : plan_ksplit(tm * tn, k / 64, vs_cus_for_split("VS_GEMM_NO_SPLIT"), 64);
+        KSplit sp = k2 ? KSplit{tm * tn, 0, 1, 0} : plan_ksplit(tm * tn, k / 64, vs_cus_for_split(!vs_opt(VS_OPT_GEMM_SPLIT)), 64);
         float* part = nullptr;
         if (sp.ntail) {
             part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
@@ -2114,36 +2094,28 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
     return VS_OK;
 }
 
-static bool fp8_lt_route(int n, int k, int epilogue);
 extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, const void* w8, long long ldw,
                            void* c, long long ldc, int m, int n, int k, int epilogue, const vs_epilogue* epi,
                            void* stream) {
     if (!a8 || !scale_a || !w8 || !c || m <= 0 || n <= 0 || k <= 0) return VS_E_INVALID;
-    // K % 128 on both routes (the MFMA kernel's K-tile), so a shape never works on one backend only
+    // K % 128: the MFMA kernel's K-tile
     if (k % 128 || n % 4 || lda < k || ldw < k || ldc < n || (lda & 15) || (ldw & 15) || (ldc & 3))
         return VS_E_INVALID;
     if (!aligned16(a8) || !aligned16(w8) || !aligned8(c)) return VS_E_INVALID;
     Epi ep;
     const int rc = fill_epi(ep, epilogue, epi, m, n);
     if (rc) return rc;
-    // Routes (VS_FP8_BACKEND=auto (default) | vstyler | lt).  r4: the 4-wave MFMA kernel
-    // (gemm_fp8_tn_4w, one-instruction DMAs) runs the fused-epilogue block GEMMs ahead of hipBLASLt
-    // fp8 + its epilogue pass at 59 280 rows -- o-proj + gate-residual 2483 vs 2204 TF/s, FFN-up +
-    // GELU 2676 vs 2541, FFN-down + gate-residual 2883 vs 2803 -- and behind it only on the plain-bias
-    // q|k|v projection (2807 vs 3067, profiles/r4/gemm_fp8_w4_ab.log), so auto keeps the library for
-    // bias-only GEMMs with N >= 2K (the fused q|k|v) and runs everything else on the MFMA kernel; the
-    // routes are bit-identical (integer-data tests).  The MFMA kernel also runs when no workspace is
-    // bound.  GELU as in vs_gemm: hipBLASLt's fused GELU_BIAS epilogue only with VS_LT_GELU=1.
-    const char* lt_gelu = getenv("VS_LT_GELU");
-    const bool use_lt = fp8_lt_route(n, k, epilogue);
-    if (use_lt && epilogue == VS_EPI_GELU && (lt_gelu && lt_gelu[0] == '1') &&
-        vs_lt_gemm_fp8(a8, lda, scale_a, w8, ldw, c, ldc, m, n, k, ep.bias, true, (hipStream_t)stream) == VS_OK)
-        return VS_OK;
-    if (use_lt &&
+    // r4 kept hipBLASLt fp8 for the plain-bias q|k|v (2807 vs 3067 TF/s); with the XCD tile queues
+    // the 4-wave kernel runs it at 3013 vs 3068 and every fused-epilogue shape ahead of the library
+    // + its epilogue pass (FFN-up 2839 vs 2500, o-proj 2652 vs 2225: profiles/r5/
+    // gemm_fp8_queue_ab_s1.log), so every fp8 GEMM runs here (the library only in the A/B build)
+#ifdef VS_AB
+    if (fp8_lt_route(n, k, epilogue) &&
         lt_with_epilogue(c, ldc, m, n, epilogue, ep, (hipStream_t)stream, [&](void* y, long long ldy) {
             return vs_lt_gemm_fp8(a8, lda, scale_a, w8, ldw, y, ldy, m, n, k, ep.bias, false, (hipStream_t)stream);
         }))
         return VS_OK;
+#endif
     // the fp8 MFMA kernels (K-tiles of 128 fp8)
     const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
     static bool attr8 = false;
@@ -2151,14 +2123,13 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
         (void)hipFuncSetAttribute((const void*)gemm_fp8_tn_8p, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
         attr8 = true;
     }
-    KSplit sp = plan_ksplit(tm * tn, k / 128, vs_cus_for_split("VS_GEMM_NO_SPLIT"), 128);
+    KSplit sp = plan_ksplit(tm * tn, k / 128, vs_cus_for_split(!vs_opt(VS_OPT_GEMM_SPLIT)), 128);
     float* part = nullptr;
     if (sp.ntail) {
         part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
         if (!part) sp = KSplit{tm * tn, 0, 1, 0};
     }
-    const char* fk = getenv("VS_GEMM_KERNEL");      // the 4-wave kernel unless VS_GEMM_KERNEL=8p
-    if (!(fk && fk[0] == '8')) {
+    if (use_4w()) {                 // the 4-wave kernel unless VS_OPT_GEMM_KERNEL 8
         using KF4 = void (*)(const uint8_t*, long long, const float*, const uint8_t*, long long, bf16_t*, long long,
                              int, int, int, Epi, int, int, int, int, int, float*, W4Sched);
         // one instantiation per 16-B epilogue mode (index: mode, 5 = gate-residual + hint), 6: 8-B path
@@ -2208,21 +2179,13 @@ extern "C" int vs_quant_fp8_rows(const void* x, long long ldx, void* x8, long lo
     return VS_OK;
 }
 
-extern "C" int vs_gemm_route(int m, int n, int k) {
-    if (m <= 0 || n <= 0 || k <= 0) return VS_E_INVALID;
-    return lt_route(m, n, k) ? 1 : 0;
-}
-
-// the route of a GEMM with a given epilogue (the residual epilogues decide between the MFMA
-// kernel's fused epilogue and hipBLASLt's staged output + the fused residual-LayerNorm pass)
-static bool fp8_lt_route(int n, int k, int epilogue) {
-    const char* fb = getenv("VS_FP8_BACKEND");
-    return fb && fb[0] == 'v' ? false : fb && fb[0] == 'l' ? true : epilogue == VS_EPI_BIAS && n >= 2 * k;
-}
+// the route of a GEMM (include/vstyler.h): 0 = the MFMA kernels with the fused epilogue, the only
+// route of the product library; the A/B build reports its library route (1) as r4 did
 extern "C" int vs_gemm_route_epi(int m, int n, int k, int epilogue, int fp8) {
     if (m <= 0 || n <= 0 || k <= 0 || epilogue < VS_EPI_BIAS || epilogue > VS_EPI_RES) return -VS_E_INVALID;
     return (fp8 ? fp8_lt_route(n, k, epilogue) : lt_route(m, n, k, epilogue)) ? 1 : 0;
 }
+extern "C" int vs_gemm_route(int m, int n, int k) { return vs_gemm_route_epi(m, n, k, VS_EPI_BIAS, 0); }
 
 extern "C" int vs_gemm_split_plan(int m, int n, int k, int cus, int* out) {
     if (!out || m <= 0 || n <= 0 || k <= 0 || k % BK || cus < 0) return VS_E_INVALID;

@@ -263,16 +263,14 @@ int launch_conv_px(const vs_conv3d& p, long long M, hipStream_t st) {
     return VS_OK;
 }
 
-// VS_VAE_PXB=1|2 pixel blocks per wave, VS_VAE_PRE=1|2|3 register stages of the global->LDS
+// VS_OPT_VAE_PXB 1 | 2 pixel blocks per wave, VS_OPT_VAE_PRE 1 | 2 | 3 register stages of the global->LDS
 // pipeline (the im2col gathers are latency-bound: with one stage 256-pixel tiles ran 0.68x of
 // 128-pixel ones).  Default 2 / 3, measured at 832x480x73 (profiles/r2/vae_conv_ab.log): tiled encode
 // 452 -> 498 TF/s, decode 467 -> 518 TF/s.  All variants are bit-identical (same K order per output).
 template <int NB>
 int launch_conv(const vs_conv3d& p, long long M, hipStream_t st) {
-    const char* e1 = getenv("VS_VAE_PXB");
-    const char* e2 = getenv("VS_VAE_PRE");
-    const bool px2 = !(e1 && e1[0] == '1');
-    const int pre = e2 ? e2[0] - '0' : 3;
+    const bool px2 = vs_opt(VS_OPT_VAE_PXB) == 2;
+    const int pre = vs_opt(VS_OPT_VAE_PRE);
     if (px2) return pre == 3 ? launch_conv_px<NB, 2, 3>(p, M, st) : pre == 2 ? launch_conv_px<NB, 2, 2>(p, M, st)
                                                                              : launch_conv_px<NB, 2, 1>(p, M, st);
     return pre == 3 ? launch_conv_px<NB, 1, 3>(p, M, st) : pre == 2 ? launch_conv_px<NB, 1, 2>(p, M, st)

@@ -10,6 +10,10 @@ LIB_PATH = os.environ.get("VSTYLER_LIB", os.path.join(_HERE, "lib", "libvstyler.
 
 VS_EPI_BIAS, VS_EPI_GELU, VS_EPI_SILU, VS_EPI_GATE_RES, VS_EPI_RES = range(5)
 
+# path-selection options (include/vstyler.h VS_OPT_*): name -> id
+OPTIONS = {"gemm_tile": 0, "gemm_kernel": 1, "gemm_split": 2, "gemm_queue": 3, "attn_impl": 4, "attn_mfma": 5,
+           "attn_nc": 6, "attn_split": 7, "attn_persist": 8, "vae_pxb": 9, "vae_pre": 10}
+
 
 class VsEpilogue(ctypes.Structure):
     _fields_ = [
@@ -63,7 +67,8 @@ SIGNATURES = {
     "vs_gemm_route": [_I, _I, _I],
     "vs_gemm_route_epi": [_I, _I, _I, _I, _I],
     "vs_split_workspace_bytes": [_I],
-    "vs_blaslt_library": [],
+    "vs_set_option": [_I, _I],
+    "vs_get_option": [_I],
     "vs_split_workspace_bind": [_I, _P, _LL, _P],
     "vs_layernorm_modulate": [_P, _LL, _P, _LL, _I, _I, _I, _P, _P, _LL, _P, _P, _F, _P],
     "vs_residual_layernorm": [_P, _LL, _P, _LL, _P, _LL, _I, _I, _I, ctypes.POINTER(VsEpilogue), _I, _P, _P, _LL,
@@ -101,7 +106,7 @@ SIGNATURES = {
     "vs_sp_comm_destroy": [_P],
     "vs_sp_last_error": [],
 }
-_RESTYPES = {"vs_strerror": ctypes.c_char_p, "vs_blaslt_library": ctypes.c_char_p, "vs_split_workspace_bytes": ctypes.c_longlong,
+_RESTYPES = {"vs_strerror": ctypes.c_char_p, "vs_split_workspace_bytes": ctypes.c_longlong,
              "vs_sp_last_error": ctypes.c_char_p}
 
 _lib = None

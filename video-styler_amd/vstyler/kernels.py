@@ -18,6 +18,46 @@ def _stream(t):
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+def set_option(name, value):
+    """Select a path of libvstyler (include/vstyler.h VS_OPT_*, e.g. set_option("gemm_queue", 0));
+    returns the previous value.  The defaults are the product configuration; tests and A/B probes
+    use the others."""
+    prev = _lib.load().vs_set_option(_lib.OPTIONS[name], int(value))
+    if prev < 0:
+        raise ValueError(f"vs_set_option: bad option {name}={value}")
+    return prev
+
+
+def get_option(name):
+    return _lib.load().vs_get_option(_lib.OPTIONS[name])
+
+
+class options:
+    """Context manager: options(gemm_kernel=8, gemm_split=0) for the duration of a with-block."""
+
+    def __init__(self, **kw):
+        self.kw, self.saved = kw, {}
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            self.saved[k] = set_option(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.saved.items():
+            set_option(k, v)
+        return False
+
+
+def apply_env_options():
+    """VSTYLER_OPTS="gemm_queue=0,attn_nc=0": the one environment hook, read by the Python host (never
+    by the library) so that A/B scripts can select paths of a whole run."""
+    spec = os.environ.get("VSTYLER_OPTS", "")
+    for item in filter(None, (x.strip() for x in spec.split(","))):
+        name, _, value = item.partition("=")
+        set_option(name.strip(), int(value))
+
+
 _SPLIT_WS = {}
 
 
@@ -33,6 +73,8 @@ def _split_ws(kind, t, nbytes=None):
         if have is not None:
             return
         nbytes = _lib.load().vs_split_workspace_bytes(kind)
+        if nbytes <= 0:             # a kind this build does not use (2, 3: the A/B build's library route)
+            return
     elif have is not None and have.numel() >= nbytes:
         return
     if torch.cuda.is_current_stream_capturing():
@@ -107,10 +149,11 @@ def gemm(a, w, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, g
         _, _, ldw2 = _rows(w2, "w2")
     if k2 == 0:
         _split_ws(1, a)
-        _split_ws(2, a)
         _split_ws(5, a)
-        if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES) and _lt_route(M, N, K, epilogue):
-            _split_ws(3, a, M * N * 2)       # staging for the hipBLASLt route (vs_gemm decides)
+        if gemm_route(M, N, K, epilogue=epilogue):   # the A/B build's library route only
+            _split_ws(2, a)
+            if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES):
+                _split_ws(3, a, M * N * 2)
     _lib.check(_lib.load().vs_gemm(a.data_ptr(), lda, w.data_ptr(), ldw, out.data_ptr(), ldc, M, N, K,
                                    int(epilogue), ep, _ptr(a2), lda2, _ptr(w2), ldw2, k2, _stream(a)))
     return out
@@ -133,12 +176,6 @@ def quant_fp8_rows(x, x8, scale):
     return x8, scale
 
 
-def _lt_route(M, N, K, epilogue=None):
-    """vs_gemm's routing decision (vs_gemm_route[_epi]): the shim binds the epilogue staging buffer
-    for GEMMs that go to hipBLASLt."""
-    return gemm_route(M, N, K, epilogue=epilogue)
-
-
 def gemm_fp8(a8, scale_a, w8, out, epilogue=VS_EPI_BIAS, bias=None, residual=None, gate=None, gate_bstride=0,
              hint=None, hint_scale=1.0, alpha=1.0, rows_per_batch=0):
     """out = epilogue(scale_a[m] * (a8 @ w8^T)) with e4m3 operands (see vs_gemm_fp8)."""
@@ -150,7 +187,7 @@ def gemm_fp8(a8, scale_a, w8, out, epilogue=VS_EPI_BIAS, bias=None, residual=Non
     ep = _epilogue(bias, residual, gate, gate_bstride, hint, hint_scale, alpha, rows_per_batch)
     _split_ws(1, a8)                                                    # split tail of the MFMA kernel
     _split_ws(5, a8)                                                    # its tile queues
-    if not os.environ.get("VS_FP8_BACKEND", "").startswith("v"):   # hipBLASLt route (vs_gemm_fp8's own test)
+    if gemm_route(M, N, K, epilogue=epilogue, fp8=True):                # the A/B build's library route only
         _split_ws(2, a8)
         if epilogue in (VS_EPI_GATE_RES, VS_EPI_RES):
             _split_ws(3, a8, M * N * 2)
@@ -223,8 +260,10 @@ def residual_layernorm(y, x, out, eps=1e-6, epilogue=VS_EPI_GATE_RES, gate=None,
 
 
 def gemm_route(M, N, K, epilogue=None, fp8=False):
-    """True if vs_gemm (vs_gemm_fp8 with fp8=True) sends an (M, N, K) GEMM without LoRA phase and
-    with `epilogue` to hipBLASLt + a separate epilogue pass (vs_gemm_route / vs_gemm_route_epi)."""
+    """True if vs_gemm (vs_gemm_fp8 with fp8=True) runs an (M, N, K) GEMM without LoRA phase and with
+    `epilogue` as a staged product + a separate epilogue pass (vs_gemm_route / vs_gemm_route_epi):
+    never in the product library (every GEMM fuses its epilogue), the vendor-library route of the
+    A/B build (make ab)."""
     if epilogue is None and not fp8:
         return _lib.load().vs_gemm_route(int(M), int(N), int(K)) == 1
     ep = VS_EPI_BIAS if epilogue is None else int(epilogue)
@@ -313,6 +352,6 @@ def ulysses_permute(src, dst, batch, s_local, world, cols_per_rank, ld_local, js
     return dst
 
 
-__all__ = ["ulysses_permute", "gemm", "attention", "layernorm_modulate", "rmsnorm_rope", "patchify", "unpatchify", "cfg_euler",
+__all__ = ["set_option", "get_option", "options", "ulysses_permute", "gemm", "attention", "layernorm_modulate", "rmsnorm_rope", "patchify", "unpatchify", "cfg_euler",
            "time_sinusoid", "mod_add", "axpy", "VS_EPI_BIAS", "VS_EPI_GELU", "VS_EPI_SILU", "VS_EPI_GATE_RES",
            "VS_EPI_RES"]

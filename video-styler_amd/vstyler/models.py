@@ -57,12 +57,12 @@ def linear(lin, x, out, ws, **epi):
 
 
 def _fusable_lt(lin, M, epilogue):
-    """True when `lin` on M rows with the residual `epilogue` would run on hipBLASLt (vs_gemm /
-    vs_gemm_fp8's library route: vs_gemm_route_epi), i.e. when that epilogue is a separate pass over
-    a staged bf16(acc + bias) anyway: the pass then fuses with the LayerNorm that follows
-    (vs_residual_layernorm) with the same rounding points.  On the MFMA kernels the residual epilogue
-    is fused into the GEMM instead and the LayerNorm runs alone.  A hot-loaded LoRA keeps the MFMA
-    kernel's fused epilogue.  VSTYLER_FUSE_RES_LN=0 disables."""
+    """True when `lin` on M rows with the residual `epilogue` would run as a staged product + a separate
+    epilogue pass (vs_gemm_route_epi != 0: the vendor-library route of the A/B build only; the
+    product library fuses every epilogue), i.e. when that pass could fuse with the LayerNorm that
+    follows (vs_residual_layernorm) with the same rounding points.  Otherwise the residual epilogue is
+    fused into the GEMM and the LayerNorm runs alone.  A hot-loaded LoRA keeps the MFMA kernel's fused
+    epilogue.  VSTYLER_FUSE_RES_LN=0 disables."""
     if getattr(lin, "lora_A", None) is not None or os.environ.get("VSTYLER_FUSE_RES_LN", "1") == "0":
         return False
     fp8 = getattr(lin, "weight_fp8", None) is not None
