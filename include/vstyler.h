@@ -39,7 +39,7 @@ int vs_abi_version(void);
 #define VS_OPT_GEMM_TILE 0     /* 0 auto (default); 128 / 256: force the 128x128 / 256x256 schedule   */
 #define VS_OPT_GEMM_KERNEL 1   /* 4: the 4-wave 256x256 kernels (default); 8: the 8-phase ones         */
 #define VS_OPT_GEMM_SPLIT 2    /* 1: split tails (default); 0: whole-tile grids                        */
-#define VS_OPT_GEMM_QUEUE 3    /* 1: XCD tile queues (default; needs a kind-5 workspace); 0: static lists */
+#define VS_OPT_QUEUE 3         /* 1: XCD work queues of the persistent GEMMs / self-attention (default; a kind-5 workspace); 0: static lists */
 #define VS_OPT_ATTN_IMPL 4     /* 0: auto (default: 4-wave for >= 16 key tiles); 4 / 8 force a kernel  */
 #define VS_OPT_ATTN_MFMA 5     /* 16 (default) / 32: the 8-wave kernel's MFMA shape                     */
 #define VS_OPT_ATTN_NC 6       /* 1: optimistic softmax + checked redo (default); 0: checked only       */

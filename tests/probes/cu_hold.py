@@ -4,7 +4,7 @@ persistent compute grid launched meanwhile.  On one GPU: `cu_hold` (tests/probes
 workgroups of 64 KB LDS resident for D microseconds on a side stream, a short delay on the compute
 stream lets them land, then the measured kernel launches.  Per shape, the kernel's duration (HIP
 events on its stream) with k = 0, 8, 16, 32 held CUs and D = about half its own time, XCD tile queues
-vs the static per-CU lists (option gemm_queue), interleaved rounds.  Ideal (perfect balance): the
+vs the static per-CU lists (option queue), interleaved rounds.  Ideal (perfect balance): the
 k = 0 time x 256 / (256 - k) while the hog runs; a static list instead waits for the held CU's
 whole list (+ D).
 usage: python tests/probes/cu_hold.py   (env: CH_K=0,8,16,32)"""
@@ -57,7 +57,7 @@ def case(name, fn, variants):
 
 
 g = torch.Generator(device="cuda").manual_seed(1)
-GEMM = {"queue": dict(gemm_queue=1), "static": dict(gemm_queue=0)}
+GEMM = {"queue": dict(queue=1), "static": dict(queue=0)}      # (the attention's item queues too)
 for M, N, Kd, epi, name in ((59280, 13824, 5120, K.VS_EPI_GELU, "ffn-up 59280"), (7410, 15360, 5120, K.VS_EPI_BIAS,
                             "q|k|v 7410 (SP=8 rows)"), (7410, 5120, 13824, K.VS_EPI_BIAS, "ffn-down 7410")):
     a = torch.randn(M, Kd, device="cuda", generator=g).to(torch.bfloat16)
@@ -71,5 +71,5 @@ for H, name in ((5, "attention SP=8 (5 heads)"), (40, "attention SP=1 (40 heads)
     B, S = 2, 29640
     q, k_, v = (torch.randn(B * S, H * 128, device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
     o = torch.empty_like(q)
-    case(name, lambda: K.attention(q, k_, v, o, H, B), {"default": {}})
+    case(name, lambda: K.attention(q, k_, v, o, H, B), GEMM)
     del q, k_, v, o

@@ -59,7 +59,7 @@ for M in [int(v) for v in sys.argv[1:]] or (59280, 7410):
             os.environ["VS_GEMM_BACKEND"] = "lt" if v == "lt" else "own"     # read by the A/B build only
             K.set_option("gemm_tile", {"auto": 0, "t128": 128}.get(v, 256))
             K.set_option("gemm_kernel", 8 if v == "8p" else 4)
-            K.set_option("gemm_queue", 0 if v == "w4s" else 1)
+            K.set_option("queue", 0 if v == "w4s" else 1)
         t = {v: [] for v in VARIANTS}
         for v in VARIANTS:             # warm (hipBLASLt autotune happens here)
             setv(v); K.gemm(a, w, out, **kw); torch.cuda.synchronize()

@@ -38,7 +38,7 @@ for M in [int(v) for v in sys.argv[1:]] or (59280,):
         def setv(v):      # 8p = the 8-phase kernel, w4 / w4s = the 4-wave kernel (tile queues / static lists), lt = hipBLASLt fp8 (A/B build)
             os.environ["VS_GEMM_BACKEND"] = "lt" if v == "lt" else "own"     # read by the A/B build only
             K.set_option("gemm_kernel", 4 if v.startswith("w4") else 8)
-            K.set_option("gemm_queue", 0 if v == "w4s" else 1)
+            K.set_option("queue", 0 if v == "w4s" else 1)
         for v in VARIANTS:
             setv(v)
             K.gemm_fp8(a8, sc, w8, out, **kw); torch.cuda.synchronize()

@@ -176,14 +176,14 @@ def test_options_table():
     value returned, and kernels.options() restoring the table."""
     from vstyler import _lib, kernels as K
     lib = _lib.load()
-    defaults = {"gemm_tile": 0, "gemm_kernel": 4, "gemm_split": 1, "gemm_queue": 1, "attn_impl": 0,
+    defaults = {"gemm_tile": 0, "gemm_kernel": 4, "gemm_split": 1, "queue": 1, "attn_impl": 0,
                 "attn_mfma": 16, "attn_nc": 1, "attn_split": 1, "attn_persist": 1, "vae_pxb": 2, "vae_pre": 3}
     assert set(defaults) == set(_lib.OPTIONS)
     for name, v in defaults.items():
         assert K.get_option(name) == v, name
-    with K.options(gemm_kernel=8, gemm_queue=0, attn_mfma=32):
-        assert (K.get_option("gemm_kernel"), K.get_option("gemm_queue"), K.get_option("attn_mfma")) == (8, 0, 32)
-    assert (K.get_option("gemm_kernel"), K.get_option("gemm_queue"), K.get_option("attn_mfma")) == (4, 1, 16)
+    with K.options(gemm_kernel=8, queue=0, attn_mfma=32):
+        assert (K.get_option("gemm_kernel"), K.get_option("queue"), K.get_option("attn_mfma")) == (8, 0, 32)
+    assert (K.get_option("gemm_kernel"), K.get_option("queue"), K.get_option("attn_mfma")) == (4, 1, 16)
     for name, bad in (("gemm_tile", 64), ("gemm_kernel", 5), ("attn_mfma", 8), ("vae_pre", 4), ("gemm_split", 2)):
         with pytest.raises(ValueError):
             K.set_option(name, bad)

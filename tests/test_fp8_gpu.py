@@ -129,7 +129,7 @@ def test_gemm_fp8_schedules_agree(epi, opt):
     sc = torch.empty(M, dtype=torch.float32, device="cuda")
     K.quant_fp8_rows(x, x8, sc)
     outs = []
-    for o in (dict(gemm_kernel=4, gemm_queue=1), dict(gemm_kernel=4, gemm_queue=0), dict(gemm_kernel=8)):
+    for o in (dict(gemm_kernel=4, queue=1), dict(gemm_kernel=4, queue=0), dict(gemm_kernel=8)):
         opt(**o)
         out = res0.clone() if epi in ("gate_res", "res") else torch.empty(M, N, dtype=BF16, device="cuda")
         kw = dict(bias=b)

@@ -7,7 +7,7 @@ through LDS and the r5 XCD tile queues (own queue, stealing, remainder pool) -- 
 Integer-valued operands keep every fp32 sum exact, so every output must equal the exact product
 through each epilogue's reference rounding points (oracle/wan_oracle.py; reference linears
 wan_video_dit.py:131-134,157-160,209-210 via AutoWrappedLinear, vram_management/layers.py:115-188)
-bit for bit, under the queue schedule and the static lists (option gemm_queue=0), with ragged last tile
+bit for bit, under the queue schedule and the static lists (option queue=0), with ragged last tile
 rows / columns.  The queue words must be zero again after every launch (graph replays depend on it).
 """
 import pytest
@@ -25,7 +25,7 @@ def ints(*shape, g, lo=-3, hi=4):
 
 @pytest.fixture(params=["queue", "static"])
 def sched(opt, request):
-    opt(gemm_tile=256, gemm_kernel=4, gemm_queue=1 if request.param == "queue" else 0)
+    opt(gemm_tile=256, gemm_kernel=4, queue=1 if request.param == "queue" else 0)
     from vstyler import kernels
     return kernels
 
@@ -75,7 +75,7 @@ def test_gemm_4w_multitile_every_epilogue_exact(sched, M, N, Kd):
     x = res.cuda()
     K.gemm(a, w, x, epilogue=K.VS_EPI_RES, bias=b, residual=x, alpha=0.125)
     assert torch.equal(x.cpu(), O.add(res, O.bf(0.125 * yc.float())))
-    assert queue_words_zero(K) or K.get_option("gemm_queue") == 0
+    assert queue_words_zero(K) or K.get_option("queue") == 0
 
 
 @pytest.mark.parametrize("M,N,Kd", [(8200, 4104, 1024), (12300, 4104, 1024), (12300, 4104, 4096)])
@@ -109,10 +109,10 @@ def test_gemm_fp8_4w_multitile_exact(sched, M, N, Kd):
     K.gemm_fp8(x8, sc, w8, xo, epilogue=K.VS_EPI_GATE_RES, bias=b.cuda(), residual=xo, gate=gate.cuda(),
                gate_bstride=N, rows_per_batch=S, hint=hint.cuda(), hint_scale=0.5)
     assert torch.equal(xo.cpu(), ref)
-    assert queue_words_zero(K) or K.get_option("gemm_queue") == 0
+    assert queue_words_zero(K) or K.get_option("queue") == 0
 
 
-def test_gemm_queue_repeat_and_graph_replay_bit_identical(opt):
+def test_queue_repeat_and_graph_replay_bit_identical(opt):
     """The queue words return to zero after every launch, so back-to-back launches and hipGraph
     replays of a multi-tile GEMM give the eager result bit for bit (random data, 14B q|k|v-like N)."""
     from vstyler import kernels as K

@@ -160,8 +160,8 @@ def test_gemm_every_schedule_exact(K, opt):
         return outs
     ref = run(gemm_tile=128)
     assert torch.equal(ref[0], (a.float() @ w.float().t() + b.float()).to(BF16))
-    for o in (dict(gemm_tile=256, gemm_kernel=8), dict(gemm_tile=256, gemm_kernel=4, gemm_queue=1),
-              dict(gemm_tile=256, gemm_kernel=4, gemm_queue=0)):
+    for o in (dict(gemm_tile=256, gemm_kernel=8), dict(gemm_tile=256, gemm_kernel=4, queue=1),
+              dict(gemm_tile=256, gemm_kernel=4, queue=0)):
         for i, (x, y) in enumerate(zip(run(**o), ref)):
             assert torch.equal(x, y), (o, i)
 
@@ -574,3 +574,26 @@ def test_ulysses_permute_interleaved_rows(K):
     rows = send.view(P, Sl, 3, cpr)
     for i, t in enumerate(src):
         assert torch.equal(rows[:, :, i], t.reshape(Sl, P, cpr).permute(1, 0, 2))
+
+
+@pytest.mark.parametrize("B,Sq,Skv,H", [(2, 7700, 7700, 10), (2, 29640, 29640, 5), (1, 12000, 4200, 24)])
+def test_attention_item_queue_matches_static_lists(K, opt, B, Sq, Skv, H):
+    """attn_fwd_w4's persistent blocks fed by the XCD item queues (default) vs the static per-block
+    item lists (option queue=0): every item is computed the same way whichever block takes it, so
+    the outputs are bit-identical; the queue words are zero again after every launch (the last block
+    zeroes them), so repeated launches agree too.  (2, 29640, 29640, 5): the Ulysses SP = 8 rank shape."""
+    D = H * 128
+    g = torch.Generator(device="cuda").manual_seed(77)
+    q = torch.randn(B * Sq, D, device="cuda", generator=g).to(BF16)
+    k = torch.randn(B * Skv, D, device="cuda", generator=g).to(BF16)
+    v = torch.randn(B * Skv, D, device="cuda", generator=g).to(BF16)
+    outs = []
+    for qopt in (1, 1, 0):
+        opt(queue=qopt)
+        o = torch.empty_like(q)
+        K.attention(q, k, v, o, H, B)
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    bufs = [b for (kind, _, _), b in K._SPLIT_WS.items() if kind == 5]
+    assert bufs and all(int(b.count_nonzero()) == 0 for b in bufs)

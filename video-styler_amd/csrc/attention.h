@@ -36,6 +36,7 @@ struct AttnArgs {
     float c;
     int Sq, Skv, H, nqb, nmain, npers, nsplit, piece_tiles;
     int nc_cap;      // items the flag workspace holds (its list and its flags)
+    unsigned* queue; // attn_fwd_w4's XCD item queues (workspace kind 5 + VS_Q_ATTN words), or null
 };
 
 // Item-flag workspace (kind 4, ints; count, done and flags zero between launches): [0] count of

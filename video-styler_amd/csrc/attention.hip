@@ -1028,7 +1028,7 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
     const long long grid = (long long)npers + (long long)sp.ntail * sp.nsplit;
     AttnArgs args{(const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, bsq, bsk, bsv, bso,
                   ldq, ldk, ldv, ldo, part, flags, c, sq, skv, heads, nqb, sp.nmain, npers, sp.nsplit,
-                  sp.piece_tiles, nc_cap};
+                  sp.piece_tiles, nc_cap, nullptr};
     auto pick = [&](int mode) -> void (*)(AttnArgs) {
         constexpr int C = MODE_CHK, N = MODE_NC, R = MODE_REDO;
         if (mode == R) return rebase ? attn_fwd_d128<true, true, R> : attn_fwd_d128<false, true, R>;
@@ -1052,6 +1052,12 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
     // the 4-wave pipeline's per-item fill and drain are a large share of an 8-tile item)
     const int impl = vs_opt(VS_OPT_ATTN_IMPL);
     const bool w4 = flags && (impl ? impl == 4 : nkv >= 16);
+    // attn_fwd_w4's persistent blocks take their items from XCD queues (kind-5 workspace, words from
+    // VS_Q_ATTN) when there is more than one item per block (VS_OPT_QUEUE 0: static lists)
+    if (w4 && npers < sp.nmain && nkv >= 16 && vs_opt(VS_OPT_QUEUE)) {
+        unsigned* qw = (unsigned*)vs_split_workspace(5, 4096, (hipStream_t)stream);
+        if (qw) args.queue = qw + VS_Q_ATTN;
+    }
     if (w4) {
         if (attn_w4_launch(args, rebase, (unsigned)grid, (hipStream_t)stream) != hipSuccess) return VS_E_LAUNCH;
     } else if (!launch(pick(flags ? MODE_NC : MODE_CHK), grid, args)) {
@@ -1068,6 +1074,7 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
         // redo: the checked kernel over the listed items, one block per CU walking the list (with
         // none listed every block returns at once); leaves the workspace's count and flags zero
         AttnArgs r = args;
+        r.queue = nullptr;
         r.part = nullptr;
         r.nsplit = 1;
         r.piece_tiles = 0;

@@ -47,15 +47,62 @@ constexpr int W4_THR = 256;
 constexpr int W4_TILE = BKV * HD * 2;      // 16 KB: one K or V tile
 constexpr int W4_SLOT = 2 * W4_TILE;
 constexpr int W4_LDS = 4 * W4_SLOT;        // 128 KB
+constexpr int W4_QSLOT = W4_LDS;           // the next item's id (LDS word, the item hand-off)
 #ifdef VS_W4_STAMPS
 // diagnostic build: s_memtime at the phase boundaries of the pipelined loop (iterations 8..39 of
 // block 0, every wave): 0 start of A, 1 end of A, 2 end of B, 3 end of C, 4 after the barrier, 5 end
 // of D, 6 after D step 3; kept in an LDS tail, copied out at the end (tests/probes/w4_stamps.py)
 __device__ unsigned long long g_w4_stamps[4][32][7];
-constexpr int W4_LDS_ALLOC = W4_LDS + 4 * 32 * 7 * 8;
+constexpr int W4_STAMP_OFF = W4_LDS + 16;
+constexpr int W4_LDS_ALLOC = W4_STAMP_OFF + 4 * 32 * 7 * 8;
 #else
-constexpr int W4_LDS_ALLOC = W4_LDS;
+constexpr int W4_LDS_ALLOC = W4_LDS + 16;
 #endif
+
+// Items of the persistent blocks (r5): XCD x owns the contiguous chunk [cs, cs + csz) of the item
+// list and gs persistent blocks (block b: XCD b % 8, slot b / 8 < gs).  A block takes its items from
+// the XCD's queue (positions cs + t, head word q[x]), then from other XCDs' queues (probed in ring
+// order) -- or, without a queue, walks the static list cs + slot + j gs (r1-r4), where a block whose
+// CU is held by another kernel (RCCL under the Ulysses overlap) delays its whole list: +24-38 % on
+// the self-attention with 8-32 CUs held for half its time (profiles/r5/cu_hold_s4.log).  The first
+// item costs one atomic round trip; after that wave 0 takes the id of the item after next at an
+// item switch (its atomic under the next item's Q loads), hands it to the other waves through an
+// LDS word read in the next item's first tile, and the K/V DMA cursor moves to it when it leaves
+// that item, hundreds of tiles later.  The last persistent block to finish zeroes the queue words.
+struct AttnChunks {
+    int nmain, npers;
+    __device__ __forceinline__ void of(int x, int& cs, int& csz, int& gs) const {
+        const int qx = nmain >> 3, rx = nmain & 7, qb = npers >> 3, rb = npers & 7;
+        cs = x < rx ? x * (qx + 1) : rx * (qx + 1) + (x - rx) * qx;
+        csz = qx + (x < rx ? 1 : 0);
+        gs = qb + (x < rb ? 1 : 0);
+    }
+    // the item after `nxt` (wave 0, all lanes; t0 = lane 0's returned own-queue head): -1 if none
+    __device__ __forceinline__ int take(unsigned* q, unsigned t0, int nxt, int lane) const {
+        const int x = blockIdx.x & 7;
+        int cs, csz, gs;
+        of(x, cs, csz, gs);
+        if (!q) return nxt + gs < cs + csz ? nxt + gs : -1;
+        const unsigned t = vs_queue_value<0>(t0);
+        if ((int)t < csz) return cs + (int)t;
+        for (int it = 0; it < 16; ++it) {          // other XCDs' queues, first live one in ring order
+            int vcs, vcsz, vgs;
+            of((x + 1 + lane) & 7, vcs, vcsz, vgs);
+            unsigned h = 0x7fffffff;
+            if (lane < 7) h = __hip_atomic_load(q + ((x + 1 + lane) & 7) * VS_Q_LINE, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long live = __ballot(lane < 7 && (int)h < vcsz);
+            if (!live) return -1;
+            const int v = (x + 1 + (int)__builtin_ctzll(live)) & 7;
+            unsigned tv = 0;
+            if (lane == 0) tv = vs_queue_add(q + v * VS_Q_LINE);
+            tv = (unsigned)__builtin_amdgcn_readfirstlane((int)tv);
+            of(v, vcs, vcsz, vgs);
+            if ((int)tv < vcsz) return vcs + (int)tv;
+        }
+        return -1;
+    }
+};
 
 template <bool REBASE>
 __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
@@ -67,35 +114,43 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
     const long long ldq = args.ldq, ldk = args.ldk, ldv = args.ldv, ldo = args.ldo;
     const float c = args.c;
 
-    // item list: identical to attn_fwd_d128 (persistent blocks stride over XCD-contiguous ranges,
-    // the blocks after npers run the split-tail pieces)
+    // items: the persistent blocks' XCD chunks and queues (AttnChunks), the blocks after npers run
+    // the split-tail pieces (one item each)
     int piece = -1, kv_begin = 0, Skv = Skv_all;
-    int g0, gstride, n_items;
-    if ((int)blockIdx.x < npers) {
-        const int x = blockIdx.x & 7, lb = blockIdx.x >> 3;
-        const int qx = nmain >> 3, rx = nmain & 7, qbk = npers >> 3, rbk = npers & 7;
-        const int cs = x < rx ? x * (qx + 1) : rx * (qx + 1) + (x - rx) * qx;
-        const int csz = qx + (x < rx ? 1 : 0);
-        gstride = qbk + (x < rbk ? 1 : 0);
-        g0 = cs + lb;
-        n_items = lb < csz ? (csz - lb + gstride - 1) / gstride : 0;
+    int cur;                                       // the item being computed
+    const bool pers = (int)blockIdx.x < npers;
+    const AttnChunks chunks{nmain, npers};
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (pers) {
+        int cs, csz, gs;
+        chunks.of(blockIdx.x & 7, cs, csz, gs);
+        cur = (int)(blockIdx.x >> 3) < csz ? cs + (int)(blockIdx.x >> 3) : -1;
     } else {
         const int t = blockIdx.x - npers;
-        g0 = nmain + t / nsplit;
-        gstride = 0;
-        n_items = 1;
+        cur = nmain + t / nsplit;
         piece = t % nsplit;
         kv_begin = piece * piece_tiles * BKV;
         Skv = min(Skv_all - kv_begin, piece_tiles * BKV);
     }
-    if (n_items == 0) return;
-    const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (pers && args.queue) {                      // the first item from the queues too
+        volatile LDS_AS int* qs = (volatile LDS_AS int*)(uintptr_t)((unsigned)(uintptr_t)smem + W4_QSLOT);
+        if (wave == 0) {
+            const unsigned t0 = vs_queue_issue(args.queue + (blockIdx.x & 7) * VS_Q_LINE);
+            const int id = chunks.take(args.queue, t0, -1, lane);
+            if (lane == 0) *qs = id;
+        }
+        __syncthreads();
+        cur = __builtin_amdgcn_readfirstlane(*qs);
+    }
+    if (cur < 0) {                                 // (a persistent block with no item: counted out)
+        if (pers && args.queue && tid == 0) vs_queue_done(args.queue, 9, npers);
+        return;
+    }
     const int r = lane & 31, hh = lane >> 5;
 
-    auto item_bh = [&](int j, int& qrow0) {
+    auto item_bh = [&](int g, int& qrow0) {
         const int nqb = cold->nqb;
-        const int g = g0 + j * gstride;
         qrow0 = (g % nqb) * BQ;
         return g / nqb;
     };
@@ -139,10 +194,11 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
         asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                      :: "s"(lds), "v"(voff), "s"(rs), "s"(soff) : "m0");
     };
-    int lj = 0, li = 0;
+    int li = 0;
+    int dnext = -1;                 // the item the DMA cursor moves to after the current one (-1: none)
     int qrow_unused;
-    const bf16_t* Kl = k_base(item_bh(0, qrow_unused));
-    const bf16_t* Vl = v_base(item_bh(0, qrow_unused));
+    const bf16_t* Kl = k_base(item_bh(cur, qrow_unused));
+    const bf16_t* Vl = v_base(item_bh(cur, qrow_unused));
     i32x4_t krs = slab_rsrc(Kl, ldk32), vrs = slab_rsrc(Vl, ldv32);
     const unsigned lds0 = (unsigned)(uintptr_t)smem + wave * 16 * 256;
     // stage(T) = stage_piece(T, 0..7) (K rows, then V rows, 4 rows per piece) + stage_next()
@@ -186,12 +242,13 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
     auto stage_next = [&]() __attribute__((always_inline)) {
         if (++li == nkv) {
             li = 0;
-            if (++lj < n_items) {
-                const int bh = item_bh(lj, qrow_unused);
+            if (dnext >= 0) {
+                const int bh = item_bh(dnext, qrow_unused);
                 Kl = k_base(bh);
                 Vl = v_base(bh);
                 krs = slab_rsrc(Kl, ldk32);
                 vrs = slab_rsrc(Vl, ldv32);
+                dnext = -1;
             }
         }
     };
@@ -348,7 +405,7 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
         if (st >= 0 && lane == 0)
             for (int k = lo; k < hi; ++k)
                 *reinterpret_cast<volatile LDS_AS unsigned long long*>(
-                    (LDS_AS char*)(uintptr_t)(smem_base + W4_LDS + 8 * ((wave * 32 + st) * 7 + k))) = stv[k];
+                    (LDS_AS char*)(uintptr_t)(smem_base + W4_STAMP_OFF + 8 * ((wave * 32 + st) * 7 + k))) = stv[k];
     };
 #else
     auto stamp = [](int) {};
@@ -427,6 +484,7 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
 #endif
         stage_begin(T + 3);
     };
+    int nxt = -1, qv = 0;           // the next item (from the LDS word, read in an item's first tile)
     // one iteration on tile T; FIRST: the item's first tile (no PV, no previous softmax)
     auto iteration = [&](int T, f32x16_t (&s1c)[2], const f32x16_t (&s1p)[2], u32x4_t (&p0c)[2][2],
                          const u32x4_t (&p0p)[2][2], auto first_c) __attribute__((always_inline)) {
@@ -489,6 +547,8 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
         for (int i = 0; i < 8; ++i) {                                   // D
             if (FIRST) stage_piece(i);
             else piece_go(i);
+            if (FIRST && i == 0)            // the item after this one (written by wave 0 before B(T+1))
+                qv = *(volatile LDS_AS int*)(uintptr_t)(smem_base + W4_QSLOT);
             rdK(kf0[i], T + 1, 0, i);
             if (!FIRST) {
                 mfV1(vfb[i], p1, i >> 2, i & 3, 0);
@@ -503,6 +563,10 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
 #endif
         }
         stamp(5);
+        if constexpr (FIRST) {
+            nxt = __builtin_amdgcn_readfirstlane(qv);
+            dnext = nxt;
+        }
         stage_next();
     };
     // after the item's last tile TL: S(TL) kb1 -> P ks2,3, PV(TL)
@@ -534,10 +598,22 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) rdK(kf0[i], 0, 0, i);
     int T = 0, q0 = 0;
-    int bh = item_bh(0, q0);
+    int bh = item_bh(cur, q0);
     q0 += 64 * wave;
-    load_q(q_base(bh), q0);
-    for (int jt = 0; jt < n_items; ++jt) {
+    // wave 0 takes the item after `after` (AttnChunks): the queue atomic goes out before the next Q's
+    // loads, which retire it (they complete in issue order), and its id into the LDS word
+    unsigned* const qw = pers ? args.queue : nullptr;
+    auto next_q = [&](int after) __attribute__((always_inline)) {
+        unsigned t0 = 0;
+        if (qw && wave == 0) t0 = vs_queue_issue(qw + (blockIdx.x & 7) * VS_Q_LINE);
+        load_q(q_base(bh), q0);
+        if (wave == 0) {
+            const int id = pers ? chunks.take(qw, t0, after, lane) : -1;
+            if (lane == 0) *(volatile LDS_AS int*)(uintptr_t)(smem_base + W4_QSLOT) = id;
+        }
+    };
+    next_q(cur);
+    for (;;) {
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
             lsum[rb] = 0.f;
@@ -556,29 +632,32 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
             ++T;
         }
         const int bh_done = bh, q0_done = q0;
-        if (jt + 1 < n_items) {          // the next item's Q (its QK starts after the drain)
-            bh = item_bh(jt + 1, q0);
+        if (nxt >= 0) {                  // the next item's Q (its QK starts after the drain)
+            bh = item_bh(nxt, q0);
             q0 += 64 * wave;
         }
         if (t < nkv) {
             iteration(T, s1b, s1a, p0b, p0a, std::false_type{});
             ++T;
-            if (jt + 1 < n_items) load_q(q_base(bh), q0);
+            if (nxt >= 0) next_q(nxt);
             drain(T - 1, s1b, p0b);
         } else {
-            if (jt + 1 < n_items) load_q(q_base(bh), q0);
+            if (nxt >= 0) next_q(nxt);
             drain(T - 1, s1a, p0a);
         }
-        finish(o_base(bh_done), q0_done, g0 + jt * gstride);
+        finish(o_base(bh_done), q0_done, cur);
+        if (nxt < 0) break;
+        cur = nxt;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (qw && tid == 0) vs_queue_done(qw, 9, npers);
 #ifdef VS_W4_STAMPS
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     stamp_store(st_it, 4, 7);
     __syncthreads();
     if (blockIdx.x == 0)
         for (int i = lane; i < 32 * 7; i += 64)
-            (&g_w4_stamps[wave][0][0])[i] = *reinterpret_cast<volatile unsigned long long*>(smem + W4_LDS + 8 * (wave * 32 * 7 + i));
+            (&g_w4_stamps[wave][0][0])[i] = *reinterpret_cast<volatile unsigned long long*>(smem + W4_STAMP_OFF + 8 * (wave * 32 * 7 + i));
 #endif
 }
 

@@ -67,6 +67,44 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 inline volatile int g_vs_opt[VS_OPT_COUNT] = {0, 4, 1, 1, 0, 16, 1, 1, 1, 2, 3};
 inline int vs_opt(int id) { return g_vs_opt[id]; }
 
+// ---- work queues of the persistent kernels (gemm.hip W4Grab, attention_w4.hip): head words in a
+// caller-bound zeroed workspace (kind 5), one 128-B line each; the last block of a launch zeroes them.
+constexpr int VS_Q_LINE = 32;                 // words per line
+constexpr int VS_Q_ATTN = 16 * VS_Q_LINE;     // attention's words start 2 KB into the workspace
+
+// One returning device-scope atomic add of 1 by lane 0 of the calling wave (EXEC set to lane 0 inside
+// the asm, so no exec-masked region for the compiler to merge around the result).  Inline asm: as a
+// compiler-visible atomic its value's first use made the compiler drain every in-flight load first
+// (vmcnt(0)); the caller retires it with a counted wait instead (vs_queue_value).
+__device__ __forceinline__ unsigned vs_queue_issue(unsigned* p) {
+    unsigned t;
+    unsigned long long sv;
+    asm volatile("s_mov_b64 %1, exec\n\t"
+                 "s_mov_b64 exec, 1\n\t"
+                 "global_atomic_add %0, %2, %3, %4 sc0\n\t"
+                 "s_mov_b64 exec, %1"
+                 : "=&v"(t), "=&s"(sv)
+                 : "v"(0), "v"(1u), "s"(p)
+                 : "memory");
+    return t;
+}
+// lane 0's returned value, wave-uniform, after vmcnt(W): the caller has issued at least W vector
+// memory operations since vs_queue_issue (they complete in issue order)
+template <int W>
+__device__ __forceinline__ unsigned vs_queue_value(unsigned t0) {
+    unsigned t;
+    asm volatile("s_waitcnt vmcnt(%1)\n\tv_readfirstlane_b32 %0, %2" : "=s"(t) : "n"(W), "v"(t0) : "memory");
+    return t;
+}
+__device__ __forceinline__ unsigned vs_queue_add(unsigned* p) {
+    return __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// after a persistent block's last item: the last of `nblocks` to get here zeroes `nlines` lines
+__device__ __forceinline__ void vs_queue_done(unsigned* q, int nlines, int nblocks) {
+    if (vs_queue_add(q + (nlines - 1) * VS_Q_LINE) == (unsigned)nblocks - 1)
+        for (int i = 0; i < nlines; ++i) __hip_atomic_store(q + i * VS_Q_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // compute units of the current device (0 when unknown or when `off`: no split)
 inline int vs_cus_for_split(bool off) {
     if (off) return 0;

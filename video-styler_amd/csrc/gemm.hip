@@ -833,28 +833,30 @@ static_assert(4 * W4_ROWB == 0x1080, "the 4w kernel's M0 step");
 // dispatch) in slot s = b / 8 and computes tiles of its XCD's contiguous id range [x R, (x+1) R),
 // R = G8 tp (G8 = npers / 8), as ONE stream of K-tiles: the DMA runs two K-tiles ahead straight
 // across tile boundaries, so a tile's first K-tiles land during the previous tile's last K-tiles
-// and its epilogue.  A block's first tile is fixed (range position s); every later one it takes
-// from its XCD's queue (head word q[x]: positions G8 + t, t = 0, 1, ..), then, once that has run
-// dry, from the other XCDs' queues (probed in ring order), then from the remainder pool (the nrem
-// whole tiles past npers tp, head q[8]).  So a block that starts late -- its CU held by another
-// kernel -- finds the queues drained and computes its one fixed tile.
+// and its epilogue.  A block takes every tile from its XCD's queue (head word q[x]: range positions
+// t = 0, 1, ..), then, once that has run dry, from the other XCDs' queues (probed in ring order),
+// then from the remainder pool (the nrem whole tiles past npers tp, head q[8]).  A block that starts
+// late -- its CU held by another kernel, e.g. RCCL under the Ulysses overlap -- finds the queues
+// drained and exits (r5 measured a fixed first tile per block: the held blocks' first tiles then
+// ran after the hog, +19 % on an SP = 8 FFN-down with 8-32 CUs held, profiles/r5/cu_hold_s4.log).
 //   r4 walked a static list (positions s, s + G8, s + 2 G8, ..).  Over a 54-tile list an XCD's CUs
 //   drifted apart, so the 32 tiles in flight on an XCD stopped being one 4 x 8 block sharing its A / W
 //   slices in L2 (FFN-up: 23.1 GB of fabric reads per dispatch against the library's 13.1,
 //   profiles/r4/pmc_fetch_rows.txt), and a CU held by a concurrent kernel (RCCL under the Ulysses
 //   overlap) delayed its whole list.  With the queue the tiles computing on an XCD are always about
 //   the 32 most recently taken ids, and a CU that is slow or held simply takes fewer.
-// The next tile id is known one tile ahead: wave 0 takes it during tile k's epilogue (its atomic
-// issued at the epilogue's start and its value used at the end, under the stores) -- the second
-// tile's under the prologue's DMAs -- writes it to an LDS word, and every wave reads that word in
-// tile k+1's first K-tile behind a barrier, before the DMA cursor crosses into tile k+2 at the end
-// of K-tile nt - 3 (nt >= 3, host-checked).  The last
+// The first tile costs one atomic round trip before the prologue; after that the next tile id is
+// known one tile ahead: wave 0 takes it during tile k's epilogue (its atomic issued at the
+// epilogue's start and its value used at the end, under the stores) -- the second tile's under the
+// prologue's DMAs -- writes it to an LDS word, and every wave reads that word in tile k+1's first
+// K-tile behind a barrier, before the DMA cursor crosses into tile k+2 at the end of K-tile nt - 3
+// (nt >= 3, host-checked).  The last
 // persistent block to finish (exit count q[9]) zeroes the queue words, so every launch finds them
 // zero (workspace kind 5: bound zeroed, one per stream, so graph replays and concurrent streams are
 // safe).  Without a bound queue the same walk runs the static list and the nrem whole tiles get
 // blocks of their own.  The blocks after those run the split-tail K pieces of the last tiles.
 // ---------------------------------------------------------------------------------------------
-constexpr int WQ_LINE = 32;                   // queue words 128 B apart (a line each)
+constexpr int WQ_LINE = VS_Q_LINE;            // queue words 128 B apart (a line each, common.h)
 constexpr int WQ_BYTES = 10 * WQ_LINE * 4;    // 8 XCD heads, the remainder head, the exit count
 struct W4Sched {
     unsigned* q;      // queue words (null: static lists)
@@ -890,9 +892,7 @@ __device__ __forceinline__ W4Work w4_work(const W4Sched& sc, int K, int nmain, i
     }
     return w;
 }
-__device__ __forceinline__ unsigned wq_add(unsigned* p) {
-    return __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+__device__ __forceinline__ unsigned wq_add(unsigned* p) { return vs_queue_add(p); }
 // The tile taking of one persistent block (wave 0; see the schedule above).  issue(): the atomic on
 // the XCD's head, lane 0 only, at the start of an epilogue; finish<W>(): the tile id (-1: none
 // left), wave-uniform, at its end.  The head atomic is inline asm that sets EXEC to lane 0 itself:
@@ -911,15 +911,7 @@ struct W4Grab {
     unsigned t0 = 0;
     __device__ __forceinline__ explicit W4Grab(const W4Sched& s) : sc(s) {}
     __device__ __forceinline__ void issue() {
-        if (!sc.q || !local) return;
-        unsigned long long sv;
-        asm volatile("s_mov_b64 %1, exec\n\t"
-                     "s_mov_b64 exec, 1\n\t"
-                     "global_atomic_add %0, %2, %3, %4 sc0\n\t"
-                     "s_mov_b64 exec, %1"
-                     : "=&v"(t0), "=&s"(sv)
-                     : "v"(0), "v"(1u), "s"(sc.q + (blockIdx.x & 7) * WQ_LINE)
-                     : "memory");
+        if (sc.q && local) t0 = vs_queue_issue(sc.q + (blockIdx.x & 7) * WQ_LINE);
     }
     template <int W>
     __device__ __forceinline__ int finish(int lane) {
@@ -929,11 +921,10 @@ struct W4Grab {
             ++k;
             return id;
         }
-        const unsigned qlen = (unsigned)(g8 * (sc.tp - 1));
+        const unsigned qlen = (unsigned)(g8 * sc.tp);
         if (local) {
-            unsigned t;
-            asm volatile("s_waitcnt vmcnt(%1)\n\tv_readfirstlane_b32 %0, %2" : "=s"(t) : "n"(W), "v"(t0) : "memory");
-            if (t < qlen) return x * g8 * sc.tp + g8 + (int)t;
+            const unsigned t = vs_queue_value<W>(t0);
+            if (t < qlen) return x * g8 * sc.tp + (int)t;
             local = false;
         }
         // other XCDs' queues: lanes 0-6 probe heads x+1 .. x+7, the first live one in ring order is
@@ -951,7 +942,7 @@ struct W4Grab {
             unsigned t = 0;
             if (lane == 0) t = wq_add(sc.q + v * WQ_LINE);
             t = (unsigned)__builtin_amdgcn_readfirstlane((int)t);
-            if (t < qlen) return v * g8 * sc.tp + g8 + (int)t;
+            if (t < qlen) return v * g8 * sc.tp + (int)t;
         }
         steal = false;
         if (sc.nrem > 0) {
@@ -964,9 +955,7 @@ struct W4Grab {
     }
     // after the block's last tile: the last persistent block to finish zeroes the queue words
     __device__ __forceinline__ void done(int tid) {
-        if (!sc.q || (int)blockIdx.x >= sc.npers || tid != 0) return;
-        if (wq_add(sc.q + 9 * WQ_LINE) == (unsigned)sc.npers - 1)
-            for (int i = 0; i < 10; ++i) __hip_atomic_store(sc.q + i * WQ_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (sc.q && (int)blockIdx.x < sc.npers && tid == 0) vs_queue_done(sc.q, 10, sc.npers);
     }
 };
 
@@ -1136,9 +1125,22 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     // instantiation issues: 32 16-B stores, + 32 residual loads (the split-K piece path: 64 stores).
     constexpr int EPI_OPS = (MODE == VS_EPI_GATE_RES || MODE == VS_EPI_RES) ? 64 : 32;
     // prologue: K-tiles 0 and 1 of the stream in flight (W then A each), then the k-step-0 fragments
+    const bool dyn = sc.q && (int)blockIdx.x < sc.npers;    // a persistent block fed by the queues
+    if (dyn) {              // the first tile from the queues too (a block that starts late: none left)
+        if (wave == 0) {
+            grab.issue();
+            const int id = grab.finish<0>(lane);
+            if (lane == 0) slot_ref() = id;
+        }
+        __syncthreads();
+        cur = __builtin_amdgcn_readfirstlane(slot_ref());
+        if (cur < 0) {
+            grab.done(tid);
+            return;
+        }
+    }
     dma_tile(cur);
     ktile_rsrc(0);
-    const bool dyn = sc.q && (int)blockIdx.x < sc.npers;    // a persistent block fed by the queues
     if (dyn && wave == 0) grab.issue();                       // the second tile, under the prologue
 #pragma unroll
     for (int d = 0; d < 16; ++d) dma_now(d);
@@ -1660,8 +1662,21 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
     };
 
     // prologue: K-tiles 0 and 1 of the stream in flight, then the early fragments of K-tile 0
-    dma_tile(cur);
     const bool dyn = sc.q && (int)blockIdx.x < sc.npers;    // a persistent block fed by the queues
+    if (dyn) {              // the first tile from the queues too (a block that starts late: none left)
+        if (wave == 0) {
+            grab.issue();
+            const int id = grab.finish<0>(lane);
+            if (lane == 0) slot_ref() = id;
+        }
+        __syncthreads();
+        cur = __builtin_amdgcn_readfirstlane(slot_ref());
+        if (cur < 0) {
+            grab.done(tid);
+            return;
+        }
+    }
+    dma_tile(cur);
     if (dyn && wave == 0) grab.issue();                       // the second tile, under the prologue
 #pragma unroll
     for (int d = 0; d < 16; ++d) dma_now(0u, d);
@@ -1876,7 +1891,7 @@ KSplit plan_ksplit(int ntiles, int nh, int cus, int step = 64) {
 // 1547-1556 TF/s, within run-to-run spread), leads on every fused-epilogue shape (FFN-up 1488-1496
 // vs 1410-1413, o-proj 1438-1441 vs 1291-1296), reads fewer L2->fabric bytes on q|k|v (16.8 vs
 // 17.9 GB per dispatch), and the whole step is as fast: 0.3906 / 0.3882 vs 0.3888 / 0.3881 steps/s
-// with the library routes, same box, interleaved (profiles/r5/gemm_queue_ab_s2.log,
+// with the library routes, same box, interleaved (profiles/r5/queue_ab_s2.log,
 // pmc_fetch_queue_s2.txt, bench_own_vs_lt_ab_s2.log).  The library route survives only in the A/B
 // build (-DVS_AB, `make ab`; VS_GEMM_BACKEND=lt there), never in libvstyler.so.
 #ifdef VS_AB
@@ -1942,7 +1957,7 @@ static bool use_4w() { return vs_opt(VS_OPT_GEMM_KERNEL) == 4; }
 
 // the schedule of a 4-wave launch (W4Sched): one persistent block per CU when the main tiles fill
 // every CU and a tile has >= 3 K-tiles (the tile-id hand-off, see the schedule's comment), fed by the
-// XCD tile queues when the stream has a queue workspace (kind 5) bound (VS_OPT_GEMM_QUEUE 0: the
+// XCD tile queues when the stream has a queue workspace (kind 5) bound (VS_OPT_QUEUE 0: the
 // static lists)
 static W4Sched w4_sched(int nmain, int nt, hipStream_t stream) {
     W4Sched s{nullptr, 0, 0, 0};
@@ -1952,7 +1967,7 @@ static W4Sched w4_sched(int nmain, int nt, hipStream_t stream) {
         s.tp = nmain / cus;
     }
     s.nrem = nmain - s.npers * s.tp;
-    if (s.npers && vs_opt(VS_OPT_GEMM_QUEUE)) s.q = (unsigned*)vs_split_workspace(5, WQ_BYTES, stream);
+    if (s.npers && vs_opt(VS_OPT_QUEUE)) s.q = (unsigned*)vs_split_workspace(5, WQ_BYTES, stream);
     return s;
 }
 static unsigned w4_grid(const W4Sched& s, const KSplit& sp) {

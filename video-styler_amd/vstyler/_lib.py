@@ -11,7 +11,7 @@ LIB_PATH = os.environ.get("VSTYLER_LIB", os.path.join(_HERE, "lib", "libvstyler.
 VS_EPI_BIAS, VS_EPI_GELU, VS_EPI_SILU, VS_EPI_GATE_RES, VS_EPI_RES = range(5)
 
 # path-selection options (include/vstyler.h VS_OPT_*): name -> id
-OPTIONS = {"gemm_tile": 0, "gemm_kernel": 1, "gemm_split": 2, "gemm_queue": 3, "attn_impl": 4, "attn_mfma": 5,
+OPTIONS = {"gemm_tile": 0, "gemm_kernel": 1, "gemm_split": 2, "queue": 3, "attn_impl": 4, "attn_mfma": 5,
            "attn_nc": 6, "attn_split": 7, "attn_persist": 8, "vae_pxb": 9, "vae_pre": 10}
 
 

@@ -19,7 +19,7 @@ def _stream(t):
 
 
 def set_option(name, value):
-    """Select a path of libvstyler (include/vstyler.h VS_OPT_*, e.g. set_option("gemm_queue", 0));
+    """Select a path of libvstyler (include/vstyler.h VS_OPT_*, e.g. set_option("queue", 0));
     returns the previous value.  The defaults are the product configuration; tests and A/B probes
     use the others."""
     prev = _lib.load().vs_set_option(_lib.OPTIONS[name], int(value))
@@ -50,7 +50,7 @@ class options:
 
 
 def apply_env_options():
-    """VSTYLER_OPTS="gemm_queue=0,attn_nc=0": the one environment hook, read by the Python host (never
+    """VSTYLER_OPTS="queue=0,attn_nc=0": the one environment hook, read by the Python host (never
     by the library) so that A/B scripts can select paths of a whole run."""
     spec = os.environ.get("VSTYLER_OPTS", "")
     for item in filter(None, (x.strip() for x in spec.split(","))):
