@@ -11,7 +11,7 @@ instantiation that reads through acc_rd (every one but the fp8 8-B fallback, whi
 And the tile-queue atomic (W4Grab::issue) must be a single returning global atomic add per kernel
 (the compiler's atomic optimizer off for gemm.o: Makefile).
 
-usage: check_isa.py <gemm.o>   (exit 1 with the offending kernels listed)"""
+usage: check_isa.py <gemm.o | libvstyler.so>   (exit 1 with the offending kernels listed)"""
 import os
 import re
 import subprocess
@@ -21,14 +21,26 @@ import tempfile
 LLVM = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "llvm", "bin")
 
 
-def code_object(obj, d):
+def code_objects(obj, d):
+    """The gfx950 code objects of a host object or shared library: its .hip_fatbin section holds one
+    offload bundle per linked translation unit (one for gemm.o, seven for libvstyler.so)."""
     fat = os.path.join(d, "fat.bin")
-    co = os.path.join(d, "dev.co")
     subprocess.run([os.path.join(LLVM, "llvm-objcopy"), "--dump-section", f".hip_fatbin={fat}", obj,
                     os.path.join(d, "copy.o")], check=True)
-    subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={fat}",
-                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
-    return co
+    data = open(fat, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+    out = []
+    for i, a in enumerate(starts):
+        part = os.path.join(d, f"b{i}.bin")
+        with open(part, "wb") as f:
+            f.write(data[a:starts[i + 1] if i + 1 < len(starts) else len(data)])
+        co = os.path.join(d, f"dev{i}.co")
+        subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={part}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+        if os.path.getsize(co):
+            out.append(co)
+    return out
 
 
 def kernels(co):
@@ -58,8 +70,12 @@ def kernels(co):
 def main():
     obj = sys.argv[1]
     bad = []
+    ks, scratch = {}, {}
     with tempfile.TemporaryDirectory() as d:
-        ks, scratch = kernels(code_object(obj, d))
+        for co in code_objects(obj, d):
+            k, sc = kernels(co)
+            ks.update(k)
+            scratch.update(sc)
     checked = 0
     for name, body in ks.items():
         if "_tn_4w" not in name:

@@ -188,3 +188,17 @@ def test_options_table():
         with pytest.raises(ValueError):
             K.set_option(name, bad)
     assert lib.vs_set_option(99, 0) < 0 and lib.vs_get_option(-1) < 0
+
+
+def test_built_library_passes_isa_guards():
+    """the accumulator-copy guard of scripts/check_isa.py (run by `make` on gemm.o)
+    holds for the gfx950 code objects inside the shipped libvstyler.so: every 4-wave GEMM
+    instantiation reads its accumulators only through acc_rd (no v_accvgpr_write / mov), 512 reads,
+    no scratch, one returning tile-queue atomic."""
+    import subprocess
+    import sys
+    from vstyler import _lib
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_isa.py"), _lib.LIB_PATH],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "13 gemm_*_4w kernels OK" in r.stdout

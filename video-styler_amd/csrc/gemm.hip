@@ -693,6 +693,16 @@ __device__ __forceinline__ float acc_rd(float a) {
     return v;
 }
 
+// The tile epilogue's shape: W4_EPI_ROWS row steps of 16 x W4_EPI_CBLK column blocks of 32, one
+// 16-B store each (+ one 16-B residual load each for the residual modes).  w4_epi_min_vmem is the
+// fewest VMEM operations any instantiation issues (bias / gate / hint loads are conditional or
+// mode-specific extras): the cross-tile drain of gemm_bf16_tn_4w (EPI_OPS; the fp8 kernel drains) relies
+// on at least that many being issued after the tile's last DMAs, and static_asserts against it.
+constexpr int W4_EPI_ROWS = 8, W4_EPI_CBLK = 4;
+constexpr int w4_epi_min_vmem(int mode) {
+    return W4_EPI_ROWS * W4_EPI_CBLK * ((mode == VS_EPI_GATE_RES || mode == VS_EPI_RES) ? 2 : 1);
+}
+
 template <int MODE, bool HINT, bool SCALED, class AccT>
 __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n_w, int lane, bf16_t* C, long long ldc,
                                                  int M, int N, const Epi& ep, const float* __restrict__ scale_a) {
@@ -715,9 +725,9 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
     const __amdgpu_buffer_rsrc_t rc = rsrc(C, ldc, true);
     const int vo_c = (int)((r * ldc + n_w + ncol) * 2);
     // bias unpacked once per tile (the per-row unpack was 8 of the ~95 VALU per 16-B store)
-    float bvf[4][8];
+    float bvf[W4_EPI_CBLK][8];
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+    for (int p = 0; p < W4_EPI_CBLK; ++p)
         unpack8(ep.bias ? ld16(ep.bias + min(nl + 32 * p, N - 8)) : u32x4_t{0, 0, 0, 0}, bvf[p]);
     u32x4_t gw0[4], gw1[4];
     int b_lo = 0;
@@ -742,7 +752,7 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
     auto load_rows = [&](auto ic, u32x4_t (&r_)[4], u32x4_t (&h_)[4]) __attribute__((always_inline)) {
         constexpr int i = decltype(ic)::value;
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
+        for (int p = 0; p < W4_EPI_CBLK; ++p) {
             r_[p] = __builtin_amdgcn_raw_buffer_load_b128(rr, vadd_opq(vo_r, (int)(16 * i * ep.ld_res * 2)) + 64 * p, 0, W4_RES_CPOL);
             if constexpr (HINT) h_[p] = __builtin_amdgcn_raw_buffer_load_b128(rh, vadd_opq(vo_h, (int)(16 * i * ep.ld_hint * 2)) + 64 * p, 0, 0);
         }
@@ -753,13 +763,13 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
             load_rows(ic, rs[i], hs[i]);
         });
     }
-    static_for<8>([&](auto ic) __attribute__((always_inline)) {
+    static_for<W4_EPI_ROWS>([&](auto ic) __attribute__((always_inline)) {
         constexpr int i = decltype(ic)::value;
         const int m = m_w + r + 16 * i;
         float sa = 1.f;
         if constexpr (SCALED) sa = scale_a[min(m, M - 1)];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
+        for (int p = 0; p < W4_EPI_CBLK; ++p) {
             float y[8];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -817,7 +827,7 @@ __device__ __forceinline__ void tile_epilogue_w4(const AccT& acc, int m_w, int n
             // of later blocks (AGPR -> VGPR copies) and run out of VGPRs
             __builtin_amdgcn_sched_barrier(0);
         }
-        if constexpr (RESID && i + DEPTH < 8) load_rows(std::integral_constant<int, i + DEPTH>{}, rs[i % DEPTH], hs[i % DEPTH]);
+        if constexpr (RESID && i + DEPTH < W4_EPI_ROWS) load_rows(std::integral_constant<int, i + DEPTH>{}, rs[i % DEPTH], hs[i % DEPTH]);
     });
 }
 
@@ -1124,6 +1134,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     // gemm_epidiag_ab.log).  EPI_OPS = the fewest VMEM operations any epilogue path of this
     // instantiation issues: 32 16-B stores, + 32 residual loads (the split-K piece path: 64 stores).
     constexpr int EPI_OPS = (MODE == VS_EPI_GATE_RES || MODE == VS_EPI_RES) ? 64 : 32;
+    static_assert(EPI_OPS <= w4_epi_min_vmem(MODE), "the epilogue issues fewer VMEM operations than the drain counts");
     // prologue: K-tiles 0 and 1 of the stream in flight (W then A each), then the k-step-0 fragments
     const bool dyn = sc.q && (int)blockIdx.x < sc.npers;    // a persistent block fed by the queues
     if (dyn) {              // the first tile from the queues too (a block that starts late: none left)
