@@ -33,6 +33,11 @@ if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "GRBM_GUI_ACTIVE" in avg:
     # MFMA busy cycles summed over SIMDs: utilisation = busy / (SIMDs * GPU cycles)
     gpu_cycles = avg["GRBM_GUI_ACTIVE"] / 8
     print(f"  MFMA busy / (1024 SIMDs x cycles) = {avg['SQ_VALU_MFMA_BUSY_CYCLES'] / (1024 * gpu_cycles):.3f}")
+if len(dur) > 1 and "SQ_VALU_MFMA_BUSY_CYCLES" in vals and "GRBM_GUI_ACTIVE" in vals:
+    # all dispatches together (kernels of many shapes, e.g. the VAE convs): time-weighted
+    tot = sum(vals["GRBM_GUI_ACTIVE"]) / 8
+    print(f"  all dispatches: MFMA busy {sum(vals['SQ_VALU_MFMA_BUSY_CYCLES']) / (1024 * tot):.3f}, "
+          f"{sum(dur) / max(1, len(glob.glob(os.path.join(d, 'p*_kernel_trace.csv')))):.1f} ms per pass")
 if "FETCH_SIZE" in avg:
     print(f"  HBM read  ~ {2 * avg['FETCH_SIZE'] * 1024 / 1e9:.3f} GB/dispatch (FETCH_SIZE x2 gfx950 correction)")
 if "WRITE_SIZE" in avg:
