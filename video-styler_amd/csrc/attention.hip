@@ -1047,14 +1047,15 @@ extern "C" int vs_attn_fwd(const void* q, const void* k, const void* v, void* o,
         hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(NTHR), lds, (hipStream_t)stream, a);
         return hipGetLastError() == hipSuccess;
     };
-    // the NC pass: attn_fwd_w4 (4 waves x 64 rows); VS_OPT_ATTN_IMPL 8 / 4 force the 8-wave / 4-wave kernel
-    // (items of fewer than 16 key tiles -- the 512-key cross-attention -- stay on the 8-wave kernel:
-    // the 4-wave pipeline's per-item fill and drain are a large share of an 8-tile item)
+    // the NC pass: attn_fwd_w4 (4 waves x 64 rows); VS_OPT_ATTN_IMPL 8 / 4 force the 8-wave / 4-wave kernel.
+    // r5: the 512-key cross-attention (8 tiles per item) too -- 0.682 vs 0.746 ms at the 14B shape,
+    // same box (profiles/r5/attn_skv_prefetch_ab_s10.log: both kernels pay ~7 us per item switch,
+    // the 4-wave one less per tile); items under 4 tiles stay on the 8-wave kernel
     const int impl = vs_opt(VS_OPT_ATTN_IMPL);
-    const bool w4 = flags && (impl ? impl == 4 : nkv >= 16);
+    const bool w4 = flags && (impl ? impl == 4 : nkv >= 4);
     // attn_fwd_w4's persistent blocks take their items from XCD queues (kind-5 workspace, words from
     // VS_Q_ATTN) when there is more than one item per block (VS_OPT_QUEUE 0: static lists)
-    if (w4 && npers < sp.nmain && nkv >= 16 && vs_opt(VS_OPT_QUEUE)) {
+    if (w4 && npers < sp.nmain && nkv >= 4 && vs_opt(VS_OPT_QUEUE)) {
         unsigned* qw = (unsigned*)vs_split_workspace(5, 4096, (hipStream_t)stream);
         if (qw) args.queue = qw + VS_Q_ATTN;
     }

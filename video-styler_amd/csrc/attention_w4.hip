@@ -48,15 +48,21 @@ constexpr int W4_TILE = BKV * HD * 2;      // 16 KB: one K or V tile
 constexpr int W4_SLOT = 2 * W4_TILE;
 constexpr int W4_LDS = 4 * W4_SLOT;        // 128 KB
 constexpr int W4_QSLOT = W4_LDS;           // the next item's id (LDS word, the item hand-off)
+constexpr int W4_LDS_BASE = W4_LDS + 16;
 #ifdef VS_W4_STAMPS
 // diagnostic build: s_memtime at the phase boundaries of the pipelined loop (iterations 8..39 of
 // block 0, every wave): 0 start of A, 1 end of A, 2 end of B, 3 end of C, 4 after the barrier, 5 end
 // of D, 6 after D step 3; kept in an LDS tail, copied out at the end (tests/probes/w4_stamps.py)
 __device__ unsigned long long g_w4_stamps[4][32][7];
-constexpr int W4_STAMP_OFF = W4_LDS + 16;
-constexpr int W4_LDS_ALLOC = W4_STAMP_OFF + 4 * 32 * 7 * 8;
+// and per item of block 0 (the first 16, every wave): 0 before its first tile, 1 after it, 2 after
+// the paired tile loop, 3 after the next item's Q loads are issued, 4 after the drain, 5 after the
+// O store (tests/probes/w4_stamps.py W4S_SKV=512: the item switch of the 8-tile cross-attention)
+__device__ unsigned long long g_w4_sw[4][16][6];
+constexpr int W4_STAMP_OFF = W4_LDS_BASE;
+constexpr int W4_SW_OFF = W4_STAMP_OFF + 4 * 32 * 7 * 8;
+constexpr int W4_LDS_ALLOC = W4_SW_OFF + 4 * 16 * 6 * 8;
 #else
-constexpr int W4_LDS_ALLOC = W4_LDS + 16;
+constexpr int W4_LDS_ALLOC = W4_LDS_BASE;
 #endif
 
 // Items of the persistent blocks (r5): XCD x owns the contiguous chunk [cs, cs + csz) of the item
@@ -407,8 +413,26 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
                 *reinterpret_cast<volatile LDS_AS unsigned long long*>(
                     (LDS_AS char*)(uintptr_t)(smem_base + W4_STAMP_OFF + 8 * ((wave * 32 + st) * 7 + k))) = stv[k];
     };
+    unsigned long long swv[6] = {0, 0, 0, 0, 0, 0};
+    int sw_i = 0;                        // item index of block 0 (stamped while < 16)
+    auto swst = [&](int k) __attribute__((always_inline)) {
+        // (waited at once: the value must not be copied before it lands)
+        if (blockIdx.x == 0 && sw_i < 16) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(swv[k]) :: "memory");
+    };
+    auto sw_store = [&]() __attribute__((always_inline)) {
+        if (blockIdx.x == 0 && sw_i < 16) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0)
+                for (int k = 0; k < 6; ++k)
+                    *reinterpret_cast<volatile LDS_AS unsigned long long*>(
+                        (LDS_AS char*)(uintptr_t)(smem_base + W4_SW_OFF + 8 * ((wave * 16 + sw_i) * 6 + k))) = swv[k];
+        }
+        ++sw_i;
+    };
 #else
     auto stamp = [](int) {};
+    auto swst = [](int) {};
+    auto sw_store = [] {};
 #endif
     auto rdK = [&](bf16x8_t& d, int T, int kb, int j) __attribute__((always_inline)) {
         d = lds16(smem_base + (T & 3) * W4_SLOT + koff[j] + kb * 32 * 256);
@@ -622,7 +646,9 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) o[rb][dt][i] = 0.f;
         }
+        swst(0);
         iteration(T, s1a, s1b, p0a, p0b, std::true_type{});
+        swst(1);
         ++T;
         int t = 1;
         for (; t + 1 < nkv; t += 2) {
@@ -631,6 +657,7 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
             iteration(T, s1a, s1b, p0a, p0b, std::false_type{});
             ++T;
         }
+        swst(2);
         const int bh_done = bh, q0_done = q0;
         if (nxt >= 0) {                  // the next item's Q (its QK starts after the drain)
             bh = item_bh(nxt, q0);
@@ -640,12 +667,17 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
             iteration(T, s1b, s1a, p0b, p0a, std::false_type{});
             ++T;
             if (nxt >= 0) next_q(nxt);
+            swst(3);
             drain(T - 1, s1b, p0b);
         } else {
             if (nxt >= 0) next_q(nxt);
+            swst(3);
             drain(T - 1, s1a, p0a);
         }
+        swst(4);
         finish(o_base(bh_done), q0_done, cur);
+        swst(5);
+        sw_store();
         if (nxt < 0) break;
         cur = nxt;
     }
@@ -658,6 +690,9 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
     if (blockIdx.x == 0)
         for (int i = lane; i < 32 * 7; i += 64)
             (&g_w4_stamps[wave][0][0])[i] = *reinterpret_cast<volatile unsigned long long*>(smem + W4_STAMP_OFF + 8 * (wave * 32 * 7 + i));
+    if (blockIdx.x == 0)
+        for (int i = lane; i < 16 * 6; i += 64)
+            (&g_w4_sw[wave][0][0])[i] = *reinterpret_cast<volatile unsigned long long*>(smem + W4_SW_OFF + 8 * (wave * 16 * 6 + i));
 #endif
 }
 
@@ -679,6 +714,9 @@ hipError_t attn_w4_launch(const AttnArgs& args, bool rebase, unsigned grid, hipS
 }  // namespace vs_attn
 
 #ifdef VS_W4_STAMPS
+extern "C" int vs_debug_w4_switch(unsigned long long* host_out) {
+    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(vs_attn::g_w4_sw), sizeof(vs_attn::g_w4_sw)) == hipSuccess ? 0 : 2;
+}
 extern "C" int vs_debug_w4_stamps(unsigned long long* host_out) {
     return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(vs_attn::g_w4_stamps), sizeof(vs_attn::g_w4_stamps)) == hipSuccess ? 0 : 2;
 }

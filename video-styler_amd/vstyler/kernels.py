@@ -62,8 +62,9 @@ _SPLIT_WS = {}
 
 
 def _split_ws(kind, t, nbytes=None):
-    """Bind library scratch of `kind` (0 attention split tail, 1 GEMM split tail, 2 hipBLASLt
-    workspace, 3 epilogue staging of `nbytes`, 4 attention item flags, 5 GEMM tile queues) for the current stream of t's device from the torch
+    """Bind library scratch of `kind` (0 attention split tail, 1 GEMM split tail, 2 / 3 the A/B build's
+    vendor-library workspace and epilogue staging, 4 attention item flags, 5 GEMM tile and attention
+    item queues) for the current stream of t's device from the torch
     allocator (vs_split_workspace_bind: the library never allocates).  Re-bound larger when a
     bigger one is needed; never inside a graph capture (the library then takes its fallback)."""
     stream = _stream(t)
@@ -210,6 +211,7 @@ def attention(q, k, v, out, num_heads, batch, scale=None):
         scale = hd ** -0.5
     _split_ws(0, q)
     _split_ws(4, q)
+    _split_ws(5, q)             # the persistent grid's XCD item queues (zero-filled words)
     _lib.check(_lib.load().vs_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), batch, sq,
                                        skv, num_heads, hd, ldq, ldk, ldv, ldo, sq * ldq, skv * ldk,
                                        skv * ldv, sq * ldo, float(scale), _stream(q)))
