@@ -33,9 +33,9 @@ for w in range(4):
     med = np.median(d[:-1], 0)
     print(f"wave {w}: " + "  ".join(f"{n} {m:.0f}" for n, m in zip(names, med)), flush=True)
 print("(s_memtime ticks; MFMA work per phase: 16 x 32 cycles = 512 shader cycles)")
-sw = (ctypes.c_ulonglong * (4 * 16 * 6))()
+sw = (ctypes.c_ulonglong * (4 * 16 * 9))()
 assert lib.vs_debug_w4_switch(sw) == 0
-sw = np.array(sw, dtype=np.int64).reshape(4, 16, 6)
+sw = np.array(sw, dtype=np.int64).reshape(4, 16, 9)
 nkv = (L + 63) // 64
 for w in range(4):
     a = sw[w]
@@ -45,5 +45,7 @@ for w in range(4):
     d = np.stack([a[:, 1] - a[:, 0], (a[:, 2] - a[:, 1]) / max(1, 2 * ((nkv - 1) // 2)), a[:, 3] - a[:, 2],
                   a[:, 4] - a[:, 3], a[:, 5] - a[:, 4], nxt0 - a[:, 5], nxt0 - a[:, 0]], 1)[:-1]
     med = np.median(d, 0)
-    print(f"wave {w} items {len(a)}: first tile {med[0]:.0f}  per loop tile {med[1]:.0f}  last tile + next Q issue "
-          f"{med[2]:.0f}  drain {med[3]:.0f}  O store {med[4]:.0f}  gap to next {med[5]:.0f}  item {med[6]:.0f}", flush=True)
+    q = np.median(np.stack([a[:, 7] - a[:, 6], a[:, 8] - a[:, 7]], 1)[:-1], 0)
+    print(f"wave {w} items {len(a)}: first tile {med[0]:.0f}  per loop tile {med[1]:.0f}  last tile + next Q "
+          f"{med[2]:.0f} (DMA drain {q[0]:.0f}, Q load {q[1]:.0f})  drain {med[3]:.0f}  O store {med[4]:.0f}  "
+          f"gap to next {med[5]:.0f}  item {med[6]:.0f}", flush=True)

@@ -55,12 +55,14 @@ constexpr int W4_LDS_BASE = W4_LDS + 16;
 // of D, 6 after D step 3; kept in an LDS tail, copied out at the end (tests/probes/w4_stamps.py)
 __device__ unsigned long long g_w4_stamps[4][32][7];
 // and per item of block 0 (the first 16, every wave): 0 before its first tile, 1 after it, 2 after
-// the paired tile loop, 3 after the next item's Q loads are issued, 4 after the drain, 5 after the
-// O store (tests/probes/w4_stamps.py W4S_SKV=512: the item switch of the 8-tile cross-attention)
-__device__ unsigned long long g_w4_sw[4][16][6];
+// the paired tile loop, 3 after the next item's Q loads, 4 after the drain, 5 after the O store; 6-8
+// inside the next-Q step: its start, the in-flight DMA drained, the Q loaded and converted
+// (tests/probes/w4_stamps.py W4S_SKV=512: the item switch of the 8-tile cross-attention)
+constexpr int W4_SWN = 9;
+__device__ unsigned long long g_w4_sw[4][16][W4_SWN];
 constexpr int W4_STAMP_OFF = W4_LDS_BASE;
 constexpr int W4_SW_OFF = W4_STAMP_OFF + 4 * 32 * 7 * 8;
-constexpr int W4_LDS_ALLOC = W4_SW_OFF + 4 * 16 * 6 * 8;
+constexpr int W4_LDS_ALLOC = W4_SW_OFF + 4 * 16 * W4_SWN * 8;
 #else
 constexpr int W4_LDS_ALLOC = W4_LDS_BASE;
 #endif
@@ -413,7 +415,7 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
                 *reinterpret_cast<volatile LDS_AS unsigned long long*>(
                     (LDS_AS char*)(uintptr_t)(smem_base + W4_STAMP_OFF + 8 * ((wave * 32 + st) * 7 + k))) = stv[k];
     };
-    unsigned long long swv[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long swv[W4_SWN] = {};
     int sw_i = 0;                        // item index of block 0 (stamped while < 16)
     auto swst = [&](int k) __attribute__((always_inline)) {
         // (waited at once: the value must not be copied before it lands)
@@ -423,9 +425,9 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
         if (blockIdx.x == 0 && sw_i < 16) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (lane == 0)
-                for (int k = 0; k < 6; ++k)
+                for (int k = 0; k < W4_SWN; ++k)
                     *reinterpret_cast<volatile LDS_AS unsigned long long*>(
-                        (LDS_AS char*)(uintptr_t)(smem_base + W4_SW_OFF + 8 * ((wave * 16 + sw_i) * 6 + k))) = swv[k];
+                        (LDS_AS char*)(uintptr_t)(smem_base + W4_SW_OFF + 8 * ((wave * 16 + sw_i) * W4_SWN + k))) = swv[k];
         }
         ++sw_i;
     };
@@ -629,8 +631,17 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
     unsigned* const qw = pers ? args.queue : nullptr;
     auto next_q = [&](int after) __attribute__((always_inline)) {
         unsigned t0 = 0;
+#ifdef VS_W4_STAMPS
+        // (diagnostic split of the next-Q cost: 6 -> 7 the in-flight K/V DMA drained, 7 -> 8 the Q loads)
+        swst(6);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        swst(7);
+#endif
         if (qw && wave == 0) t0 = vs_queue_issue(qw + (blockIdx.x & 7) * VS_Q_LINE);
         load_q(q_base(bh), q0);
+#ifdef VS_W4_STAMPS
+        swst(8);
+#endif
         if (wave == 0) {
             const int id = pers ? chunks.take(qw, t0, after, lane) : -1;
             if (lane == 0) *(volatile LDS_AS int*)(uintptr_t)(smem_base + W4_QSLOT) = id;
@@ -691,8 +702,8 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
         for (int i = lane; i < 32 * 7; i += 64)
             (&g_w4_stamps[wave][0][0])[i] = *reinterpret_cast<volatile unsigned long long*>(smem + W4_STAMP_OFF + 8 * (wave * 32 * 7 + i));
     if (blockIdx.x == 0)
-        for (int i = lane; i < 16 * 6; i += 64)
-            (&g_w4_sw[wave][0][0])[i] = *reinterpret_cast<volatile unsigned long long*>(smem + W4_SW_OFF + 8 * (wave * 16 * 6 + i));
+        for (int i = lane; i < 16 * W4_SWN; i += 64)
+            (&g_w4_sw[wave][0][0])[i] = *reinterpret_cast<volatile unsigned long long*>(smem + W4_SW_OFF + 8 * (wave * 16 * W4_SWN + i));
 #endif
 }
 
