@@ -2,7 +2,8 @@
 for CUs (as RCCL's all-to-all does on a real node), on ONE GPU: the product UlyssesGroup with each
 collective replaced by a G-workgroup copy kernel (tests/probes/fakecomm) launched on a side stream
 after an event, and waited on by event -- RCCL's async pattern.  Interleaved rounds in one process:
-  python tests/probes/sp_contention.py   (env: SPC_G=16,64  SPC_PERSIST=0,1)"""
+  python tests/probes/sp_contention.py   (env: SPC_G=16,64  SPC_PERSIST=0,1  SPC_QUEUE=1,0 -- the r5 XCD
+  tile / item queues of the persistent GEMM and attention grids vs the static per-CU lists)"""
 import ctypes, os, sys, time
 ROOT = os.path.join(os.path.dirname(__file__), "..", "..")
 sys.path.insert(0, os.path.join(ROOT, "video-styler_amd"))
@@ -67,17 +68,19 @@ t = torch.tensor([999.0], device=dev).to(torch.bfloat16)
 P = 8
 Gs = [int(x) for x in os.environ.get("SPC_G", "0,16,64").split(",")]
 pers = os.environ.get("SPC_PERSIST", "1,0").split(",")
+queues = os.environ.get("SPC_QUEUE", "1").split(",")
 ovs = [o == "1" for o in os.environ.get("SPC_OVERLAP", "1,0").split(",")]
 ev = os.environ.get("SPC_ENV", "")          # "VAR=a,b": one more interleaved dimension
 evar, evals = ev.split("=") if ev else ("", "-")
-cases = [(G, pz, ov, e) for G in Gs for pz in pers for ov in ovs for e in evals.split(",")]
+cases = [(G, pz, ov, e, qu) for G in Gs for pz in pers for ov in ovs for e in evals.split(",") for qu in queues]
 res = {c: [] for c in cases}
 for rnd in range(3):
     for c in cases:
-        G, pz, ov, e = c
+        G, pz, ov, e, qu = c
         if evar:
             os.environ[evar] = e
         K.set_option("attn_persist", 1 if pz == "1" else 0)
+        K.set_option("queue", int(qu))
         sp = FakeCommUlysses(P, overlap=ov, nblocks=G)
         fn = lambda: model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=ctx, vace_context=vc,
                                         use_unified_sequence_parallel=True, sp_group=sp)
@@ -87,6 +90,6 @@ for rnd in range(3):
             t0 = time.perf_counter(); fn(); torch.cuda.synchronize(); ts.append(time.perf_counter() - t0)
         res[c].append(1000 * min(ts))
     print(f"round {rnd} done", flush=True)
-for (G, pz, ov, e), ms in res.items():
-    print(f"SP=8 comm-G={G:3d} persist={pz} overlap={int(ov)}" + (f" {evar}={e}" if evar else "") + ": "
+for (G, pz, ov, e, qu), ms in res.items():
+    print(f"SP=8 comm-G={G:3d} persist={pz} overlap={int(ov)} queue={qu}" + (f" {evar}={e}" if evar else "") + ": "
           + " ".join(f"{x:.1f}" for x in ms) + " ms", flush=True)

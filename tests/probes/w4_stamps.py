@@ -33,6 +33,17 @@ for w in range(4):
     med = np.median(d[:-1], 0)
     print(f"wave {w}: " + "  ".join(f"{n} {m:.0f}" for n, m in zip(names, med)), flush=True)
 print("(s_memtime ticks; MFMA work per phase: 16 x 32 cycles = 512 shader cycles)")
+if L < S:
+    # the phases of each item's last tile (T % nkv == nkv - 1) against the median iteration
+    nkv0 = (L + 63) // 64
+    for w in range(4):
+        nxt = np.append(st[w, 1:, 0], 0)
+        d = np.stack([st[w, :, 1] - st[w, :, 0], st[w, :, 2] - st[w, :, 1], st[w, :, 3] - st[w, :, 2],
+                      st[w, :, 4] - st[w, :, 3], st[w, :, 6] - st[w, :, 4], st[w, :, 5] - st[w, :, 6]], 1)
+        last = [i for i in range(31) if (i + 8) % nkv0 == nkv0 - 1]
+        if last:
+            med = np.median(d[last], 0)
+            print(f"wave {w} last tiles: " + "  ".join(f"{n} {m:.0f}" for n, m in zip(names[:6], med)), flush=True)
 sw = (ctypes.c_ulonglong * (4 * 16 * 9))()
 assert lib.vs_debug_w4_switch(sw) == 0
 sw = np.array(sw, dtype=np.int64).reshape(4, 16, 9)
