@@ -1821,6 +1821,12 @@ __global__ __launch_bounds__(256, 1) void gemm_fp8_tn_4w(
 }
 
 
+// fp8_linear's activation quantisation (vram_management/layers.py:115-151): per row s = max(bf16(max|x| /
+// 448), 1), x8 = e4m3(x / (s + 1e-8)).  One wave per row.  NC > 0: the row stays in registers
+// between the max and the conversion (NC 16-B chunks per lane: cols <= 512 NC) -- one HBM read of x
+// instead of two (r5; r1-r4 re-read the row: 249 us per 59 280 x 5120 launch, 4.1 % of a config-5
+// step, profiles/r5/prof_fp8_r5s17); NC == 0: the two-pass form for wider rows.
+template <int NC>
 __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __restrict__ x, long long ldx,
                                                              uint8_t* __restrict__ x8, long long ld8,
                                                              float* __restrict__ scale, int rows, int cols) {
@@ -1828,20 +1834,13 @@ __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __res
     const int lane = threadIdx.x & 63;
     if (row >= rows) return;
     const bf16_t* xr = x + (long long)row * ldx;
+    uint8_t* yr = x8 + (long long)row * ld8;
     float mx = 0.f;
-    for (int c = lane * 8; c < cols; c += 512) {
-        const u32x4_t w = *reinterpret_cast<const u32x4_t*>(xr + c);
+    auto absmax = [&](const u32x4_t& w) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) mx = fmaxf(mx, fmaxf(fabsf(bflo(w[e])), fabsf(bfhi(w[e]))));
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    const float s = fmaxf(rbf(mx / 448.0f), 1.0f);
-    const float d = s + 1e-8f;
-    if (lane == 0) scale[row] = s;
-    uint8_t* yr = x8 + (long long)row * ld8;
-    for (int c = lane * 8; c < cols; c += 512) {
-        const u32x4_t w = *reinterpret_cast<const u32x4_t*>(xr + c);
+    };
+    auto convert = [&](const u32x4_t& w, float d, int c) {
         u32x2_t o;
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
@@ -1850,6 +1849,32 @@ __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __res
             o[e] = (uint32_t)v;
         }
         *reinterpret_cast<u32x2_t*>(yr + c) = o;
+    };
+    u32x4_t w[NC > 0 ? NC : 1];
+    if constexpr (NC > 0) {
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+            const int c = lane * 8 + 512 * i;
+            w[i] = c < cols ? *reinterpret_cast<const u32x4_t*>(xr + c) : u32x4_t{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int i = 0; i < NC; ++i) absmax(w[i]);
+    } else {
+        for (int c = lane * 8; c < cols; c += 512) absmax(*reinterpret_cast<const u32x4_t*>(xr + c));
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    const float s = fmaxf(rbf(mx / 448.0f), 1.0f);
+    const float d = s + 1e-8f;
+    if (lane == 0) scale[row] = s;
+    if constexpr (NC > 0) {
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+            const int c = lane * 8 + 512 * i;
+            if (c < cols) convert(w[i], d, c);
+        }
+    } else {
+        for (int c = lane * 8; c < cols; c += 512) convert(*reinterpret_cast<const u32x4_t*>(xr + c), d, c);
     }
 }
 
@@ -2199,7 +2224,11 @@ extern "C" int vs_quant_fp8_rows(const void* x, long long ldx, void* x8, long lo
     if (!x || !x8 || !scale || rows <= 0 || cols <= 0 || cols % 8 || ldx < cols || ld8 < cols || (ldx & 7) ||
         (ld8 & 7) || !aligned16(x) || !aligned8(x8))
         return VS_E_INVALID;
-    hipLaunchKernelGGL(quant_fp8_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+    const int nc = (cols + 511) / 512;
+    void (*kern)(const bf16_t*, long long, uint8_t*, long long, float*, int, int) =
+        nc <= 4 ? quant_fp8_rows_kernel<4> : nc <= 12 ? quant_fp8_rows_kernel<12> : nc <= 28 ? quant_fp8_rows_kernel<28>
+                                                                               : quant_fp8_rows_kernel<0>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                        (const bf16_t*)x, ldx, (uint8_t*)x8, ld8, scale, rows, cols);
     VS_CHECK_LAUNCH();
     return VS_OK;
