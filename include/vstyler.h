@@ -166,6 +166,14 @@ int vs_layernorm_modulate(const void* x, long long ldx, void* out, long long ldo
                           long long mod_bstride, const void* weight, const void* bias, float eps,
                           void* stream);
 
+/* vs_layernorm_modulate into fp8_linear's quantised activation instead of a bf16 row (config 5):
+ * x8 [rows, >=dim] e4m3fn bytes and qscale [rows] fp32, exactly vs_quant_fp8_rows of the bf16 rows
+ * vs_layernorm_modulate would write (layers.py:115-151). */
+int vs_layernorm_modulate_fp8(const void* x, long long ldx, void* x8, long long ld8, float* qscale, int rows,
+                              int dim, int rows_per_batch, const void* shift, const void* scale,
+                              long long mod_bstride, const void* weight, const void* bias, float eps,
+                              void* stream);
+
 /*
  * x = epilogue(y, x) then out = vs_layernorm_modulate(x): the gate-residual / residual epilogue of a
  * projection whose bf16(A W^T + bias) was staged in y, fused with the

@@ -20,19 +20,51 @@ def _k():
     return K
 
 
-def test_quant_fp8_rows_bit_exact():
+@pytest.mark.parametrize("cols", [640, 5120, 13824, 20000])   # row in registers (<= 4 / 12 / 28 chunks), two-pass
+def test_quant_fp8_rows_bit_exact(cols):
     K = _k()
     g = torch.Generator().manual_seed(1)
-    x = torch.randn(300, 640, generator=g)
+    x = torch.randn(300, cols, generator=g)
     x[::3] *= 1000.0           # rows with max > 448: scale > 1
     x[1::7] *= 1e-3            # e4m3 subnormal range
     x = x.to(BF16)
     ref8, ref_s = O.fp8_quant_rows(x)
-    x8 = torch.empty(300, 640, dtype=torch.uint8, device="cuda")
+    x8 = torch.empty(300, cols, dtype=torch.uint8, device="cuda")
     sc = torch.empty(300, dtype=torch.float32, device="cuda")
     K.quant_fp8_rows(x.cuda(), x8, sc)
     assert torch.equal(sc.cpu(), ref_s[:, 0])
     assert torch.equal(x8.cpu(), ref8.view(torch.uint8))
+
+
+@pytest.mark.parametrize("D", [1536, 5120])
+@pytest.mark.parametrize("mode", ["modulate", "affine"])
+def test_layernorm_modulate_fp8_equals_two_passes(D, mode):
+    """vs_layernorm_modulate_fp8 == vs_layernorm_modulate then vs_quant_fp8_rows, every byte and scale
+    (the config-5 LN1 / LN3 / LN2 feeding fp8 linears, models.ln_into)."""
+    K = _k()
+    B, S = 2, 333
+    g = torch.Generator(device="cuda").manual_seed(D)
+    x = (2.0 * torch.randn(B * S, D, device="cuda", generator=g)).to(BF16)
+    if mode == "modulate":
+        mod = (0.3 * torch.randn(B, 6, D, device="cuda", generator=g)).to(BF16)
+        mod[:, 1, :64] = 300.0     # large scales: outputs above 448 (per-row scale > 1)
+        ln = dict(shift=mod[:, 0], scale=mod[:, 1], mod_bstride=6 * D, rows_per_batch=S)
+    else:
+        w = (1 + 0.1 * torch.randn(D, device="cuda", generator=g)).to(BF16)
+        w[:64] = 300.0
+        b = (0.1 * torch.randn(D, device="cuda", generator=g)).to(BF16)
+        ln = dict(weight=w, bias=b)
+    h = torch.empty(B * S, D, dtype=BF16, device="cuda")
+    K.layernorm_modulate(x, h, 1e-6, **ln)
+    ref8 = torch.empty(B * S, D, dtype=torch.uint8, device="cuda")
+    refs = torch.empty(B * S, dtype=torch.float32, device="cuda")
+    K.quant_fp8_rows(h, ref8, refs)
+    x8 = torch.full((B * S, D), 7, dtype=torch.uint8, device="cuda")
+    sc = torch.zeros(B * S, dtype=torch.float32, device="cuda")
+    K.layernorm_modulate_fp8(x, x8, sc, 1e-6, **ln)
+    assert torch.equal(sc, refs)
+    assert torch.equal(x8, ref8)
+    assert (refs > 1).any()
 
 
 @pytest.mark.parametrize("M,N,Kd", [(256, 256, 128), (300, 520, 384), (1000, 768, 640)])   # K % 128 (vstyler.h)
@@ -109,6 +141,36 @@ def test_model_fn_fp8_tiny_vs_oracle():
     mx, rl = err(out, ref)
     print(f"fp8 tiny forward: max-abs {mx:.4g} rel-L2 {rl:.4g} (floor {fmx:.4g} / {frl:.4g})")
     assert rl <= 1.5 * frl + 2e-3 and mx <= 1.5 * fmx + 2e-2
+
+
+def test_model_fn_fp8_ln_fusion_bit_identical(monkeypatch):
+    """The config-5 forward with the LayerNorms writing fp8_linear's quantised activations directly
+    (models.ln_into -> vs_layernorm_modulate_fp8) equals the forward with bf16 LN rows + a separate
+    quantisation, bit for bit."""
+    from test_model_gpu import build
+    from vstyler import model_fn_wan_video, models
+    from vstyler.models import quantize_fp8_
+    cfg = O.WAN_CONFIGS["tiny"]
+    W = O.random_weights(cfg, seed=7)
+    dit, vace = build(cfg, W)
+    quantize_fp8_(dit)
+    quantize_fp8_(vace)
+    lat, cp, cn, vc = O.synthetic_inputs(cfg, 5, 128, 128)
+    t = torch.tensor([700.0]).to(BF16).cuda()
+    run = lambda: model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=cp.cuda(),
+                                     vace_context=vc.cuda()).clone()
+    calls = []
+    real = _k().layernorm_modulate_fp8
+
+    def counted(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+    monkeypatch.setattr(_k(), "layernorm_modulate_fp8", counted)
+    fused = run()
+    assert calls, "the fused LN -> fp8 path did not run"
+    monkeypatch.setattr(models, "_fp8_consumer", lambda target: False)
+    plain = run()
+    assert torch.equal(fused, plain)
 
 
 @pytest.mark.parametrize("epi", ["bias", "gelu", "gate_res", "res"])

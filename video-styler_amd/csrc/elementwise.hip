@@ -35,12 +35,31 @@ __device__ __forceinline__ u32x4_t pack8(const float* v) {
     return w;
 }
 
+__device__ __forceinline__ float block_max(float v, float* red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < RT / 64; ++i) t = fmaxf(t, red[i]);
+    return t;
+}
+
 // LayerNorm (fp32, eps) [affine] -> bf16, then optional modulate  (layers.py:89-91,
-// wan_video_dit.py:64-65): out = bf16(bf16(n * bf16(1 + scale)) + shift)
+// wan_video_dit.py:64-65): out = bf16(bf16(n * bf16(1 + scale)) + shift).
+// Q8 (r5, config 5): the row is not stored as bf16 but handed straight to fp8_linear's activation
+// quantisation (layers.py:115-151, vs_quant_fp8_rows): per-row s = max(bf16(max|h| / 448), 1) and
+// e4m3(h / (s + 1e-8)) of the bf16 values h the plain kernel would store -- bit-identical to the two
+// passes, without the bf16 write and the quantisation's read (the row's consumer is an fp8 GEMM).
+template <bool Q8>
 __global__ __launch_bounds__(RT) void ln_modulate_kernel(
     const bf16_t* __restrict__ x, long long ldx, bf16_t* __restrict__ out, long long ldo, int dim,
     int rpb, const bf16_t* __restrict__ shift, const bf16_t* __restrict__ scale, long long mbs,
-    const bf16_t* __restrict__ w, const bf16_t* __restrict__ bb, float eps) {
+    const bf16_t* __restrict__ w, const bf16_t* __restrict__ bb, float eps, uint8_t* __restrict__ x8,
+    long long ld8, float* __restrict__ qscale) {
     __shared__ float red[RT / 64];
     const long long row = blockIdx.x;
     const int nch = dim >> 3;
@@ -93,7 +112,38 @@ __global__ __launch_bounds__(RT) void ln_modulate_kernel(
 #pragma unroll
             for (int e = 0; e < 8; ++e) y[e] = rbf(rbf(rbf(y[e]) * rbf(1.f + sc[e])) + sh[e]);
         }
-        *reinterpret_cast<u32x4_t*>(orow + ch * 8) = pack8(y);
+        if constexpr (Q8) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[c][e] = rbf(y[e]);       // the bf16 row h, kept for the quantisation
+        } else {
+            *reinterpret_cast<u32x4_t*>(orow + ch * 8) = pack8(y);
+        }
+    }
+    if constexpr (Q8) {
+        float mx = 0.f;
+#pragma unroll
+        for (int c = 0; c < MAXCH; ++c)
+            if ((int)threadIdx.x + c * RT < nch)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf(v[c][e]));
+        mx = block_max(mx, red);
+        const float s8 = fmaxf(rbf(mx / 448.0f), 1.0f);
+        const float d = s8 + 1e-8f;
+        if (threadIdx.x == 0) qscale[row] = s8;
+        uint8_t* yr = x8 + row * ld8;
+#pragma unroll
+        for (int c = 0; c < MAXCH; ++c) {
+            const int ch = threadIdx.x + c * RT;
+            if (ch >= nch) continue;
+            u32x2_t o;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                int t = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][4 * e] / d, v[c][4 * e + 1] / d, 0, false);
+                t = __builtin_amdgcn_cvt_pk_fp8_f32(v[c][4 * e + 2] / d, v[c][4 * e + 3] / d, t, true);
+                o[e] = (uint32_t)t;
+            }
+            *reinterpret_cast<u32x2_t*>(yr + ch * 8) = o;
+        }
     }
 }
 
@@ -480,10 +530,30 @@ extern "C" int vs_layernorm_modulate(const void* x, long long ldx, void* out, lo
     if (shift && (!al16(shift) || !al16(scale) || (mod_bstride & 7))) return VS_E_INVALID;
     if (weight && (!al16(weight) || !al16(bias))) return VS_E_INVALID;
     if (rows_per_batch <= 0) rows_per_batch = rows;
-    hipLaunchKernelGGL(ln_modulate_kernel, dim3(rows), dim3(RT), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(ln_modulate_kernel<false>, dim3(rows), dim3(RT), 0, (hipStream_t)stream,
                        (const bf16_t*)x, ldx, (bf16_t*)out, ldo, dim, rows_per_batch,
                        (const bf16_t*)shift, (const bf16_t*)scale, mod_bstride,
-                       (const bf16_t*)weight, (const bf16_t*)bias, eps);
+                       (const bf16_t*)weight, (const bf16_t*)bias, eps, nullptr, 0LL, nullptr);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
+extern "C" int vs_layernorm_modulate_fp8(const void* x, long long ldx, void* x8, long long ld8, float* qscale,
+                                         int rows, int dim, int rows_per_batch, const void* shift,
+                                         const void* scale, long long mod_bstride, const void* weight,
+                                         const void* bias, float eps, void* stream) {
+    if (!x || !x8 || !qscale || rows <= 0 || dim <= 0 || dim % 8 || dim > MAXCH * RT * 8) return VS_E_INVALID;
+    if (ldx < dim || ld8 < dim || (ldx & 7) || (ld8 & 7) || !al16(x) || (reinterpret_cast<uintptr_t>(x8) & 7))
+        return VS_E_INVALID;
+    if ((shift == nullptr) != (scale == nullptr)) return VS_E_INVALID;
+    if ((weight == nullptr) != (bias == nullptr)) return VS_E_INVALID;
+    if (shift && (!al16(shift) || !al16(scale) || (mod_bstride & 7))) return VS_E_INVALID;
+    if (weight && (!al16(weight) || !al16(bias))) return VS_E_INVALID;
+    if (rows_per_batch <= 0) rows_per_batch = rows;
+    hipLaunchKernelGGL(ln_modulate_kernel<true>, dim3(rows), dim3(RT), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, ldx, nullptr, 0LL, dim, rows_per_batch,
+                       (const bf16_t*)shift, (const bf16_t*)scale, mod_bstride,
+                       (const bf16_t*)weight, (const bf16_t*)bias, eps, (uint8_t*)x8, ld8, qscale);
     VS_CHECK_LAUNCH();
     return VS_OK;
 }

@@ -71,6 +71,7 @@ SIGNATURES = {
     "vs_get_option": [_I],
     "vs_split_workspace_bind": [_I, _P, _LL, _P],
     "vs_layernorm_modulate": [_P, _LL, _P, _LL, _I, _I, _I, _P, _P, _LL, _P, _P, _F, _P],
+    "vs_layernorm_modulate_fp8": [_P, _LL, _P, _LL, _P, _I, _I, _I, _P, _P, _LL, _P, _P, _F, _P],
     "vs_residual_layernorm": [_P, _LL, _P, _LL, _P, _LL, _I, _I, _I, ctypes.POINTER(VsEpilogue), _I, _P, _P, _LL,
                               _P, _P, _F, _P],
     "vs_rmsnorm_rope": [_P, _LL, _I, _I, _I, _P, _F, _P, _I, _I, _I, _I, _I, _I, _P],

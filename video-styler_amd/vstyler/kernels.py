@@ -244,6 +244,22 @@ def layernorm_modulate(x, out, eps=1e-6, shift=None, scale=None, mod_bstride=0, 
     return out
 
 
+def layernorm_modulate_fp8(x, x8, qscale, eps=1e-6, shift=None, scale=None, mod_bstride=0, rows_per_batch=0,
+                           weight=None, bias=None):
+    """layernorm_modulate straight into fp8_linear's activation quantisation: x8 [M, D] uint8 (e4m3fn
+    bytes), qscale [M] fp32 -- equal to quant_fp8_rows of layernorm_modulate's bf16 output."""
+    M, D, ldx = _rows(x, "x")
+    if x8.dtype != torch.uint8 or x8.dim() != 2 or x8.shape[0] != M or x8.shape[1] < D or x8.stride(1) != 1:
+        raise ValueError("layernorm_modulate_fp8: x8 must be uint8 [M, >=D] with unit column stride")
+    if qscale.dtype != torch.float32 or qscale.numel() < M or not qscale.is_contiguous():
+        raise ValueError("layernorm_modulate_fp8: qscale must be contiguous float32 [M]")
+    _lib.check(_lib.load().vs_layernorm_modulate_fp8(x.data_ptr(), ldx, x8.data_ptr(), x8.stride(0), qscale.data_ptr(),
+                                                     M, D, int(rows_per_batch), _ptr(shift), _ptr(scale),
+                                                     int(mod_bstride), _ptr(weight), _ptr(bias), float(eps),
+                                                     _stream(x)))
+    return x8, qscale
+
+
 def residual_layernorm(y, x, out, eps=1e-6, epilogue=VS_EPI_GATE_RES, gate=None, gate_bstride=0, gate_rows=0,
                        alpha=1.0, hint=None, hint_scale=1.0, shift=None, scale=None, mod_bstride=0,
                        rows_per_batch=0, weight=None, bias=None):

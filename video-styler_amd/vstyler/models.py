@@ -33,20 +33,55 @@ class Linear(nn.Module):
         self.bias = _param(out_features, device=device, dtype=dtype) if bias else None
 
 
+class Q8:
+    """An activation already quantised for fp8_linear (x8 e4m3 bytes [M, K], per-row scale [M]): what
+    ln_into() hands to linear() / fused_linear() when the consumer is an fp8 layer."""
+
+    def __init__(self, x8, scale):
+        self.x8, self.scale = x8, scale
+        self.shape = x8.shape
+
+
+def _fp8_consumer(target):
+    """True when `target` (a Linear, or a module whose fused projections run as one GEMM) consumes
+    its input through fp8_linear."""
+    if isinstance(target, AttentionParams):
+        f = _fused_views(target)
+        return f is not None and f[2] is not None
+    return getattr(target, "weight_fp8", None) is not None and getattr(target, "lora_A", None) is None
+
+
+def ln_into(x, h, ws, target, eps, **ln):
+    """LayerNorm(+modulate) of x for `target`'s projection: into the bf16 buffer h, or -- when target
+    runs fp8_linear -- straight into its quantised activation (vs_layernorm_modulate_fp8: the bf16 row
+    is never stored and not re-read; bit-identical)."""
+    if target is not None and _fp8_consumer(target):
+        M, D = x.shape
+        return Q8(*K.layernorm_modulate_fp8(x, ws.get("fp8_x", (M, D), torch.uint8),
+                                            ws.get("fp8_scale", (M,), torch.float32), eps, **ln))
+    K.layernorm_modulate(x, h, eps, **ln)
+    return h
+
+
 def linear(lin, x, out, ws, **epi):
     """Linear through vs_gemm; a hot-loaded LoRA (lin.lora_A = alpha*A, lin.lora_B = B) is fused as
     the GEMM's second K phase (AutoWrappedLinear, vram_management/layers.py:173-188).  A layer
     converted by quantize_fp8_ runs the fp8 path of AutoWrappedLinear.fp8_linear (:115-151):
-    per-row activation quantisation + e4m3 MFMA GEMM with the same fused epilogue."""
+    per-row activation quantisation (or the Q8 input ln_into made) + e4m3 MFMA GEMM with the same
+    fused epilogue."""
     w8 = getattr(lin, "weight_fp8", None)
     if w8 is not None:
         if getattr(lin, "lora_A", None) is not None:
             raise NotImplementedError("hot-loaded LoRA on an fp8 layer: merge the LoRA before quantize_fp8_")
+        if isinstance(x, Q8):
+            return K.gemm_fp8(x.x8, x.scale, w8, out, bias=lin.bias, **epi)
         M, Kd = x.shape
         x8 = ws.get("fp8_x", (M, Kd), torch.uint8)
         sc = ws.get("fp8_scale", (M,), torch.float32)
         K.quant_fp8_rows(x, x8, sc)
         return K.gemm_fp8(x8, sc, w8, out, bias=lin.bias, **epi)
+    if isinstance(x, Q8):
+        raise ValueError("a quantised activation for a bf16 layer")
     la = getattr(lin, "lora_A", None)
     a2 = w2 = None
     if la is not None:
@@ -179,6 +214,8 @@ def fused_linear(mod, x, ws, tag):
         return None
     W, b, W8 = f
     out = ws.get("fused" + tag, (x.shape[0], W.shape[0]))
+    if W8 is not None and isinstance(x, Q8):
+        return K.gemm_fp8(x.x8, x.scale, W8, out, bias=b)
     if W8 is not None:
         M, Kd = x.shape
         x8 = ws.get("fp8_x", (M, Kd), torch.uint8)
@@ -353,7 +390,7 @@ class DiTBlock(nn.Module):
         for p in parts:
             self._phase_attn(p, rc)
         for p in parts:
-            self._phase_o(p, rc)
+            self._phase_o(p, rc, direct=tail is None)
             if tail is None:
                 self._phase_cross_ffn(p, rc, hint_scale, fuse)
         if tail is not None:
@@ -379,10 +416,10 @@ class DiTBlock(nn.Module):
         # --- self-attention inputs (wan_video_dit.py:225-226, :140-145)
         S, D, eps, ws = rc.seq, self.dim, self.eps, rc.ws
         mod, h, q, k, v = p["mod"], p["h"], p["q"], p["k"], p["v"]
-        if not p["ln1_done"]:
-            K.layernorm_modulate(p["x"], h, eps, shift=mod[:, 0], scale=mod[:, 1], mod_bstride=6 * D,
-                                 rows_per_batch=S)
         sa = self.self_attn
+        if not p["ln1_done"]:
+            h = ln_into(p["x"], h, ws, sa, eps, shift=mod[:, 0], scale=mod[:, 1], mod_bstride=6 * D,
+                        rows_per_batch=S)
         qkv = fused_linear(sa, h, ws, "qkv" + p["tag"])
         if qkv is not None:            # one GEMM; q/k/v are column slices of [M, 3D]
             q, k, v = p["q"], p["k"], p["v"] = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
@@ -405,7 +442,9 @@ class DiTBlock(nn.Module):
             K.attention(p["q"], p["k"], p["v"], p["o"], self.num_heads, p["nb"])
             TIMER.stop(ev)
 
-    def _phase_o(self, p, rc):
+    def _phase_o(self, p, rc, direct=True):
+        """direct: this part's cross-attention runs next (its LN3 may go straight into an fp8 cross-q's
+        quantised input); False: the merged SP tail reads the bf16 LN3 rows of every part."""
         S, D, eps, ws = rc.seq, self.dim, self.eps, rc.ws
         x, mod, h, o, M = p["x"], p["mod"], p["h"], p["o"], p["M"]
         if rc.sp is not None:
@@ -421,14 +460,15 @@ class DiTBlock(nn.Module):
             linear(sa.o, o, x, ws, epilogue=K.VS_EPI_GATE_RES, residual=x, gate=mod[:, 2],
                    gate_bstride=6 * D, rows_per_batch=S)
             # --- cross-attention (wan_video_dit.py:227, :171-186)
-            K.layernorm_modulate(x, h, eps, weight=self.norm3.weight, bias=self.norm3.bias)
+            p["h3"] = ln_into(x, h, ws, self.cross_attn.q if direct else None, eps, weight=self.norm3.weight,
+                              bias=self.norm3.bias)
 
     def _phase_cross_ffn(self, p, rc, hint_scale, fuse=None):
         S, D, eps, ws = rc.seq, self.dim, self.eps, rc.ws
         x, mod, h, q, o, nb, M = p["x"], p["mod"], p["h"], p["q"], p["o"], p["nb"], p["M"]
         ca = self.cross_attn
         L = rc.ctx_len
-        linear(ca.q, h, q, ws)
+        linear(ca.q, p.pop("h3", h), q, ws)
         K.rmsnorm_rope(q, ca.norm_q.weight, eps)
         kv = fused_linear(ca, p["ctx"], ws, "kvc" + p["tag"])
         if kv is not None:
@@ -447,7 +487,8 @@ class DiTBlock(nn.Module):
         else:
             linear(ca.o, o, x, ws, epilogue=K.VS_EPI_RES, residual=x)
             # --- FFN (wan_video_dit.py:228-229) + VACE hint (wan_video_new.py:1450)
-            K.layernorm_modulate(x, h, eps, shift=mod[:, 3], scale=mod[:, 4], mod_bstride=6 * D, rows_per_batch=S)
+            h = ln_into(x, h, ws, self.ffn[0], eps, shift=mod[:, 3], scale=mod[:, 4], mod_bstride=6 * D,
+                        rows_per_batch=S)
         f = ws.get("f" + p["tag"], (M, self.ffn_dim))
         linear(self.ffn[0], h, f, ws, epilogue=K.VS_EPI_GELU)
         if fuse is not None:
