@@ -20,7 +20,7 @@ def _k():
     return K
 
 
-@pytest.mark.parametrize("cols", [640, 5120, 13824, 20000])   # row in registers (<= 4 / 12 / 28 chunks), two-pass
+@pytest.mark.parametrize("cols", [640, 5120, 13824, 16384, 20000])   # wave per row (<= 4 / 12 chunks), block per row, two-pass
 def test_quant_fp8_rows_bit_exact(cols):
     K = _k()
     g = torch.Generator().manual_seed(1)
