@@ -677,16 +677,19 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
         if (t < nkv) {
             iteration(T, s1b, s1a, p0b, p0a, std::false_type{});
             ++T;
-            if (nxt >= 0) next_q(nxt);
             swst(3);
             drain(T - 1, s1b, p0b);
         } else {
-            if (nxt >= 0) next_q(nxt);
             swst(3);
             drain(T - 1, s1a, p0a);
         }
         swst(4);
         finish(o_base(bh_done), q0_done, cur);
+        // the next item's Q after the O store (r5): its loads wait at once anyway (the scaling
+        // pass), and loaded before the drain the new Q was live beside the old O through the drain
+        // and the store -- the register allocator spilled part of it (scratch reloads whose vmcnt
+        // waits drained the K/V DMA, profiles/r5/w4_lasttile_s16.log)
+        if (nxt >= 0) next_q(nxt);
         swst(5);
         sw_store();
         if (nxt < 0) break;
