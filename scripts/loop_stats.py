@@ -1,7 +1,10 @@
 """Loop bodies of a disassembled gfx950 code object (llvm-objdump -d --no-show-raw-insn output): per
 kernel, every backward branch's body length in instructions and its scratch (spill) accesses --
 to check that a hand-scheduled inner loop stays spill-free after a change.
-usage: python3 scripts/loop_stats.py <disasm.s> [min_len] [max_len]"""
+usage: python3 scripts/loop_stats.py <disasm.s> [min_len] [max_len]   (LOOP_MIX=n: the n commonest
+opcodes of each loop too)"""
+import collections
+import os
 import re
 import sys
 
@@ -29,10 +32,14 @@ def main():
                 if tgt < a and tgt in idx:
                     body = ins[idx[tgt]:idx[a] + 1]
                     if lo <= len(body) <= hi:
-                        loops.add((len(body), sum(1 for _, x in body if x.startswith("scratch_")), hex(tgt)))
+                        mix = collections.Counter(x.split()[0] for _, x in body)
+                        loops.add((len(body), sum(1 for _, x in body if x.startswith("scratch_")), hex(tgt),
+                                   tuple(mix.most_common(int(os.environ.get("LOOP_MIX", "0"))))))
         print(m.group(2), "instructions", len(ins), "scratch", sum(1 for _, x in ins if x.startswith("scratch_")))
-        for n, sc, t in sorted(loops):
+        for n, sc, t, mix in sorted(loops):
             print(f"  loop at {t}: {n} instructions, {sc} scratch")
+            if mix:
+                print("    " + " ".join(f"{k} {v}" for k, v in mix))
 
 
 if __name__ == "__main__":

@@ -436,11 +436,28 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
     auto swst = [](int) {};
     auto sw_store = [] {};
 #endif
-    auto rdK = [&](bf16x8_t& d, int T, int kb, int j) __attribute__((always_inline)) {
-        d = lds16(smem_base + (T & 3) * W4_SLOT + koff[j] + kb * 32 * 256);
+    // K fragment addresses: the slot's base + the lane's swizzled offset, made opaque once per tile
+    // (in phase D, for its kb0 reads and the next phase A's kb1 reads), so the kb displacement
+    // folds into the ds instruction's offset field -- with the slot base added in an SGPR, every
+    // read cost its own v_add_u32.  -3.4 % self-attention time (profiles/r5/attn_ldsbase_kv_ab_s24.log:
+    // the same for V bases too cost 4 more live VGPRs and measured no better than K alone)
+    unsigned kbs[8], vbs[4];
+    auto kbase = [&](int T) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            kbs[j] = smem_base + (T & 3) * W4_SLOT + koff[j];
+            asm volatile("" : "+v"(kbs[j]));
+        }
     };
-    auto rdV = [&](bf16x8_t& d, int T, int ks, int dt) __attribute__((always_inline)) {
-        const unsigned a0 = smem_base + (T & 3) * W4_SLOT + voff[dt] + ks * 16 * 256;
+    auto vbase = [&](int T) __attribute__((always_inline)) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) vbs[dt] = smem_base + (T & 3) * W4_SLOT + voff[dt];
+    };
+    auto rdK = [&](bf16x8_t& d, int kb, int j) __attribute__((always_inline)) {
+        d = lds16(kbs[j] + kb * 32 * 256);
+    };
+    auto rdV = [&](bf16x8_t& d, int ks, int dt) __attribute__((always_inline)) {
+        const unsigned a0 = vbs[dt] + ks * 16 * 256;
         const i16x4_t v0 = tr8(a0), v1 = tr8(a0 + 8 * 256);
         d = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, v0), __builtin_bit_cast(bf16x4_t, v1), 0, 1, 2,
                                     3, 4, 5, 6, 7);
@@ -466,7 +483,10 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
         asm volatile("" : "+a"(o[rb][dt]));
     };
     // softmax of elements e, e+1 of one 16-value S block of row block rb: P pair -> dword
-    // (e >> 1) & 3 of k-step (e >> 3) of pkd, the two p into rb's row sum
+    // (e >> 1) & 3 of k-step (e >> 3) of pkd, the two p into rb's row sum.  The two v_add_f32
+    // stay: packed (v_pk_add_f32 on a pair) or one v_dot2c_f32_bf16 of the packed P with (1, 1)
+    // issue fewer VALU ops but stall beside the MFMAs -- +6 % and +11 % self-attention time
+    // (profiles/r5/attn_pksum_ldsbase_ab_s23.log, attn_dot2_rowsum_ab_s25.log)
     auto smp = [&](const f32x16_t& sv, int e, u32x4_t (&pkd)[2], int rb) __attribute__((always_inline)) {
         const float pa = __builtin_amdgcn_exp2f(sv[e]), pb = __builtin_amdgcn_exp2f(sv[e + 1]);
         lsum[rb] += pa + pb;
@@ -528,7 +548,7 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {                                   // A
             float pa = 0.f, pb = 0.f;
-            rdK(kf1[j], T, 1, j);
+            rdK(kf1[j], 1, j);
             mfK1(kf0[j], j, s0, 0);
             fence();
             if (!FIRST) smp_e(s1p[0], 2 * j, pa, pb);
@@ -539,10 +559,11 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
             fence();
         }
         stamp(1);
+        if (!FIRST) vbase(T - 1);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {                                   // B
             float pa = 0.f, pb = 0.f;
-            if (!FIRST) rdV(vfa[j], T - 1, j >> 2, j & 3);
+            if (!FIRST) rdV(vfa[j], j >> 2, j & 3);
             mfK1(kf1[j], j, s1c, 0);
             fence();
             if (!FIRST) smp_e(s1p[1], 2 * j, pa, pb);
@@ -559,8 +580,8 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
                 // V ks2,3 fragments in the first half of C: the lgkmcnt(0) before the barrier
                 // then finds them landed
                 if (i < 4) {
-                    rdV(vfb[2 * i], T - 1, 2 + (i >> 1), (2 * i) & 3);
-                    rdV(vfb[2 * i + 1], T - 1, 2 + (i >> 1), (2 * i + 1) & 3);
+                    rdV(vfb[2 * i], 2 + (i >> 1), (2 * i) & 3);
+                    rdV(vfb[2 * i + 1], 2 + (i >> 1), (2 * i + 1) & 3);
                 }
                 mfV(vfa[i], p0p, i >> 2, i & 3);
             }
@@ -569,13 +590,14 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
             fence();
         }
         sync(T, first_c);
+        kbase(T + 1);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {                                   // D
             if (FIRST) stage_piece(i);
             else piece_go(i);
             if (FIRST && i == 0)            // the item after this one (written by wave 0 before B(T+1))
                 qv = *(volatile LDS_AS int*)(uintptr_t)(smem_base + W4_QSLOT);
-            rdK(kf0[i], T + 1, 0, i);
+            rdK(kf0[i], 0, i);
             if (!FIRST) {
                 mfV1(vfb[i], p1, i >> 2, i & 3, 0);
                 fence();
@@ -597,15 +619,16 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
     };
     // after the item's last tile TL: S(TL) kb1 -> P ks2,3, PV(TL)
     auto drain = [&](int TL, const f32x16_t (&s1l)[2], const u32x4_t (&p0l)[2][2]) __attribute__((always_inline)) {
+        vbase(TL);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            rdV(vfa[j], TL, j >> 2, j & 3);
+            rdV(vfa[j], j >> 2, j & 3);
             smp(s1l[0], 2 * j, p1[0], 0);
             fence();
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            rdV(vfb[j], TL, 2 + (j >> 2), j & 3);
+            rdV(vfb[j], 2 + (j >> 2), j & 3);
             smp(s1l[1], 2 * j, p1[1], 1);
             fence();
         }
@@ -621,8 +644,9 @@ __global__ __launch_bounds__(W4_THR, 1) void attn_fwd_w4(const AttnArgs args) {
     asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
     fence();
     stage(2);
+    kbase(0);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) rdK(kf0[i], 0, 0, i);
+    for (int i = 0; i < 8; ++i) rdK(kf0[i], 0, i);
     int T = 0, q0 = 0;
     int bh = item_bh(cur, q0);
     q0 += 64 * wave;
