@@ -47,7 +47,8 @@ int vs_abi_version(void);
 #define VS_OPT_ATTN_PERSIST 8  /* 1: persistent item walk (default); 0: one block per item             */
 #define VS_OPT_VAE_PXB 9       /* 2 (default) / 1: 128-pixel blocks per wave of the VAE conv            */
 #define VS_OPT_VAE_PRE 10      /* 3 (default) / 2 / 1: register stages of the VAE conv's gathers        */
-#define VS_OPT_COUNT 11
+#define VS_OPT_VAE_HALO 11     /* 1 (default): the VAE's 3x3(x3) stride-1 convs on the patch-resident kernel; 0: per-tap gathers */
+#define VS_OPT_COUNT 12
 int vs_set_option(int id, int value);
 int vs_get_option(int id);
 

@@ -88,10 +88,36 @@ def test_conv_pixel_blocks_bit_identical(cin, cout, up2, opt):
     cw = vae.ConvW(_rand((cout, cin, 3, 3, 3), g, 1 / math.sqrt(27 * cin)), _rand((cout,), g, 0.1), "cuda")
     outs = []
     for pxb, pre in ((1, 1), (2, 1), (1, 2), (2, 2), (1, 3), (2, 3)):
-        opt(vae_pxb=pxb, vae_pre=pre)
+        opt(vae_pxb=pxb, vae_pre=pre, vae_halo=0)
         outs.append(vae.conv(x, cw, (5, 2 * h if up2 else h, 2 * w if up2 else w), pad=(2, 1, 1), up2=up2).cpu())
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
+
+
+@pytest.mark.parametrize("cin,cout,kt,t_lo,h,w", [(96, 96, 3, 0, 17, 45), (32, 192, 3, 2, 9, 33),
+                                                  (192, 96, 1, 0, 16, 64), (384, 384, 3, 0, 8, 32)])
+def test_conv_halo_kernel(cin, cout, kt, t_lo, h, w, opt):
+    """The patch-resident 3x3(x3) kernel (option vae_halo, the default for these shapes) vs a
+    bf16-rounded fp32 torch conv and vs the per-tap gather kernel: ragged 8 x 32 tiles, the causal
+    time pad, frames below t_lo read as zero, a 2-D (kt = 1) conv, two batch slices."""
+    vae = _vae()
+    g = torch.Generator().manual_seed(cin + 3 * cout + kt)
+    T = 5
+    x = _rand((2, cin, T, h, w), g)
+    wt = _rand((cout, cin, kt, 3, 3), g, 1 / math.sqrt(9 * kt * cin))
+    b = _rand((cout,), g, 0.1)
+    xz = x.clone()
+    xz[:, :, :t_lo] = 0
+    pt = kt - 1
+    ref = F.conv3d(F.pad(xz.float(), (1, 1, 1, 1, pt, 0)), wt.float(), b.float()).to(BF16)
+    cw = vae.ConvW(wt, b, "cuda")
+    xg = _to_nthwc(x)
+    outs = []
+    for halo in (1, 0):
+        opt(vae_halo=halo)
+        outs.append(_from_nthwc(vae.conv(xg, cw, (T, h, w), pad=(pt, 1, 1), t_lo=t_lo), cout))
+    _close_conv(outs[0], ref)
+    _close_conv(outs[0], outs[1])
 
 
 def test_rgb_input_conv_channel_padding():

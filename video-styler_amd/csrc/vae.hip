@@ -32,6 +32,55 @@ __device__ __forceinline__ int swz(int row, int ch) {
     return row * 64 + 16 * (ch ^ ((((row >> 1) ^ (row >> 2)) & 1) | ((row >> 2) & 2)));
 }
 
+// The conv's output store for one pixel (n, to, yo, xo) of slice z: a lane's NB accumulator blocks hold
+// channels n0 + 32j + 8g + 4h + {0..3} (h = lane >> 5) -- bias, residual, the time interleave of
+// `split`, bf16 rounding (or fp32 alpha * acc) as vs_conv3d documents.
+template <int NB, bool F32>
+__device__ __forceinline__ void conv_store(const vs_conv3d& p, const f32x16_t (&acc)[NB], int z, long long nn, int to,
+                                           int yo, int xo, int n0, int lane) {
+    const int h = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = n0 + 32 * j + 8 * g + 4 * h;
+            if (n >= p.cout) continue;
+            int co = n, sub = 0;
+            if (p.split > 0 && n >= p.split) { co = n - p.split; sub = 1; }
+            const int tt = to * p.t_mul + p.t_add + sub;
+            const long long off = z * p.y_zs + nn * p.y_ns + ((long long)(tt * p.h_out + yo) * p.w_out + xo) * p.ldy + co;
+            const int nv = min(4, p.cout - n);
+            if constexpr (F32) {
+                float* y = (float*)p.y + off;
+                if (nv == 4) {
+                    *(f32x4_t*)y = f32x4_t{p.alpha * acc[j][4 * g], p.alpha * acc[j][4 * g + 1],
+                                           p.alpha * acc[j][4 * g + 2], p.alpha * acc[j][4 * g + 3]};
+                } else {
+                    for (int e = 0; e < nv; ++e) y[e] = p.alpha * acc[j][4 * g + e];
+                }
+            } else {
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float a = acc[j][4 * g + e];
+                    if (p.bias && e < nv) a += bf2f(((const bf16_t*)p.bias)[n + e]);
+                    v[e] = rbf(a);
+                }
+                bf16_t* y = (bf16_t*)p.y + off;
+                if (p.res) {
+                    const bf16_t* r = (const bf16_t*)p.res + off;
+                    for (int e = 0; e < nv; ++e) v[e] = rbf(v[e] + bf2f(r[e]));
+                }
+                if (nv == 4) {
+                    *(u32x2_t*)y = u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
+                } else {
+                    for (int e = 0; e < nv; ++e) y[e] = (bf16_t)f2bf(v[e]);
+                }
+            }
+        }
+    }
+}
+
 template <int NB, bool F32, int PXB, int PRE>
 __global__ __launch_bounds__(CNTHR, 2) void vae_conv_kernel(vs_conv3d p, long long M, int ntn) {
     // PRE = 2: two register stages, the global loads of step s+2 issued before step s's MFMAs (two
@@ -218,7 +267,6 @@ __global__ __launch_bounds__(CNTHR, 2) void vae_conv_kernel(vs_conv3d p, long lo
     }
 
     // ---- epilogue: lane owns pixel m, channels n0 + 32j + 8g + 4h + {0..3}
-    const int h = lane >> 5;
 #pragma unroll
     for (int b = 0; b < PXB; ++b) {
         const long long me = m0 + BM * b + wave * 32 + (lane & 31);
@@ -228,46 +276,186 @@ __global__ __launch_bounds__(CNTHR, 2) void vae_conv_kernel(vs_conv3d p, long lo
         const int yo = (int)(q % p.h_out); q /= p.h_out;
         const int to = (int)(q % p.t_out);
         const long long nn = q / p.t_out;
+        conv_store<NB, F32>(p, acc[b], z, nn, to, yo, xo, n0, lane);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// vae_conv_halo_kernel (r5): the 3x3(x3) stride-1 convs (ResidualBlock / middle / head CausalConv3d,
+// 71 % + of the VAE's conv time) with the input read ONCE per (input frame, 32-channel chunk) instead
+// of once per tap.  The implicit GEMM above gathers a 256-pixel x 32-channel A tile per tap: 27
+// gathers of every input pixel from L2 per output (N = 96 channels gives 96 FLOP per byte gathered,
+// and a plain GEMM of the same K with contiguous rows runs slower still, HBM-bound:
+// profiles/r5/vae_conv_probe_s26.log).  Here a workgroup owns an 8 x 32 output tile of one frame and
+// 32 * NB output channels; per stage (channel chunk c, time tap kt) it LDS-DMAs the 10 x 34 input
+// patch of frame t + kt - pt (pitch 36 pixels, 64 B each) and the 9 spatial taps' weights
+// (9 x 32NB rows x 64 B), and runs all 9 taps from LDS.  Two stages in LDS (154 KB: one workgroup
+// per CU), the DMA of stage s + 1 in flight during stage s.  Padding and the causal time pad:
+// a patch pixel outside the frame loads through an out-of-range buffer offset, which the buffer
+// unit returns as zero; a time tap outside [t_lo, t_in) is skipped (its contribution is zero).
+// LDS swizzle: chunk k of patch pixel (row, col) at k ^ ((col >> 2) & 3), of weight row r at
+// k ^ ((r >> 2) & 3): with the 2304-B patch row pitch (a multiple of the 256-B bank window) every
+// fragment read -- 32 consecutive columns from any start column 0..2 -- is conflict-free for both
+// ds_read_b128 lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}: per column residue four
+// distinct chunks).  The K order per output differs from vae_conv_kernel's (chunk-major instead
+// of tap-major): results agree to bf16 rounding of the fp32 sums.
+typedef int i32x4h_t __attribute__((ext_vector_type(4)));
+constexpr int HT = 8, HW = 32, HPITCH = 36, HPROWS = HT + 2;
+constexpr int HPATCH_SLOTS = 368;                              // 10 x 36 pixels, rounded up to 16
+constexpr int HPATCH_B = HPATCH_SLOTS * 64;
+constexpr int HPATCH_Q = HPATCH_SLOTS / 16;                    // 23 DMA instructions of 1 KB
+template <int NB> constexpr int halo_w_bytes() { return 9 * 32 * NB * 64; }
+template <int NB> constexpr int halo_buf_bytes() { return HPATCH_B + halo_w_bytes<NB>(); }
+
+template <int NB, bool F32>
+__global__ __launch_bounds__(CNTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int tiles_x, int tiles_y) {
+    constexpr int BN = 32 * NB, WQ = 9 * BN / 16, BUF = halo_buf_bytes<NB>();
+    constexpr int PQW = (HPATCH_Q + 3) / 4, WQW = (WQ + 3) / 4;   // DMA instructions per wave
+    extern __shared__ __attribute__((aligned(16))) char hsmem[];
+    const unsigned smem_base = (unsigned)(uintptr_t)hsmem;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n0 = blockIdx.y * BN, z = blockIdx.z;
+    // XCD-aware order: workgroup b runs on XCD b % 8, which takes a contiguous eighth of the work
+    // list (n, tile row, tile column, output frame -- frame fastest), so one XCD's CUs work on
+    // consecutive frames of the same tile at once and the three frames each input frame feeds read
+    // its patch from that XCD's L2 instead of HBM
+    const long long nblk = (long long)p.n * tiles_y * tiles_x * p.t_out, per = (nblk + 7) / 8;
+    long long bid = (long long)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (bid >= nblk) return;
+    const int to = (int)(bid % p.t_out); bid /= p.t_out;
+    const int tx = (int)(bid % tiles_x); bid /= tiles_x;
+    const int ty = (int)(bid % tiles_y);
+    const long long nn = bid / tiles_y;
+    const int x0 = tx * HW, y0 = ty * HT;
+    const int tb = to - p.pt;                                   // input frame of time tap 0 (st = 1)
+    const int kt_lo = max(0, p.t_lo - tb), kt_hi = min(p.kt, p.t_in - tb);
+    const int nkt = max(0, kt_hi - kt_lo);
+    const int nst = nkt * (p.cin / BK);
+
+    auto rsrc = [](const void* base, unsigned bytes) {
+        const unsigned long long a = (unsigned long long)(uintptr_t)base;
+        return i32x4h_t{(int)(unsigned)a, (int)((unsigned)(a >> 32) & 0xffffu), (int)bytes, 0x00020000};
+    };
+    const long long plane = (long long)p.h_in * p.w_in * p.ldx * 2;      // bytes per input frame
+    i32x4h_t xr = rsrc((const bf16_t*)p.x + z * p.x_zs + nn * p.x_ns, (unsigned)(plane * p.t_in));
+    i32x4h_t wr = rsrc((const bf16_t*)p.w + z * p.w_zs + (long long)n0 * p.ldw,
+                       (unsigned)((long long)(p.cout - n0) * p.ldw * 2));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        xr[e] = __builtin_amdgcn_readfirstlane(xr[e]);
+        wr[e] = __builtin_amdgcn_readfirstlane(wr[e]);
+    }
+    // per-lane DMA source offsets (the uniform frame / chunk / tap-plane part goes in soffset)
+    unsigned pvo[PQW], wvo[WQW];
+#pragma unroll
+    for (int i = 0; i < PQW; ++i) {
+        const int P = 16 * (wave + 4 * i) + (lane >> 2);
+        const int pr = P / HPITCH, pc = P % HPITCH;
+        const int yi = y0 - p.ph + pr, xi = x0 - p.pw + pc;
+        const int lc = (lane & 3) ^ ((pc >> 2) & 3);
+        const bool v = pr < HPROWS && pc < HW + 2 && yi >= 0 && yi < p.h_in && xi >= 0 && xi < p.w_in;
+        pvo[i] = v ? (unsigned)(((long long)yi * p.w_in + xi) * p.ldx * 2 + lc * 16) : 0x80000000u;
+    }
+#pragma unroll
+    for (int i = 0; i < WQW; ++i) {
+        const int R = 16 * (wave + 4 * i) + (lane >> 2);
+        const int tap = R / BN, co = R % BN;
+        const int lc = (lane & 3) ^ ((co >> 2) & 3);
+        wvo[i] = (unsigned)((long long)co * p.ldw * 2 + tap * p.cin * 2 + lc * 16);
+    }
+    auto dma = [](unsigned lds, unsigned voff, i32x4h_t rs, int soff) __attribute__((always_inline)) {
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :: "s"(lds), "v"(voff), "s"(rs), "s"(soff) : "m0", "memory");
+    };
+    auto issue = [&](int s) __attribute__((always_inline)) {
+        // (uniform values the compiler may hold in VGPRs: the asm's "s" operands take readfirstlane)
+        const int c = s / nkt, kt = kt_lo + s % nkt;
+        const unsigned buf = __builtin_amdgcn_readfirstlane(smem_base + (s & 1) * BUF);
+        const int sx = __builtin_amdgcn_readfirstlane((int)((tb + kt) * plane) + c * 64);
+        const int sw = __builtin_amdgcn_readfirstlane((kt * 9 * p.cin + c * BK) * 2);
+#pragma unroll
+        for (int i = 0; i < PQW; ++i)
+            if (wave + 4 * i < HPATCH_Q) dma(buf + (wave + 4 * i) * 1024, pvo[i], xr, sx);
+#pragma unroll
+        for (int i = 0; i < WQW; ++i)
+            if (wave + 4 * i < WQ) dma(buf + HPATCH_B + (wave + 4 * i) * 1024, wvo[i], wr, sw);
+    };
+
+    f32x16_t acc[2][NB];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int n = n0 + 32 * j + 8 * g + 4 * h;
-                if (n >= p.cout) continue;
-                int co = n, sub = 0;
-                if (p.split > 0 && n >= p.split) { co = n - p.split; sub = 1; }
-                const int tt = to * p.t_mul + p.t_add + sub;
-                const long long off = z * p.y_zs + nn * p.y_ns + ((long long)(tt * p.h_out + yo) * p.w_out + xo) * p.ldy + co;
-                const int nv = min(4, p.cout - n);
-                if constexpr (F32) {
-                    float* y = (float*)p.y + off;
-                    if (nv == 4) {
-                        *(f32x4_t*)y = f32x4_t{p.alpha * acc[b][j][4 * g], p.alpha * acc[b][j][4 * g + 1],
-                                               p.alpha * acc[b][j][4 * g + 2], p.alpha * acc[b][j][4 * g + 3]};
-                    } else {
-                        for (int e = 0; e < nv; ++e) y[e] = p.alpha * acc[b][j][4 * g + e];
-                    }
-                } else {
-                    float v[4];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        float a = acc[b][j][4 * g + e];
-                        if (p.bias && e < nv) a += bf2f(((const bf16_t*)p.bias)[n + e]);
-                        v[e] = rbf(a);
-                    }
-                    bf16_t* y = (bf16_t*)p.y + off;
-                    if (p.res) {
-                        const bf16_t* r = (const bf16_t*)p.res + off;
-                        for (int e = 0; e < nv; ++e) v[e] = rbf(v[e] + bf2f(r[e]));
-                    }
-                    if (nv == 4) {
-                        *(u32x2_t*)y = u32x2_t{pack2(v[0], v[1]), pack2(v[2], v[3])};
-                    } else {
-                        for (int e = 0; e < nv; ++e) y[e] = (bf16_t)f2bf(v[e]);
-                    }
-                }
-            }
+            for (int r = 0; r < 16; ++r) acc[b][j][r] = 0.f;
+            asm volatile("" : "+a"(acc[b][j]));
         }
+
+    // wave w: output rows 2w, 2w + 1 of the tile (pixel blocks b), 32 columns, all NB channel blocks
+    const int hi = lane >> 5, l32 = lane & 31;
+    auto lds16 = [](unsigned addr) { return *reinterpret_cast<const LDS_AS bf16x8_t*>((const LDS_AS char*)(uintptr_t)addr); };
+    auto compute = [&](int s) __attribute__((always_inline)) {
+        const unsigned buf = smem_base + (s & 1) * BUF;
+        unsigned xb[3][2], wb2[2];
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int col = kx + l32;
+                xb[kx][ks] = buf + (2 * wave * HPITCH + col) * 64 + 16 * ((2 * ks + hi) ^ ((col >> 2) & 3));
+                asm volatile("" : "+v"(xb[kx][ks]));        // (row / tap displacements fold into ds offsets)
+            }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            wb2[ks] = buf + HPATCH_B + l32 * 64 + 16 * ((2 * ks + hi) ^ ((l32 >> 2) & 3));
+            asm volatile("" : "+v"(wb2[ks]));
+        }
+        // 18 steps (tap, 16-channel half); the fragments of step i + 1 are read before step i's
+        // MFMAs (one wave per SIMD: with the reads issued right before their MFMAs -- the compiler's
+        // schedule -- every step waited out the LDS latency with the MFMA pipe empty)
+        bf16x8_t xa[2][2], wf[2][NB];
+        auto rd = [&](int i, int buf2) __attribute__((always_inline)) {
+            const int tap = i >> 1, ks = i & 1, ky = tap / 3, kx = tap % 3;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) xa[buf2][b] = lds16(xb[kx][ks] + (b + ky) * HPITCH * 64);
+#pragma unroll
+            for (int j = 0; j < NB; ++j) wf[buf2][j] = lds16(wb2[ks] + (tap * BN + 32 * j) * 64);
+        };
+        rd(0, 0);
+#pragma unroll
+        for (int i = 0; i < 18; ++i) {
+            if (i + 1 < 18) rd(i + 1, (i + 1) & 1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < NB; ++j)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    acc[b][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i & 1][j], xa[i & 1][b], acc[b][j], 0, 0, 0);
+                    // (pinned to AGPRs: held in VGPRs across the stage loop, the accumulators
+                    // were copied into AGPRs and back every stage)
+                    asm volatile("" : "+a"(acc[b][j]));
+                }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+#ifndef VS_HALO_DIAG
+#define VS_HALO_DIAG 0      // diagnostic builds only (wrong results): 1 no DMA, 2 no MFMA, 3 no DMA wait
+#endif
+    if (nst > 0) {
+        if (VS_HALO_DIAG != 1) issue(0);
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        for (int s = 0; s < nst; ++s) {
+            if (s + 1 < nst && VS_HALO_DIAG != 1) issue(s + 1);
+            if (VS_HALO_DIAG != 2) compute(s);
+            if (VS_HALO_DIAG == 3) asm volatile("s_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int yo = y0 + 2 * wave + b, xo = x0 + l32;
+        if (yo < p.h_out && xo < p.w_out) conv_store<NB, F32>(p, acc[b], z, nn, to, yo, xo, n0, lane);
     }
 }
 
@@ -289,6 +477,33 @@ int launch_conv_px(const vs_conv3d& p, long long M, hipStream_t st) {
 // pipeline (the im2col gathers are latency-bound: with one stage 256-pixel tiles ran 0.68x of
 // 128-pixel ones).  Default 2 / 3, measured at 832x480x73 (profiles/r2/vae_conv_ab.log): tiled encode
 // 452 -> 498 TF/s, decode 467 -> 518 TF/s.  All variants are bit-identical (same K order per output).
+// The halo kernel's shapes: 3x3 spatial taps, stride 1, spatial pad 1, kt <= 3 (any time pad), no
+// upsample, whole 96-channel blocks, bf16 output, the frame slice and weight rows addressable with
+// 31-bit buffer offsets.
+bool halo_ok(const vs_conv3d& p) {
+    return vs_opt(VS_OPT_VAE_HALO) && !p.up2 && p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.st == 1 &&
+           p.ph == 1 && p.pw == 1 && p.kt <= 3 && p.cout % 96 == 0 && !p.out_f32 &&
+           (long long)p.t_in * p.h_in * p.w_in * p.ldx * 2 < (1LL << 31) && (long long)p.cout * p.ldw * 2 < (1LL << 31);
+}
+
+int launch_conv_halo(const vs_conv3d& p, hipStream_t st) {
+    constexpr int NB = 3;
+    const int tiles_x = (p.w_out + HW - 1) / HW, tiles_y = (p.h_out + HT - 1) / HT;
+    const long long nblk = (long long)p.n * p.t_out * tiles_y * tiles_x;
+    if (nblk > 0x7ffffff0LL) return VS_E_UNSUPPORTED;
+    const int lds = 2 * halo_buf_bytes<NB>();
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)vae_conv_halo_kernel<NB, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        attr = true;
+    }
+    hipLaunchKernelGGL((vae_conv_halo_kernel<NB, false>), dim3((unsigned)((nblk + 7) / 8 * 8), p.cout / (32 * NB), p.nz), dim3(CNTHR),
+                       lds, st, p, tiles_x, tiles_y);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
+}
+
 template <int NB>
 int launch_conv(const vs_conv3d& p, long long M, hipStream_t st) {
     const bool px2 = vs_opt(VS_OPT_VAE_PXB) == 2;
@@ -549,6 +764,7 @@ extern "C" int vs_vae_conv(const vs_conv3d* pp, void* stream) {
     if (p.t_out == 0) return VS_OK;
     const long long M = (long long)p.n * p.t_out * p.h_out * p.w_out;
     hipStream_t st = (hipStream_t)stream;
+    if (halo_ok(p)) return launch_conv_halo(p, st);
     if (p.cout <= 32) return launch_conv<1>(p, M, st);
     if (p.cout <= 64) return launch_conv<2>(p, M, st);
     if (p.cout <= 96) return launch_conv<3>(p, M, st);
