@@ -282,35 +282,40 @@ __global__ __launch_bounds__(CNTHR, 2) void vae_conv_kernel(vs_conv3d p, long lo
 
 // ------------------------------------------------------------------------------------------
 // vae_conv_halo_kernel (r5): the 3x3(x3) stride-1 convs (ResidualBlock / middle / head CausalConv3d,
-// 71 % + of the VAE's conv time) with the input read ONCE per (input frame, 32-channel chunk) instead
+// 71 % + of the VAE's conv time) with the input read ONCE per (input frame, channel chunk) instead
 // of once per tap.  The implicit GEMM above gathers a 256-pixel x 32-channel A tile per tap: 27
-// gathers of every input pixel from L2 per output (N = 96 channels gives 96 FLOP per byte gathered,
-// and a plain GEMM of the same K with contiguous rows runs slower still, HBM-bound:
-// profiles/r5/vae_conv_probe_s26.log).  Here a workgroup owns an 8 x 32 output tile of one frame and
-// 32 * NB output channels; per stage (channel chunk c, time tap kt) it LDS-DMAs the 10 x 34 input
-// patch of frame t + kt - pt (pitch 36 pixels, 64 B each) and the 9 spatial taps' weights
-// (9 x 32NB rows x 64 B), and runs all 9 taps from LDS.  Two stages in LDS (154 KB: one workgroup
-// per CU), the DMA of stage s + 1 in flight during stage s.  Padding and the causal time pad:
-// a patch pixel outside the frame loads through an out-of-range buffer offset, which the buffer
-// unit returns as zero; a time tap outside [t_lo, t_in) is skipped (its contribution is zero).
-// LDS swizzle: chunk k of patch pixel (row, col) at k ^ ((col >> 2) & 3), of weight row r at
-// k ^ ((r >> 2) & 3): with the 2304-B patch row pitch (a multiple of the 256-B bank window) every
+// gathers of every input pixel per output (N = 96 channels gives 96 FLOP per byte gathered, and a
+// plain GEMM of the same K with contiguous rows runs slower still, HBM-bound:
+// profiles/r5/vae_conv_probe_s26.log).  Here a workgroup (8 waves) owns a 16 x 32 output tile of
+// one frame and 32 * NB output channels; per stage (16-channel chunk c, time tap kt) it LDS-DMAs the
+// 18 x 34 input patch of frame t + kt - pt (pitch 40 pixels, 32 B each) and the 9 spatial taps'
+// weights (9 x 32NB rows x 32 B), and runs all 9 taps from LDS.  A ring of three stages (150 KB:
+// one workgroup per CU), the DMA two stages ahead.  The LDS-DMA bytes bound this kernel (diagnostic
+// builds of the first, 32-channel / 256-pixel version: the DMA alone 0.82 ms, the MFMAs alone
+// 1.05 ms, both 1.28 ms -- profiles/r5/vae_halo_diag_s29.log -- at the chip's LDS-DMA rate,
+// MI355X_MICROARCH 'ldsdma-fill'); 512-pixel tiles halve the weight bytes per FLOP, and 16-channel
+// stages fit the deeper ring.  Padding and the causal time pad: a patch pixel outside the frame
+// loads through an out-of-range buffer offset, which the buffer unit returns as zero; a time tap
+// outside [t_lo, t_in) is skipped (its contribution is zero).
+// LDS swizzle: half k of patch pixel (row, col) at k ^ ((col >> 3) & 1), of weight row r at
+// k ^ ((r >> 3) & 1): with the 1280-B patch row pitch (a multiple of the 256-B bank window) every
 // fragment read -- 32 consecutive columns from any start column 0..2 -- is conflict-free for both
-// ds_read_b128 lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}: per column residue four
-// distinct chunks).  The K order per output differs from vae_conv_kernel's (chunk-major instead
-// of tap-major): results agree to bf16 rounding of the fp32 sums.
+// ds_read_b128 lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}: the two lanes of each column
+// residue mod 8 sit 8 or 24 columns apart, so in opposite halves).  The K order per output differs
+// from vae_conv_kernel's (chunk-major instead of tap-major): results agree to bf16 rounding of the
+// fp32 sums.
 typedef int i32x4h_t __attribute__((ext_vector_type(4)));
-constexpr int HT = 8, HW = 32, HPITCH = 36, HPROWS = HT + 2;
-constexpr int HPATCH_SLOTS = 368;                              // 10 x 36 pixels, rounded up to 16
-constexpr int HPATCH_B = HPATCH_SLOTS * 64;
-constexpr int HPATCH_Q = HPATCH_SLOTS / 16;                    // 23 DMA instructions of 1 KB
-template <int NB> constexpr int halo_w_bytes() { return 9 * 32 * NB * 64; }
+constexpr int HTHR = 512, HT = 16, HW = 32, HPITCH = 40, HPROWS = HT + 2;
+constexpr int HPATCH_Q = (HPROWS * HPITCH + 31) / 32;          // 23 DMA instructions of 1 KB (32 slots)
+constexpr int HPATCH_B = HPATCH_Q * 1024;
+template <int NB> constexpr int halo_w_bytes() { return 9 * 32 * NB * 32; }
 template <int NB> constexpr int halo_buf_bytes() { return HPATCH_B + halo_w_bytes<NB>(); }
+constexpr int HSLOTS = 3;
 
 template <int NB, bool F32>
-__global__ __launch_bounds__(CNTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int tiles_x, int tiles_y) {
-    constexpr int BN = 32 * NB, WQ = 9 * BN / 16, BUF = halo_buf_bytes<NB>();
-    constexpr int PQW = (HPATCH_Q + 3) / 4, WQW = (WQ + 3) / 4;   // DMA instructions per wave
+__global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int tiles_x, int tiles_y) {
+    constexpr int BN = 32 * NB, WQ = 9 * BN / 32, BUF = halo_buf_bytes<NB>();
+    constexpr int PQW = (HPATCH_Q + 7) / 8, WQW = (WQ + 7) / 8;   // DMA instructions per wave (at most)
     extern __shared__ __attribute__((aligned(16))) char hsmem[];
     const unsigned smem_base = (unsigned)(uintptr_t)hsmem;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -318,7 +323,8 @@ __global__ __launch_bounds__(CNTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, in
     // XCD-aware order: workgroup b runs on XCD b % 8, which takes a contiguous eighth of the work
     // list (n, tile row, tile column, output frame -- frame fastest), so one XCD's CUs work on
     // consecutive frames of the same tile at once and the three frames each input frame feeds read
-    // its patch from that XCD's L2 instead of HBM
+    // its patch from that XCD's L2 instead of HBM (HBM bytes 2.74 -> 0.52 GB per launch of the
+    // dominant shape, profiles/r5/pmc_vaeconv_halo{,2})
     const long long nblk = (long long)p.n * tiles_y * tiles_x * p.t_out, per = (nblk + 7) / 8;
     long long bid = (long long)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
     if (bid >= nblk) return;
@@ -330,7 +336,7 @@ __global__ __launch_bounds__(CNTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, in
     const int tb = to - p.pt;                                   // input frame of time tap 0 (st = 1)
     const int kt_lo = max(0, p.t_lo - tb), kt_hi = min(p.kt, p.t_in - tb);
     const int nkt = max(0, kt_hi - kt_lo);
-    const int nst = nkt * (p.cin / BK);
+    const int nst = nkt * (p.cin / 16);
 
     auto rsrc = [](const void* base, unsigned bytes) {
         const unsigned long long a = (unsigned long long)(uintptr_t)base;
@@ -345,24 +351,27 @@ __global__ __launch_bounds__(CNTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, in
         xr[e] = __builtin_amdgcn_readfirstlane(xr[e]);
         wr[e] = __builtin_amdgcn_readfirstlane(wr[e]);
     }
-    // per-lane DMA source offsets (the uniform frame / chunk / tap-plane part goes in soffset)
+    // per-lane DMA source offsets (the uniform frame / chunk / tap-plane part goes in soffset); lane l
+    // fills 16-B half (l & 1) of slot 32q + (l >> 1)
     unsigned pvo[PQW], wvo[WQW];
 #pragma unroll
     for (int i = 0; i < PQW; ++i) {
-        const int P = 16 * (wave + 4 * i) + (lane >> 2);
+        const int P = 32 * (wave + 8 * i) + (lane >> 1);
         const int pr = P / HPITCH, pc = P % HPITCH;
         const int yi = y0 - p.ph + pr, xi = x0 - p.pw + pc;
-        const int lc = (lane & 3) ^ ((pc >> 2) & 3);
+        const int lc = (lane & 1) ^ ((pc >> 3) & 1);
         const bool v = pr < HPROWS && pc < HW + 2 && yi >= 0 && yi < p.h_in && xi >= 0 && xi < p.w_in;
         pvo[i] = v ? (unsigned)(((long long)yi * p.w_in + xi) * p.ldx * 2 + lc * 16) : 0x80000000u;
     }
 #pragma unroll
     for (int i = 0; i < WQW; ++i) {
-        const int R = 16 * (wave + 4 * i) + (lane >> 2);
+        const int R = 32 * (wave + 8 * i) + (lane >> 1);
         const int tap = R / BN, co = R % BN;
-        const int lc = (lane & 3) ^ ((co >> 2) & 3);
+        const int lc = (lane & 1) ^ ((co >> 3) & 1);
         wvo[i] = (unsigned)((long long)co * p.ldw * 2 + tap * p.cin * 2 + lc * 16);
     }
+    // this wave's DMA instructions per stage (the counted wait below)
+    const int nq = (wave < HPATCH_Q % 8 || HPATCH_Q % 8 == 0 ? PQW : PQW - 1) + (wave < WQ % 8 || WQ % 8 == 0 ? WQW : WQW - 1);
     auto dma = [](unsigned lds, unsigned voff, i32x4h_t rs, int soff) __attribute__((always_inline)) {
         asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                      :: "s"(lds), "v"(voff), "s"(rs), "s"(soff) : "m0", "memory");
@@ -370,15 +379,15 @@ __global__ __launch_bounds__(CNTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, in
     auto issue = [&](int s) __attribute__((always_inline)) {
         // (uniform values the compiler may hold in VGPRs: the asm's "s" operands take readfirstlane)
         const int c = s / nkt, kt = kt_lo + s % nkt;
-        const unsigned buf = __builtin_amdgcn_readfirstlane(smem_base + (s & 1) * BUF);
-        const int sx = __builtin_amdgcn_readfirstlane((int)((tb + kt) * plane) + c * 64);
-        const int sw = __builtin_amdgcn_readfirstlane((kt * 9 * p.cin + c * BK) * 2);
+        const unsigned buf = __builtin_amdgcn_readfirstlane(smem_base + (s % HSLOTS) * BUF);
+        const int sx = __builtin_amdgcn_readfirstlane((int)((tb + kt) * plane) + c * 32);
+        const int sw = __builtin_amdgcn_readfirstlane((kt * 9 * p.cin + c * 16) * 2);
 #pragma unroll
         for (int i = 0; i < PQW; ++i)
-            if (wave + 4 * i < HPATCH_Q) dma(buf + (wave + 4 * i) * 1024, pvo[i], xr, sx);
+            if (wave + 8 * i < HPATCH_Q) dma(buf + (wave + 8 * i) * 1024, pvo[i], xr, sx);
 #pragma unroll
         for (int i = 0; i < WQW; ++i)
-            if (wave + 4 * i < WQ) dma(buf + HPATCH_B + (wave + 4 * i) * 1024, wvo[i], wr, sw);
+            if (wave + 8 * i < WQ) dma(buf + HPATCH_B + (wave + 8 * i) * 1024, wvo[i], wr, sw);
     };
 
     f32x16_t acc[2][NB];
@@ -395,36 +404,31 @@ __global__ __launch_bounds__(CNTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, in
     const int hi = lane >> 5, l32 = lane & 31;
     auto lds16 = [](unsigned addr) { return *reinterpret_cast<const LDS_AS bf16x8_t*>((const LDS_AS char*)(uintptr_t)addr); };
     auto compute = [&](int s) __attribute__((always_inline)) {
-        const unsigned buf = smem_base + (s & 1) * BUF;
-        unsigned xb[3][2], wb2[2];
+        const unsigned buf = smem_base + (s % HSLOTS) * BUF;
+        unsigned xb[3], wb1;
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                const int col = kx + l32;
-                xb[kx][ks] = buf + (2 * wave * HPITCH + col) * 64 + 16 * ((2 * ks + hi) ^ ((col >> 2) & 3));
-                asm volatile("" : "+v"(xb[kx][ks]));        // (row / tap displacements fold into ds offsets)
-            }
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            wb2[ks] = buf + HPATCH_B + l32 * 64 + 16 * ((2 * ks + hi) ^ ((l32 >> 2) & 3));
-            asm volatile("" : "+v"(wb2[ks]));
+        for (int kx = 0; kx < 3; ++kx) {
+            const int col = kx + l32;
+            xb[kx] = buf + (2 * wave * HPITCH + col) * 32 + 16 * (hi ^ ((col >> 3) & 1));
+            asm volatile("" : "+v"(xb[kx]));        // (row / tap displacements fold into ds offsets)
         }
-        // 18 steps (tap, 16-channel half); the fragments of step i + 1 are read before step i's
-        // MFMAs (one wave per SIMD: with the reads issued right before their MFMAs -- the compiler's
-        // schedule -- every step waited out the LDS latency with the MFMA pipe empty)
+        wb1 = buf + HPATCH_B + l32 * 32 + 16 * (hi ^ ((l32 >> 3) & 1));
+        asm volatile("" : "+v"(wb1));
+        // 9 steps (taps); the fragments of step i + 1 are read before step i's MFMAs (with the
+        // reads issued right before their MFMAs -- the compiler's schedule -- every step waited
+        // out the LDS latency with the MFMA pipe empty)
         bf16x8_t xa[2][2], wf[2][NB];
-        auto rd = [&](int i, int buf2) __attribute__((always_inline)) {
-            const int tap = i >> 1, ks = i & 1, ky = tap / 3, kx = tap % 3;
+        auto rd = [&](int tap, int buf2) __attribute__((always_inline)) {
+            const int ky = tap / 3, kx = tap % 3;
 #pragma unroll
-            for (int b = 0; b < 2; ++b) xa[buf2][b] = lds16(xb[kx][ks] + (b + ky) * HPITCH * 64);
+            for (int b = 0; b < 2; ++b) xa[buf2][b] = lds16(xb[kx] + (b + ky) * HPITCH * 32);
 #pragma unroll
-            for (int j = 0; j < NB; ++j) wf[buf2][j] = lds16(wb2[ks] + (tap * BN + 32 * j) * 64);
+            for (int j = 0; j < NB; ++j) wf[buf2][j] = lds16(wb1 + (tap * BN + 32 * j) * 32);
         };
         rd(0, 0);
 #pragma unroll
-        for (int i = 0; i < 18; ++i) {
-            if (i + 1 < 18) rd(i + 1, (i + 1) & 1);
+        for (int i = 0; i < 9; ++i) {
+            if (i + 1 < 9) rd(i + 1, (i + 1) & 1);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = 0; j < NB; ++j)
@@ -439,24 +443,59 @@ __global__ __launch_bounds__(CNTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, in
         }
     };
 
+    // ring of HSLOTS stages, DMA two ahead: before stage s, wait for this wave's stage-s pieces
+    // (its stage-(s+1) pieces, issued later, may stay in flight: vmcnt(nq)), then the barrier makes
+    // every wave's pieces visible and frees slot (s+2) % 3 (stage s-1's, read by all waves)
 #ifndef VS_HALO_DIAG
-#define VS_HALO_DIAG 0      // diagnostic builds only (wrong results): 1 no DMA, 2 no MFMA, 3 no DMA wait
+#define VS_HALO_DIAG 0      // diagnostic builds only (wrong results): 1 no DMA, 2 no MFMA
 #endif
-    if (nst > 0) {
-        if (VS_HALO_DIAG != 1) issue(0);
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        for (int s = 0; s < nst; ++s) {
-            if (s + 1 < nst && VS_HALO_DIAG != 1) issue(s + 1);
-            if (VS_HALO_DIAG != 2) compute(s);
-            if (VS_HALO_DIAG == 3) asm volatile("s_barrier" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (nst > 0 && VS_HALO_DIAG != 1) issue(0);
+    if (nst > 1 && VS_HALO_DIAG != 1) issue(1);
+    for (int s = 0; s < nst; ++s) {
+        if (s + 1 < nst) {
+            if (nq == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+            else if (nq == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else if (nq == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        asm volatile("s_barrier" ::: "memory");
+        if (s + 2 < nst && VS_HALO_DIAG != 1) issue(s + 2);
+        if (VS_HALO_DIAG != 2) compute(s);
     }
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
         const int yo = y0 + 2 * wave + b, xo = x0 + l32;
         if (yo < p.h_out && xo < p.w_out) conv_store<NB, F32>(p, acc[b], z, nn, to, yo, xo, n0, lane);
     }
+}
+
+// The halo kernel's shapes: 3x3 spatial taps, stride 1, spatial pad 1, kt <= 3 (any time pad), no
+// upsample, whole 96-channel blocks, bf16 output, the frame slice and weight rows addressable with
+// 31-bit buffer offsets.
+bool halo_ok(const vs_conv3d& p) {
+    return vs_opt(VS_OPT_VAE_HALO) && !p.up2 && p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.st == 1 &&
+           p.ph == 1 && p.pw == 1 && p.kt <= 3 && p.cout % 96 == 0 && !p.out_f32 && p.cin % 16 == 0 &&
+           (long long)p.t_in * p.h_in * p.w_in * p.ldx * 2 < (1LL << 31) && (long long)p.cout * p.ldw * 2 < (1LL << 31);
+}
+
+int launch_conv_halo(const vs_conv3d& p, hipStream_t st) {
+    constexpr int NB = 3;
+    const int tiles_x = (p.w_out + HW - 1) / HW, tiles_y = (p.h_out + HT - 1) / HT;
+    const long long nblk = (long long)p.n * p.t_out * tiles_y * tiles_x;
+    if (nblk > 0x7ffffff0LL) return VS_E_UNSUPPORTED;
+    const int lds = HSLOTS * halo_buf_bytes<NB>();
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)vae_conv_halo_kernel<NB, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        attr = true;
+    }
+    hipLaunchKernelGGL((vae_conv_halo_kernel<NB, false>), dim3((unsigned)((nblk + 7) / 8 * 8), p.cout / (32 * NB), p.nz),
+                       dim3(HTHR), lds, st, p, tiles_x, tiles_y);
+    VS_CHECK_LAUNCH();
+    return VS_OK;
 }
 
 template <int NB, int PXB, int PRE>
@@ -477,33 +516,6 @@ int launch_conv_px(const vs_conv3d& p, long long M, hipStream_t st) {
 // pipeline (the im2col gathers are latency-bound: with one stage 256-pixel tiles ran 0.68x of
 // 128-pixel ones).  Default 2 / 3, measured at 832x480x73 (profiles/r2/vae_conv_ab.log): tiled encode
 // 452 -> 498 TF/s, decode 467 -> 518 TF/s.  All variants are bit-identical (same K order per output).
-// The halo kernel's shapes: 3x3 spatial taps, stride 1, spatial pad 1, kt <= 3 (any time pad), no
-// upsample, whole 96-channel blocks, bf16 output, the frame slice and weight rows addressable with
-// 31-bit buffer offsets.
-bool halo_ok(const vs_conv3d& p) {
-    return vs_opt(VS_OPT_VAE_HALO) && !p.up2 && p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.st == 1 &&
-           p.ph == 1 && p.pw == 1 && p.kt <= 3 && p.cout % 96 == 0 && !p.out_f32 &&
-           (long long)p.t_in * p.h_in * p.w_in * p.ldx * 2 < (1LL << 31) && (long long)p.cout * p.ldw * 2 < (1LL << 31);
-}
-
-int launch_conv_halo(const vs_conv3d& p, hipStream_t st) {
-    constexpr int NB = 3;
-    const int tiles_x = (p.w_out + HW - 1) / HW, tiles_y = (p.h_out + HT - 1) / HT;
-    const long long nblk = (long long)p.n * p.t_out * tiles_y * tiles_x;
-    if (nblk > 0x7ffffff0LL) return VS_E_UNSUPPORTED;
-    const int lds = 2 * halo_buf_bytes<NB>();
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)vae_conv_halo_kernel<NB, false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        attr = true;
-    }
-    hipLaunchKernelGGL((vae_conv_halo_kernel<NB, false>), dim3((unsigned)((nblk + 7) / 8 * 8), p.cout / (32 * NB), p.nz), dim3(CNTHR),
-                       lds, st, p, tiles_x, tiles_y);
-    VS_CHECK_LAUNCH();
-    return VS_OK;
-}
-
 template <int NB>
 int launch_conv(const vs_conv3d& p, long long M, hipStream_t st) {
     const bool px2 = vs_opt(VS_OPT_VAE_PXB) == 2;
