@@ -464,10 +464,37 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
         if (s + 2 < nst && VS_HALO_DIAG != 1) issue(s + 2);
         if (VS_HALO_DIAG != 2) compute(s);
     }
+    // epilogue (halo_ok: bf16 output, whole 4-channel groups, no time split, 8-B aligned y / res /
+    // bias): per lane and channel group one 8-B bias load, one rounding, one 8-B residual load and
+    // store -- the generic conv_store's per-element loads and branches were ~1.5 k VALU per wave
+    const bf16_t* bias = (const bf16_t*)p.bias;
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
         const int yo = y0 + 2 * wave + b, xo = x0 + l32;
-        if (yo < p.h_out && xo < p.w_out) conv_store<NB, F32>(p, acc[b], z, nn, to, yo, xo, n0, lane);
+        if (yo >= p.h_out || xo >= p.w_out) continue;
+        const long long pix = z * p.y_zs + nn * p.y_ns +
+                              ((long long)((to * p.t_mul + p.t_add) * p.h_out + yo) * p.w_out + xo) * p.ldy;
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n = n0 + 32 * j + 8 * g + 4 * hi;
+                float a[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) a[e] = acc[b][j][4 * g + e];
+                if (bias) {
+                    const u32x2_t bb = *(const u32x2_t*)(bias + n);
+                    a[0] += bf2f(bb[0] & 0xffffu); a[1] += bf2f(bb[0] >> 16);
+                    a[2] += bf2f(bb[1] & 0xffffu); a[3] += bf2f(bb[1] >> 16);
+                }
+                u32x2_t v = {pack2(a[0], a[1]), pack2(a[2], a[3])};
+                if (p.res) {
+                    const u32x2_t rr = *(const u32x2_t*)((const bf16_t*)p.res + pix + n);
+                    v[0] = pack2(bf2f(v[0] & 0xffffu) + bf2f(rr[0] & 0xffffu), bf2f(v[0] >> 16) + bf2f(rr[0] >> 16));
+                    v[1] = pack2(bf2f(v[1] & 0xffffu) + bf2f(rr[1] & 0xffffu), bf2f(v[1] >> 16) + bf2f(rr[1] >> 16));
+                }
+                *(u32x2_t*)((bf16_t*)p.y + pix + n) = v;
+            }
     }
 }
 
@@ -476,7 +503,8 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
 // 31-bit buffer offsets.
 bool halo_ok(const vs_conv3d& p) {
     return vs_opt(VS_OPT_VAE_HALO) && !p.up2 && p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.st == 1 &&
-           p.ph == 1 && p.pw == 1 && p.kt <= 3 && p.cout % 96 == 0 && !p.out_f32 && p.cin % 16 == 0 &&
+           p.ph == 1 && p.pw == 1 && p.kt <= 3 && p.cout % 96 == 0 && !p.out_f32 && p.cin % 16 == 0 && p.split == 0 &&
+           !(((uintptr_t)p.y | (uintptr_t)p.res | (uintptr_t)p.bias) & 7) &&
            (long long)p.t_in * p.h_in * p.w_in * p.ldx * 2 < (1LL << 31) && (long long)p.cout * p.ldw * 2 < (1LL << 31);
 }
 
