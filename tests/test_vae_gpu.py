@@ -120,6 +120,26 @@ def test_conv_halo_kernel(cin, cout, kt, t_lo, h, w, opt):
     _close_conv(outs[0], outs[1])
 
 
+def test_conv_halo_long_sequence(opt):
+    """A 121-frame 240 x 416 x 96 slice (2.3 GB: more than 31-bit offsets reach, the C4 tile shape):
+    the halo kernel rebases its input resource per frame; vs the per-tap kernel on the GPU."""
+    vae = _vae()
+    g = torch.Generator(device="cuda").manual_seed(11)
+    T, h, w, c = 121, 240, 416, 96
+    x = torch.randn((1, T, h, w, c), generator=g, device="cuda").to(BF16)
+    wt = (torch.randn((c, c, 3, 3, 3), generator=g, device="cuda") / math.sqrt(27 * c)).to(BF16)
+    cw = vae.ConvW(wt, (0.1 * torch.randn((c,), generator=g, device="cuda")).to(BF16), "cuda")
+    outs = []
+    for halo in (1, 0):
+        opt(vae_halo=halo)
+        outs.append(vae.conv(x, cw, (T, h, w), pad=(2, 1, 1)))
+    del x
+    a, b = outs[0].float(), outs[1].float()
+    scale = b.abs().max().item()
+    assert (a - b).abs().max().item() <= 1.5 * scale * 2.0 ** -8
+    assert (outs[0] == outs[1]).float().mean().item() >= 0.9
+
+
 def test_rgb_input_conv_channel_padding():
     vae = _vae()
     g = torch.Generator().manual_seed(3)

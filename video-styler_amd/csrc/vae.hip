@@ -342,15 +342,13 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
         const unsigned long long a = (unsigned long long)(uintptr_t)base;
         return i32x4h_t{(int)(unsigned)a, (int)((unsigned)(a >> 32) & 0xffffu), (int)bytes, 0x00020000};
     };
-    const long long plane = (long long)p.h_in * p.w_in * p.ldx * 2;      // bytes per input frame
-    i32x4h_t xr = rsrc((const bf16_t*)p.x + z * p.x_zs + nn * p.x_ns, (unsigned)(plane * p.t_in));
+    // the input buffer resource spans ONE frame, rebased per stage (any t_in; offsets < 2^31 per frame)
+    const long long plane = (long long)p.h_in * p.w_in * p.ldx;          // elements per input frame
+    const bf16_t* const xs = (const bf16_t*)p.x + z * p.x_zs + nn * p.x_ns;
     i32x4h_t wr = rsrc((const bf16_t*)p.w + z * p.w_zs + (long long)n0 * p.ldw,
                        (unsigned)((long long)(p.cout - n0) * p.ldw * 2));
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        xr[e] = __builtin_amdgcn_readfirstlane(xr[e]);
-        wr[e] = __builtin_amdgcn_readfirstlane(wr[e]);
-    }
+    for (int e = 0; e < 4; ++e) wr[e] = __builtin_amdgcn_readfirstlane(wr[e]);
     // per-lane DMA source offsets (the uniform frame / chunk / tap-plane part goes in soffset); lane l
     // fills 16-B half (l & 1) of slot 32q + (l >> 1)
     unsigned pvo[PQW], wvo[WQW];
@@ -380,7 +378,10 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
         // (uniform values the compiler may hold in VGPRs: the asm's "s" operands take readfirstlane)
         const int c = s / nkt, kt = kt_lo + s % nkt;
         const unsigned buf = __builtin_amdgcn_readfirstlane(smem_base + (s % HSLOTS) * BUF);
-        const int sx = __builtin_amdgcn_readfirstlane((int)((tb + kt) * plane) + c * 32);
+        i32x4h_t xr = rsrc(xs + (tb + kt) * plane, (unsigned)(plane * 2));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xr[e] = __builtin_amdgcn_readfirstlane(xr[e]);
+        const int sx = __builtin_amdgcn_readfirstlane(c * 32);
         const int sw = __builtin_amdgcn_readfirstlane((kt * 9 * p.cin + c * 16) * 2);
 #pragma unroll
         for (int i = 0; i < PQW; ++i)
@@ -499,13 +500,13 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
 }
 
 // The halo kernel's shapes: 3x3 spatial taps, stride 1, spatial pad 1, kt <= 3 (any time pad), no
-// upsample, whole 96-channel blocks, bf16 output, the frame slice and weight rows addressable with
-// 31-bit buffer offsets.
+// upsample, whole 96-channel blocks, bf16 output, one input frame and the weight rows addressable
+// with 31-bit buffer offsets.
 bool halo_ok(const vs_conv3d& p) {
     return vs_opt(VS_OPT_VAE_HALO) && !p.up2 && p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.st == 1 &&
            p.ph == 1 && p.pw == 1 && p.kt <= 3 && p.cout % 96 == 0 && !p.out_f32 && p.cin % 16 == 0 && p.split == 0 &&
            !(((uintptr_t)p.y | (uintptr_t)p.res | (uintptr_t)p.bias) & 7) &&
-           (long long)p.t_in * p.h_in * p.w_in * p.ldx * 2 < (1LL << 31) && (long long)p.cout * p.ldw * 2 < (1LL << 31);
+           (long long)p.h_in * p.w_in * p.ldx * 2 < (1LL << 31) && (long long)p.cout * p.ldw * 2 < (1LL << 31);
 }
 
 int launch_conv_halo(const vs_conv3d& p, hipStream_t st) {
