@@ -94,28 +94,33 @@ def test_conv_pixel_blocks_bit_identical(cin, cout, up2, opt):
         assert torch.equal(outs[0], o)
 
 
-@pytest.mark.parametrize("cin,cout,kt,t_lo,h,w", [(96, 96, 3, 0, 17, 45), (32, 192, 3, 2, 9, 33),
-                                                  (192, 96, 1, 0, 16, 64), (384, 384, 3, 0, 8, 32)])
-def test_conv_halo_kernel(cin, cout, kt, t_lo, h, w, opt):
+@pytest.mark.parametrize("cin,cout,kt,t_lo,h,w,up2", [(96, 96, 3, 0, 17, 45, False), (32, 192, 3, 2, 9, 33, False),
+                                                      (192, 96, 1, 0, 16, 64, False), (384, 384, 3, 0, 8, 32, False),
+                                                      (384, 192, 1, 0, 7, 19, True), (192, 96, 1, 0, 9, 16, True)])
+def test_conv_halo_kernel(cin, cout, kt, t_lo, h, w, up2, opt):
     """The patch-resident 3x3(x3) kernel (option vae_halo, the default for these shapes) vs a
-    bf16-rounded fp32 torch conv and vs the per-tap gather kernel: ragged 8 x 32 tiles, the causal
-    time pad, frames below t_lo read as zero, a 2-D (kt = 1) conv, two batch slices."""
+    bf16-rounded fp32 torch conv and vs the per-tap gather kernel: ragged 16 x 32 tiles, the causal
+    time pad, frames below t_lo read as zero, a 2-D (kt = 1) conv, the nearest-x2 upsample of the
+    Resample convs (up2), two batch slices."""
     vae = _vae()
-    g = torch.Generator().manual_seed(cin + 3 * cout + kt)
+    g = torch.Generator().manual_seed(cin + 3 * cout + kt + up2)
     T = 5
     x = _rand((2, cin, T, h, w), g)
     wt = _rand((cout, cin, kt, 3, 3), g, 1 / math.sqrt(9 * kt * cin))
     b = _rand((cout,), g, 0.1)
     xz = x.clone()
     xz[:, :, :t_lo] = 0
+    if up2:
+        xz = xz.repeat_interleave(2, dim=3).repeat_interleave(2, dim=4)
     pt = kt - 1
     ref = F.conv3d(F.pad(xz.float(), (1, 1, 1, 1, pt, 0)), wt.float(), b.float()).to(BF16)
     cw = vae.ConvW(wt, b, "cuda")
     xg = _to_nthwc(x)
+    ho, wo = (2 * h, 2 * w) if up2 else (h, w)
     outs = []
     for halo in (1, 0):
         opt(vae_halo=halo)
-        outs.append(_from_nthwc(vae.conv(xg, cw, (T, h, w), pad=(pt, 1, 1), t_lo=t_lo), cout))
+        outs.append(_from_nthwc(vae.conv(xg, cw, (T, ho, wo), pad=(pt, 1, 1), t_lo=t_lo, up2=up2), cout))
     _close_conv(outs[0], ref)
     _close_conv(outs[0], outs[1])
 

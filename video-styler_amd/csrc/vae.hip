@@ -356,10 +356,14 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
     for (int i = 0; i < PQW; ++i) {
         const int P = 32 * (wave + 8 * i) + (lane >> 1);
         const int pr = P / HPITCH, pc = P % HPITCH;
+        // (yi, xi): the conv's input grid -- with up2 the nearest-x2 upsample of the frame, read as
+        // source pixel (yi / 2, xi / 2): the Resample upsample convs gather through it, no copy
         const int yi = y0 - p.ph + pr, xi = x0 - p.pw + pc;
+        const int hv = p.up2 ? 2 * p.h_in : p.h_in, wv = p.up2 ? 2 * p.w_in : p.w_in;
+        const int ys = p.up2 ? yi >> 1 : yi, xs = p.up2 ? xi >> 1 : xi;
         const int lc = (lane & 1) ^ ((pc >> 3) & 1);
-        const bool v = pr < HPROWS && pc < HW + 2 && yi >= 0 && yi < p.h_in && xi >= 0 && xi < p.w_in;
-        pvo[i] = v ? (unsigned)(((long long)yi * p.w_in + xi) * p.ldx * 2 + lc * 16) : 0x80000000u;
+        const bool v = pr < HPROWS && pc < HW + 2 && yi >= 0 && yi < hv && xi >= 0 && xi < wv;
+        pvo[i] = v ? (unsigned)(((long long)ys * p.w_in + xs) * p.ldx * 2 + lc * 16) : 0x80000000u;
     }
 #pragma unroll
     for (int i = 0; i < WQW; ++i) {
@@ -499,11 +503,11 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
     }
 }
 
-// The halo kernel's shapes: 3x3 spatial taps, stride 1, spatial pad 1, kt <= 3 (any time pad), no
-// upsample, whole 96-channel blocks, bf16 output, one input frame and the weight rows addressable
-// with 31-bit buffer offsets.
+// The halo kernel's shapes: 3x3 spatial taps, stride 1, spatial pad 1, kt <= 3 (any time pad), with
+// or without the nearest-x2 upsample, whole 96-channel blocks, bf16 output, one input frame and the
+// weight rows addressable with 31-bit buffer offsets.
 bool halo_ok(const vs_conv3d& p) {
-    return vs_opt(VS_OPT_VAE_HALO) && !p.up2 && p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.st == 1 &&
+    return vs_opt(VS_OPT_VAE_HALO) && p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.st == 1 &&
            p.ph == 1 && p.pw == 1 && p.kt <= 3 && p.cout % 96 == 0 && !p.out_f32 && p.cin % 16 == 0 && p.split == 0 &&
            !(((uintptr_t)p.y | (uintptr_t)p.res | (uintptr_t)p.bias) & 7) &&
            (long long)p.h_in * p.w_in * p.ldx * 2 < (1LL << 31) && (long long)p.cout * p.ldw * 2 < (1LL << 31);
