@@ -451,11 +451,8 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
     // ring of HSLOTS stages, DMA two ahead: before stage s, wait for this wave's stage-s pieces
     // (its stage-(s+1) pieces, issued later, may stay in flight: vmcnt(nq)), then the barrier makes
     // every wave's pieces visible and frees slot (s+2) % 3 (stage s-1's, read by all waves)
-#ifndef VS_HALO_DIAG
-#define VS_HALO_DIAG 0      // diagnostic builds only (wrong results): 1 no DMA, 2 no MFMA
-#endif
-    if (nst > 0 && VS_HALO_DIAG != 1) issue(0);
-    if (nst > 1 && VS_HALO_DIAG != 1) issue(1);
+    if (nst > 0) issue(0);
+    if (nst > 1) issue(1);
     for (int s = 0; s < nst; ++s) {
         if (s + 1 < nst) {
             if (nq == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
@@ -466,8 +463,8 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         asm volatile("s_barrier" ::: "memory");
-        if (s + 2 < nst && VS_HALO_DIAG != 1) issue(s + 2);
-        if (VS_HALO_DIAG != 2) compute(s);
+        if (s + 2 < nst) issue(s + 2);
+        compute(s);
     }
     // epilogue (halo_ok: bf16 output, whole 4-channel groups, no time split, 8-B aligned y / res /
     // bias): per lane and channel group one 8-B bias load, one rounding, one 8-B residual load and
