@@ -466,37 +466,51 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
         if (s + 2 < nst) issue(s + 2);
         compute(s);
     }
-    // epilogue (halo_ok: bf16 output, whole 4-channel groups, no time split, 8-B aligned y / res /
-    // bias): per lane and channel group one 8-B bias load, one rounding, one 8-B residual load and
-    // store -- the generic conv_store's per-element loads and branches were ~1.5 k VALU per wave
+    // epilogue through LDS (halo_ok: bf16 output, no time split, ldy % 8 == 0, 16-B aligned y / res,
+    // 8-B aligned bias): bias + rounding in the accumulator layout (lane = pixel, 4-channel groups),
+    // then the wave's 64 pixels x 96 channels are transposed through LDS (pixel pitch 208 B:
+    // conflict-free 8-B writes) so each global store / residual load instruction moves 64
+    // consecutive 16-B chunks (a pixel's 192 B, then the next pixel's) -- stored straight from the
+    // accumulator layout, every instruction touched 64 lines at 8 B each, and the epilogue cost as
+    // much as 16 % of the kernel (profiles/r5/vae_halo2_compute_diag_s38.log)
+    constexpr int EP = 208;
+    asm volatile("s_barrier" ::: "memory");                    // every wave is done with the ring
     const bf16_t* bias = (const bf16_t*)p.bias;
+    const unsigned eb = smem_base + wave * 64 * EP;
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-        const int yo = y0 + 2 * wave + b, xo = x0 + l32;
-        if (yo >= p.h_out || xo >= p.w_out) continue;
-        const long long pix = z * p.y_zs + nn * p.y_ns +
-                              ((long long)((to * p.t_mul + p.t_add) * p.h_out + yo) * p.w_out + xo) * p.ldy;
+    for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int j = 0; j < NB; ++j)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const int n = n0 + 32 * j + 8 * g + 4 * hi;
+                const int c = 32 * j + 8 * g + 4 * hi;
                 float a[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) a[e] = acc[b][j][4 * g + e];
                 if (bias) {
-                    const u32x2_t bb = *(const u32x2_t*)(bias + n);
+                    const u32x2_t bb = *(const u32x2_t*)(bias + n0 + c);
                     a[0] += bf2f(bb[0] & 0xffffu); a[1] += bf2f(bb[0] >> 16);
                     a[2] += bf2f(bb[1] & 0xffffu); a[3] += bf2f(bb[1] >> 16);
                 }
-                u32x2_t v = {pack2(a[0], a[1]), pack2(a[2], a[3])};
-                if (p.res) {
-                    const u32x2_t rr = *(const u32x2_t*)((const bf16_t*)p.res + pix + n);
-                    v[0] = pack2(bf2f(v[0] & 0xffffu) + bf2f(rr[0] & 0xffffu), bf2f(v[0] >> 16) + bf2f(rr[0] >> 16));
-                    v[1] = pack2(bf2f(v[1] & 0xffffu) + bf2f(rr[1] & 0xffffu), bf2f(v[1] >> 16) + bf2f(rr[1] >> 16));
-                }
-                *(u32x2_t*)((bf16_t*)p.y + pix + n) = v;
+                *reinterpret_cast<LDS_AS u32x2_t*>((LDS_AS char*)(uintptr_t)(eb + (32 * b + l32) * EP + 2 * c)) =
+                    u32x2_t{pack2(a[0], a[1]), pack2(a[2], a[3])};
             }
+    // chunk q = 64 i + lane of the wave's 64 x 12 (pixel, 16-B chunk) pairs
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        const int q = 64 * i + lane, px = q / 12, k = q % 12;
+        const int yo = y0 + 2 * wave + (px >> 5), xo = x0 + (px & 31);
+        u32x4_t v = *reinterpret_cast<const LDS_AS u32x4_t*>((const LDS_AS char*)(uintptr_t)(eb + px * EP + 16 * k));
+        if (yo >= p.h_out || xo >= p.w_out) continue;
+        const long long off = z * p.y_zs + nn * p.y_ns +
+                              ((long long)((to * p.t_mul + p.t_add) * p.h_out + yo) * p.w_out + xo) * p.ldy + n0 + 8 * k;
+        if (p.res) {
+            const u32x4_t rr = *(const u32x4_t*)((const bf16_t*)p.res + off);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                v[e] = pack2(bf2f(v[e] & 0xffffu) + bf2f(rr[e] & 0xffffu), bf2f(v[e] >> 16) + bf2f(rr[e] >> 16));
+        }
+        *(u32x4_t*)((bf16_t*)p.y + off) = v;
     }
 }
 
@@ -506,7 +520,7 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
 bool halo_ok(const vs_conv3d& p) {
     return vs_opt(VS_OPT_VAE_HALO) && p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.st == 1 &&
            p.ph == 1 && p.pw == 1 && p.kt <= 3 && p.cout % 96 == 0 && !p.out_f32 && p.cin % 16 == 0 && p.split == 0 &&
-           !(((uintptr_t)p.y | (uintptr_t)p.res | (uintptr_t)p.bias) & 7) &&
+           p.ldy % 8 == 0 && !(((uintptr_t)p.y | (uintptr_t)p.res) & 15) && !((uintptr_t)p.bias & 7) &&
            (long long)p.h_in * p.w_in * p.ldx * 2 < (1LL << 31) && (long long)p.cout * p.ldw * 2 < (1LL << 31);
 }
 
