@@ -521,6 +521,7 @@ bool halo_ok(const vs_conv3d& p) {
     return vs_opt(VS_OPT_VAE_HALO) && p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.st == 1 &&
            p.ph == 1 && p.pw == 1 && p.kt <= 3 && p.cout % 96 == 0 && !p.out_f32 && p.cin % 16 == 0 && p.split == 0 &&
            p.ldy % 8 == 0 && !(((uintptr_t)p.y | (uintptr_t)p.res) & 15) && !((uintptr_t)p.bias & 7) &&
+           (p.y_zs | p.y_ns | p.x_zs | p.x_ns) % 8 == 0 &&
            (long long)p.h_in * p.w_in * p.ldx * 2 < (1LL << 31) && (long long)p.cout * p.ldw * 2 < (1LL << 31);
 }
 
