@@ -5,8 +5,16 @@
 
 namespace {
 
-constexpr int RT = 256;     // threads per row-kernel block
-constexpr int MAXCH = 3;    // 8-element chunks per thread -> dim <= 6144
+#ifndef VS_RT
+#define VS_RT 128
+#define VS_MAXCH 5
+#endif
+// threads per row-kernel block / 8-element chunks per thread (dim <= RT * MAXCH * 8 = 5120).  r5:
+// 128 threads x 5 chunks instead of 256 x 3 -- LayerNorm+modulate at 59 280 x 5120 309-317 -> 279-289 us
+// (the 256-thread rows split 640 chunks 3 / 2 unevenly); 320 and 640 threads were slower
+// (profiles/r5/rowkernel_threads_ab_s41.log)
+constexpr int RT = VS_RT;
+constexpr int MAXCH = VS_MAXCH;
 
 __device__ __forceinline__ float block_sum(float v, float* red) {
 #pragma unroll
