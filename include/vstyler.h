@@ -328,8 +328,9 @@ typedef struct vs_conv3d {
 int vs_vae_conv(const vs_conv3d* p, void* stream);
 
 /* RMS_norm over channels (F.normalize(x, dim=C) * sqrt(C) * gamma, wan_video_vae.py:55-70) with
- * the bf16 rounding points of the reference, optionally followed by nn.SiLU (:276-278).
- * x, y: npix rows of c channels (row strides ldx, ldy); c % 32 == 0. */
+ * the bf16 rounding points of the reference, optionally followed by nn.SiLU (:276-278); the fp32
+ * division and SiLU are evaluated with a per-row reciprocal and exp2/rcp (within one bf16 ulp).
+ * x, y: npix rows of c channels (row strides ldx, ldy); c % 32 == 0, c <= 384. */
 int vs_vae_rmsnorm(const void* x, long long ldx, void* y, long long ldy, const void* gamma,
                    long long npix, int c, int silu, void* stream);
 
