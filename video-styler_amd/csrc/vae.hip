@@ -578,43 +578,46 @@ __global__ __launch_bounds__(256) void vae_rmsnorm_kernel(const bf16_t* __restri
                                                           bf16_t* __restrict__ y, long long ldy,
                                                           const bf16_t* __restrict__ gamma, long long npix,
                                                           int c, int silu, float scale) {
-    // r5: the pixel's chunks stay in registers between the norm and the write (c <= 384: one read of
-    // x), one correctly rounded division per pixel (1 / ||x||) and a multiply per element instead of
-    // an fp32 division per element, SiLU as v * rcp(1 + exp2(-v log2 e)): 357 -> 311 us at
-    // 2.1 M pixels x 96 (2.25 -> 2.59 TB/s, profiles/r5/vae_rmsnorm_s43.log; the 4-lanes-per-pixel
-    // access -- 64-B pieces at the pixel stride -- and not the VALU is what holds it there).  Agrees
+    // r5: 16 lanes per pixel, lane q owning 16-B chunks q, q + 16, q + 32 (c <= 384), so one load /
+    // store instruction moves 4 whole consecutive pixel rows (768 contiguous B at c = 96) -- with 4
+    // lanes per pixel each instruction took 64-B pieces at the pixel stride and the kernel ran at
+    // 2.2 TB/s (profiles/r5/vae_rmsnorm_s43.log); the row stays in registers between the norm and the
+    // write (one read of x); one correctly rounded division per pixel (1 / ||x||) and a multiply per
+    // element instead of an fp32 division per element; SiLU as v * rcp(1 + exp2(-v log2 e)).  Agrees
     // with the reference's bf16 ops to the test's bar (<= 1 bf16 ulp, > 99.5 % bit-equal: the fp32
     // values differ by a few ulp before the bf16 rounding).
-    constexpr int MAXN = 12;
+    constexpr int MAXN = 3;
     const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
-    const long long pix = gid >> 2;
-    const int q = (int)(gid & 3);
+    const long long pix = gid >> 4;
+    const int q = (int)(gid & 15);
     const bool valid = pix < npix;
-    const int nch = c >> 5;  // chunks per lane
+    const int nck = c >> 3;  // 16-B chunks per pixel
     const bf16_t* xr = x + (valid ? pix : 0) * ldx;
     u32x4_t w[MAXN];
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < MAXN; ++i) {
-        if (i >= nch) break;
-        w[i] = *(const u32x4_t*)(xr + (q + 4 * i) * 8);
+        const int k = q + 16 * i;
+        if (k < nck) {
+            w[i] = *(const u32x4_t*)(xr + k * 8);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float a = bflo(w[i][e]), b = bfhi(w[i][e]);
-            ss += a * a + b * b;
+            for (int e = 0; e < 4; ++e) {
+                const float a = bflo(w[i][e]), b = bfhi(w[i][e]);
+                ss += a * a + b * b;
+            }
         }
     }
-    ss += __shfl_xor(ss, 1);
-    ss += __shfl_xor(ss, 2);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) ss += __shfl_xor(ss, o);
     if (!valid) return;
     const float nrm = fmaxf(rbf(sqrtf(ss)), 1e-12f);  // F.normalize: x / max(||x||, eps), norm in bf16
     const float rn = 1.0f / nrm;
     bf16_t* yr = y + pix * ldy;
 #pragma unroll
     for (int i = 0; i < MAXN; ++i) {
-        if (i >= nch) break;
-        const int c0 = (q + 4 * i) * 8;
-        const u32x4_t gw = *(const u32x4_t*)(gamma + c0);
+        const int k = q + 16 * i;
+        if (k >= nck) continue;
+        const u32x4_t gw = *(const u32x4_t*)(gamma + k * 8);
         u32x4_t o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -626,7 +629,7 @@ __global__ __launch_bounds__(256) void vae_rmsnorm_kernel(const bf16_t* __restri
             }
             o[e] = pack2(v0, v1);
         }
-        *(u32x4_t*)(yr + c0) = o;
+        *(u32x4_t*)(yr + k * 8) = o;
     }
 }
 
@@ -846,7 +849,7 @@ extern "C" int vs_vae_rmsnorm(const void* x, long long ldx, void* y, long long l
                               long long npix, int c, int silu, void* stream) {
     if (!x || !y || !gamma || c <= 0 || c % 32 || c > 384 || ldx % 8 || ldy % 8 || npix < 0) return VS_E_INVALID;
     if (npix == 0) return VS_OK;
-    const long long threads = npix * 4;
+    const long long threads = npix * 16;
     hipLaunchKernelGGL(vae_rmsnorm_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, (const bf16_t*)x, ldx, (bf16_t*)y, ldy, (const bf16_t*)gamma, npix,
                        c, silu, (float)sqrt((double)c));
