@@ -531,12 +531,12 @@ int launch_conv_halo(const vs_conv3d& p, hipStream_t st) {
     const long long nblk = (long long)p.n * p.t_out * tiles_y * tiles_x;
     if (nblk > 0x7ffffff0LL) return VS_E_UNSUPPORTED;
     const int lds = HSLOTS * halo_buf_bytes<NB>();
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)vae_conv_halo_kernel<NB, false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        attr = true;
-    }
+    // (once per process, thread-safe: a function-local static's initialiser)
+    static const bool attr = [lds] {
+        return hipFuncSetAttribute((const void*)vae_conv_halo_kernel<NB, false>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+    }();
+    (void)attr;
     hipLaunchKernelGGL((vae_conv_halo_kernel<NB, false>), dim3((unsigned)((nblk + 7) / 8 * 8), p.cout / (32 * NB), p.nz),
                        dim3(HTHR), lds, st, p, tiles_x, tiles_y);
     VS_CHECK_LAUNCH();
