@@ -96,12 +96,14 @@ def test_conv_pixel_blocks_bit_identical(cin, cout, up2, opt):
 
 @pytest.mark.parametrize("cin,cout,kt,t_lo,h,w,up2", [(96, 96, 3, 0, 17, 45, False), (32, 192, 3, 2, 9, 33, False),
                                                       (192, 96, 1, 0, 16, 64, False), (384, 384, 3, 0, 8, 32, False),
-                                                      (384, 192, 1, 0, 7, 19, True), (192, 96, 1, 0, 9, 16, True)])
+                                                      (384, 192, 1, 0, 7, 19, True), (192, 96, 1, 0, 9, 16, True),
+                                                      (96, 32, 3, 0, 17, 45, False), (192, 16, 3, 1, 9, 33, False),
+                                                      (64, 32, 1, 0, 7, 19, True)])
 def test_conv_halo_kernel(cin, cout, kt, t_lo, h, w, up2, opt):
     """The patch-resident 3x3(x3) kernel (option vae_halo, the default for these shapes) vs a
     bf16-rounded fp32 torch conv and vs the per-tap gather kernel: ragged 16 x 32 tiles, the causal
     time pad, frames below t_lo read as zero, a 2-D (kt = 1) conv, the nearest-x2 upsample of the
-    Resample convs (up2), two batch slices."""
+    Resample convs (up2), 96-channel blocks and the <= 32-channel heads (NB = 1), two batch slices."""
     vae = _vae()
     g = torch.Generator().manual_seed(cin + 3 * cout + kt + up2)
     T = 5

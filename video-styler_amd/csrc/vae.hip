@@ -455,10 +455,14 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
     if (nst > 1) issue(1);
     for (int s = 0; s < nst; ++s) {
         if (s + 1 < nst) {
-            if (nq == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-            else if (nq == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-            else if (nq == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            switch (nq) {          // (an immediate operand: one wait per possible count)
+                case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+                case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+                case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+                case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+                case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+                default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+            }
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -473,6 +477,16 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
     // consecutive 16-B chunks (a pixel's 192 B, then the next pixel's) -- stored straight from the
     // accumulator layout, every instruction touched 64 lines at 8 B each, and the epilogue cost as
     // much as 16 % of the kernel (profiles/r5/vae_halo2_compute_diag_s38.log)
+    if constexpr (NB != 3) {
+        // (NB = 1: the conv_out / head convs with at most 32 output channels -- few bytes out, the
+        // generic store with its channel and stride predicates)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int yo = y0 + 2 * wave + b, xo = x0 + l32;
+            if (yo < p.h_out && xo < p.w_out) conv_store<NB, F32>(p, acc[b], z, nn, to, yo, xo, n0, lane);
+        }
+        return;
+    }
     constexpr int EP = 208;
     asm volatile("s_barrier" ::: "memory");                    // every wave is done with the ring
     const bf16_t* bias = (const bf16_t*)p.bias;
@@ -515,30 +529,37 @@ __global__ __launch_bounds__(HTHR, 1) void vae_conv_halo_kernel(vs_conv3d p, int
 }
 
 // The halo kernel's shapes: 3x3 spatial taps, stride 1, spatial pad 1, kt <= 3 (any time pad), with
-// or without the nearest-x2 upsample, whole 96-channel blocks, bf16 output, one input frame and the
-// weight rows addressable with 31-bit buffer offsets.
-bool halo_ok(const vs_conv3d& p) {
-    return vs_opt(VS_OPT_VAE_HALO) && p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.st == 1 &&
-           p.ph == 1 && p.pw == 1 && p.kt <= 3 && p.cout % 96 == 0 && !p.out_f32 && p.cin % 16 == 0 && p.split == 0 &&
-           p.ldy % 8 == 0 && !(((uintptr_t)p.y | (uintptr_t)p.res) & 15) && !((uintptr_t)p.bias & 7) &&
-           (p.y_zs | p.y_ns | p.x_zs | p.x_ns) % 8 == 0 &&
-           (long long)p.h_in * p.w_in * p.ldx * 2 < (1LL << 31) && (long long)p.cout * p.ldw * 2 < (1LL << 31);
+// or without the nearest-x2 upsample, bf16 output, one input frame and the weight rows addressable
+// with 31-bit buffer offsets; then either whole 96-channel blocks (NB = 3, the LDS-transposed
+// epilogue: ldy % 8, 16-B aligned y / res) or at most 32 output channels (NB = 1: the decoder's
+// 96 -> 3 conv_out and the encoder's 32-channel head, the generic epilogue).  0: not eligible.
+int halo_nb(const vs_conv3d& p) {
+    const bool base = vs_opt(VS_OPT_VAE_HALO) && p.kh == 3 && p.kw == 3 && p.sh == 1 && p.sw == 1 && p.st == 1 &&
+                      p.ph == 1 && p.pw == 1 && p.kt <= 3 && !p.out_f32 && p.cin % 16 == 0 && p.split == 0 &&
+                      (p.x_zs | p.x_ns) % 8 == 0 && (long long)p.h_in * p.w_in * p.ldx * 2 < (1LL << 31) &&
+                      (long long)p.cout * p.ldw * 2 < (1LL << 31);
+    if (!base) return 0;
+    if (p.cout % 96 == 0 && p.ldy % 8 == 0 && !(((uintptr_t)p.y | (uintptr_t)p.res) & 15) &&
+        !((uintptr_t)p.bias & 7) && (p.y_zs | p.y_ns) % 8 == 0)
+        return 3;
+    return p.cout <= 32 ? 1 : 0;
 }
 
+template <int NB>
 int launch_conv_halo(const vs_conv3d& p, hipStream_t st) {
-    constexpr int NB = 3;
     const int tiles_x = (p.w_out + HW - 1) / HW, tiles_y = (p.h_out + HT - 1) / HT;
     const long long nblk = (long long)p.n * p.t_out * tiles_y * tiles_x;
     if (nblk > 0x7ffffff0LL) return VS_E_UNSUPPORTED;
     const int lds = HSLOTS * halo_buf_bytes<NB>();
-    // (once per process, thread-safe: a function-local static's initialiser)
+    // (once per process and instance, thread-safe: a function-local static's initialiser)
     static const bool attr = [lds] {
         return hipFuncSetAttribute((const void*)vae_conv_halo_kernel<NB, false>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
     }();
     (void)attr;
-    hipLaunchKernelGGL((vae_conv_halo_kernel<NB, false>), dim3((unsigned)((nblk + 7) / 8 * 8), p.cout / (32 * NB), p.nz),
-                       dim3(HTHR), lds, st, p, tiles_x, tiles_y);
+    hipLaunchKernelGGL((vae_conv_halo_kernel<NB, false>),
+                       dim3((unsigned)((nblk + 7) / 8 * 8), (p.cout + 32 * NB - 1) / (32 * NB), p.nz), dim3(HTHR), lds,
+                       st, p, tiles_x, tiles_y);
     VS_CHECK_LAUNCH();
     return VS_OK;
 }
@@ -837,7 +858,11 @@ extern "C" int vs_vae_conv(const vs_conv3d* pp, void* stream) {
     if (p.t_out == 0) return VS_OK;
     const long long M = (long long)p.n * p.t_out * p.h_out * p.w_out;
     hipStream_t st = (hipStream_t)stream;
-    if (halo_ok(p)) return launch_conv_halo(p, st);
+    switch (halo_nb(p)) {
+        case 3: return launch_conv_halo<3>(p, st);
+        case 1: return launch_conv_halo<1>(p, st);
+        default: break;
+    }
     if (p.cout <= 32) return launch_conv<1>(p, M, st);
     if (p.cout <= 64) return launch_conv<2>(p, M, st);
     if (p.cout <= 96) return launch_conv<3>(p, M, st);
