@@ -5,8 +5,14 @@ One step = the reference's CFG denoising step (wan_video_new.py:518-542): DiT(40
 and the Euler update.  Synthetic data: random-init weights (N(0,0.02), seed 5), seeded latents /
 contexts / VACE context of the real shapes (no checkpoints or datasets are reachable offline).
 
-  python bench.py [--gpus N --steps K --warmup W]        (N>1: torchrun over RCCL, Ulysses SP over all
-                                                         N ranks; VSTYLER_CFG_PARALLEL=1 selects CFG parallel)
+  python bench.py [--gpus N --steps K --warmup W]
+
+N > 1: one process per GPU, Ulysses SP over all N ranks over RCCL (VSTYLER_CFG_PARALLEL=1 selects CFG
+parallelism).  Under torchrun (WORLD_SIZE set) WORLD_SIZE must equal N; without a launcher this
+process spawns the N ranks itself (launch_ranks: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR
+127.0.0.1 / MASTER_PORT per child, rank 0 prints the line, exit code = the worst child's) and refuses
+when fewer than N GPUs are visible.  The line carries `rccl_world` and every rank's device and
+ms/step; `n_gpus` is the process group's size.
 
 Prints one JSON line with `roofline` (self-attention kernel, HIP-event timed inside the timed
 region) and, on rank 0 at N=1, `cpu_baseline` (the CPU oracle on a bounded token sample).
@@ -174,6 +180,38 @@ def e2e_components(dev, frames, height, width, step_s, steps=50):
                     "tiled decode + uint8; random-init weights, synthetic frames"}
 
 
+def e2e_measured(dev, dit, vace, ctx, frames, height, width, t5_s=None, steps=50):
+    """One real WanVideoPipeline.__call__ (wan_video_new.py:416-560, as inference/infer_ditto.py:20-59
+    calls it), timed from the call to the uint8 frames on the device: the VACE unit (2 tiled VAE
+    encodes of a synthetic 832x480x73 control video + mask latents), the noise on the CPU generator,
+    `steps` CFG-5 Euler steps (step 0 eager, hipGraph capture, replays), the tiled decode and the uint8
+    conversion -- host glue included.  Prompt embeddings are passed (no tokenizer files offline); the
+    two UMT5-XXL encodes are the separately timed `t5_s`.  Random-init weights."""
+    from vstyler.pipeline import WanVideoPipeline
+    from vstyler.vae import WanVideoVAE
+    pipe = WanVideoPipeline(device=dev)
+    pipe.dit, pipe.vace = dit, vace
+    pipe.vae = WanVideoVAE(device=dev).init_random_(6)
+    g = torch.Generator(device=dev).manual_seed(3)
+    video = torch.randint(0, 256, (frames, height, width, 3), generator=g, device=dev, dtype=torch.uint8)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = pipe(prompt_emb=ctx[0:1], negative_prompt_emb=ctx[1:2], vace_video=video, seed=0, height=height,
+               width=width, num_frames=frames, num_inference_steps=steps, cfg_scale=5.0, output_type="u8")
+    torch.cuda.synchronize()
+    sec = time.perf_counter() - t0
+    shape = list(out.shape)
+    del pipe, out, video
+    torch.cuda.empty_cache()
+    res = {"measured_call_s": round(sec, 2), "measured_output": shape, "measured_steps": steps,
+           "measured_note": "one WanVideoPipeline.__call__(prompt_emb=, negative_prompt_emb=, vace_video=<73 "
+                            "frames u8>, num_inference_steps=50, cfg_scale=5, output_type='u8'): VACE encodes "
+                            "+ 50 steps + decode + uint8, host glue included"}
+    if t5_s is not None:
+        res["sec_per_video_measured"] = round(sec + t5_s, 2)
+    return res
+
+
 def _parallelism(sp, world):
     """'single', 'sp<N>' (Ulysses over N ranks) or 'cfg2' / 'cfg2_sp<u>' (CFG parallelism: one CFG
     sample per half of the ranks, Ulysses over the u ranks of a half)."""
@@ -183,6 +221,77 @@ def _parallelism(sp, world):
     if isinstance(sp, CfgParallel):
         return "cfg2" if sp.ulysses is None else f"cfg2_sp{sp.ulysses.world_size}"
     return f"sp{world}"
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_gpus():
+    """GPUs this process could bind, without initialising HIP (torch.cuda.device_count() does not
+    create a context on this image; the launcher must never touch the GPU before its children)."""
+    return torch.cuda.device_count()
+
+
+def rank_env(base, rank, world, port):
+    """The environment rank `rank` of `world` gets: torchrun's variables, one GPU per rank
+    (LOCAL_RANK == RANK on one node), rendezvous on 127.0.0.1."""
+    env = dict(base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    return env
+
+
+def launch_ranks(n, argv, script=None, gpus=None, env=None, timeout=None):
+    """`bench.py --gpus N` without an external launcher: N fresh child processes of `script` (this
+    file), one per GPU, each with rank_env; the parent never touches the GPU (the reference's USP is
+    one process per GPU, examples/wanvideo/README.md:220, wan_video_new.py:313-338).  Rank 0 prints
+    the JSON line; the return value is 0 or the exit code of the first child to fail (every child
+    still running then is terminated).  Fails fast (rc 2, no child started) when fewer than N GPUs are
+    visible."""
+    import subprocess
+    gpus = visible_gpus() if gpus is None else gpus
+    if gpus < n:
+        print(f"[bench] --gpus {n} needs {n} visible GPUs, this node has {gpus}: refusing to time "
+              f"fewer GPUs than asked", file=sys.stderr, flush=True)
+        return 2
+    script = script or os.path.abspath(__file__)
+    port = _free_port()
+    base = dict(os.environ if env is None else env)
+    procs = [subprocess.Popen([sys.executable, script] + list(argv), env=rank_env(base, r, n, port))
+             for r in range(n)]
+    rcs = [None] * n
+    first_bad = None
+    t0 = time.time()
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+                if rcs[r] not in (None, 0) and first_bad is None:
+                    first_bad = rcs[r]
+        late = timeout is not None and time.time() - t0 > timeout
+        if first_bad is not None or late:
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    p.terminate()
+            for r, p in enumerate(procs):
+                try:
+                    rcs[r] = p.wait(30) if rcs[r] is None else rcs[r]
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    rcs[r] = p.wait()
+            if first_bad is None:
+                print(f"[bench] ranks still running after {timeout} s: terminated", file=sys.stderr, flush=True)
+                return 124
+            break
+        time.sleep(0.2)
+    # the first child to fail is the cause (the ranks terminated after it report SIGTERM)
+    return first_bad if first_bad is not None else 0
 
 
 def main():
@@ -199,19 +308,30 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of hipGraph replay")
     ap.add_argument("--progress", action="store_true", help="sync + stderr line after every timed step")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end sec/video components")
+    ap.add_argument("--no-e2e-call", action="store_true",
+                    help="skip the measured 50-step WanVideoPipeline.__call__ (keep the composed e2e breakdown)")
     ap.add_argument("--config", default="bf16", choices=("bf16", "fp8"),
                     help="bf16: BASELINE config (50-step Euler, CFG 5); fp8: config 5 (fp8 block linears, "
                          "UniPC, CFG 1.2, shift 2, SLG block 2, VACE strength 0.975)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no external launcher: this process only spawns the ranks (it never touches the GPU)
+        rc = launch_ranks(args.gpus, sys.argv[1:])
+        sys.exit(rc if rc >= 0 else 128 - rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and the flag disagree",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
     if world > 1:
         import torch.distributed as dist
         from vstyler.usp import init_distributed, get_default_group
         local = init_distributed()
         dev = torch.device(f"cuda:{local}")
         sp = get_default_group()
+        world = dist.get_world_size()
     else:
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
@@ -316,10 +436,18 @@ def main():
     TIMER.enabled = False
     attn_ms, attn_n = TIMER.mean_ms("self_attn")
     attn_tf = TIMER.tflops("self_attn")       # summed launch FLOPs / summed launch time
+    ranks_info = None
     if world > 1:
-        tt = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = tt.item()
+        # every rank's own ms/step and device, so the record shows RCCL formed `world` ranks on
+        # `world` distinct GPUs; the step time is the slowest rank's
+        props = torch.cuda.get_device_properties(dev)
+        mine = torch.tensor([elapsed, float(dev.index), float(getattr(props, "pci_bus_id", -1)),
+                             float(getattr(props, "pci_device_id", -1))], dtype=torch.float64, device=dev)
+        every = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        ranks_info = [{"rank": r, "device": int(e[1]), "pci_bus": int(e[2]), "pci_device": int(e[3]),
+                       "ms_per_step": round(1000 * float(e[0]) / args.steps, 2)} for r, e in enumerate(every)]
+        elapsed = max(float(e[0]) for e in every)
 
     default_shape = (args.model, args.width, args.height, args.frames) == ("14B", 832, 480, 73)
     ms_per_step = 1000 * elapsed / args.steps
@@ -348,6 +476,8 @@ def main():
                    "step_exec": "hipGraph replay" if use_graph else "eager launches",
                    "sampler": ("UniPC bh2 order 2, cfg 1.2, shift 2.0, SLG block 2 @ 0.2-0.7, VACE 0.975"
                                if args.config == "fp8" else "flow-match Euler, cfg 5.0, shift 5.0")},
+        "rccl_world": dist.get_world_size() if world > 1 else 1,
+        "ranks": ranks_info,
         "model_tflops_per_step": round(fl_step / 1e12, 1),
         "mfu_bf16": round(fl_step * value / world / 1e12 / PEAK_BF16_TFLOPS, 4),
         "roofline": {"kernel": "attn_fwd_w4 (self-attention)", "bound": "mfma",
@@ -364,6 +494,10 @@ def main():
     }
     if world == 1 and not args.no_e2e and args.config == "bf16":
         out["e2e"] = e2e_components(dev, args.frames, args.height, args.width, elapsed / args.steps)
+        if not args.no_e2e_call:
+            del stepper
+            out["e2e"].update(e2e_measured(dev, dit, vace, ctx, args.frames, args.height, args.width,
+                                           t5_s=out["e2e"]["t5_2_prompts_s"]))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(m, S, rows=args.cpu_rows)
     if rank == 0:

@@ -39,6 +39,10 @@ WAN_CONFIGS = {
     # scaled-down shape used by fast tests (head_dim stays 128 like every Wan model)
     "tiny": dict(dim=256, ffn_dim=512, num_heads=2, num_layers=4, in_dim=16, out_dim=16,
                  text_dim=4096, freq_dim=256, eps=1e-6, vace_layers=(0, 2), vace_in_dim=96),
+    # eight heads, so Ulysses runs at world 2 / 4 / 8 with heads % world == 0 (the 14B model's 40 heads
+    # give 5 per rank at SP = 8; tests/test_sp.py)
+    "sp8": dict(dim=1024, ffn_dim=2048, num_heads=8, num_layers=3, in_dim=16, out_dim=16,
+                text_dim=4096, freq_dim=256, eps=1e-6, vace_layers=(0, 2), vace_in_dim=96),
 }
 
 

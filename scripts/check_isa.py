@@ -9,7 +9,9 @@ instantiation that reads through acc_rd (every one but the fp8 8-B fallback, whi
   * exactly 512 v_accvgpr_read (256 in the tile epilogue, 256 in the split-piece path),
   * no scratch (a spilled accumulator or fragment would be a scratch round trip in the K loop).
 And the tile-queue atomic (W4Grab::issue) must be a single returning global atomic add per kernel
-(the compiler's atomic optimizer off for gemm.o: Makefile).
+(the compiler's atomic optimizer off for gemm.o: Makefile), whose destination VGPR nothing touches
+between the atomic and the `s_waitcnt vmcnt` + `v_readfirstlane` that consume it (queue_value_hazards;
+also checked in the attention kernels, which take their items from the same kind of queue).
 
 usage: check_isa.py <gemm.o | libvstyler.so>   (exit 1 with the offending kernels listed)"""
 import os
@@ -67,6 +69,93 @@ def kernels(co):
     return out, scratch
 
 
+def _vregs(operands):
+    """VGPR numbers named in an operand string (v7, v[4:7])."""
+    out = set()
+    for a, b in re.findall(r"\bv\[(\d+):(\d+)\]", operands):
+        out.update(range(int(a), int(b) + 1))
+    out.update(int(r) for r in re.findall(r"\bv(\d+)\b", operands))
+    return out
+
+
+def _instructions(body):
+    """(address, opcode, operands, branch target address or None) of a kernel's disassembly."""
+    m = re.match(r"([0-9a-f]+) <", body)
+    base = int(m.group(1), 16) if m else 0
+    out = []
+    for ln in body.splitlines():
+        m = re.match(r"\s*([a-z_0-9]+)\s*(.*?)\s*//\s*([0-9A-Fa-f]+):", ln)
+        if not m:
+            continue
+        op, args, addr = m.group(1), m.group(2), int(m.group(3), 16)
+        t = re.search(r"<_Z[^>+]*\+0x([0-9a-f]+)>", ln)
+        out.append((addr, op, args, base + int(t.group(1), 16) if t and op.startswith(("s_branch", "s_cbranch"))
+                    else None))
+    return out
+
+
+def queue_value_hazards(body):
+    """The tile-queue atomic (vs_queue_issue, csrc/common.h) returns its value in a VGPR the compiler
+    believes ready when the asm ends; only vs_queue_value's `s_waitcnt vmcnt(W)` + `v_readfirstlane`
+    wait for it.  A copy (or any other read, or a reuse) of that VGPR placed between the two by the
+    register allocator would read a stale tile id.  For every such atomic (returning, EXEC set to
+    lane 0 just before it), follow every control-flow path from it (branches taken and not taken) to
+    the first v_readfirstlane of its destination VGPR, and report any instruction on the way that
+    READS that VGPR, or a readfirstlane reached without a vmcnt wait after the atomic.
+    A path that overwrites the VGPR or ends the program is one on which the allocator holds the value
+    dead (paths correlated with the kernel's own `wave == 0` branches that it never takes); at least
+    one path must consume it."""
+    insts = _instructions(body)
+    at = {addr: i for i, (addr, _, _, _) in enumerate(insts)}
+    issues, n_atomics = [], 0
+    stores = ("global_store", "buffer_store", "ds_write", "ds_store", "flat_store", "scratch_store")
+    for i, (_, op, args, _) in enumerate(insts):
+        # vs_queue_issue's atomic: returning (sc0), issued with EXEC = lane 0 by the asm itself
+        if op != "global_atomic_add" or not re.search(r"\bsc0\b", args) or \
+                not any(o == "s_mov_b64" and a.startswith("exec, 1") for _, o, a, _ in insts[max(0, i - 2):i]):
+            continue
+        n_atomics += 1
+        dst = int(re.match(r"v(\d+)", args).group(1))
+        consumed = False
+        todo, seen = [(i + 1, False)], set()
+        while todo:
+            j, waited = todo.pop()
+            while j < len(insts) and (j, waited) not in seen:
+                seen.add((j, waited))
+                _, op2, args2, tgt = insts[j]
+                if op2 == "s_waitcnt" and "vmcnt" in args2:
+                    waited = True
+                if op2 == "v_readfirstlane_b32" and dst in _vregs(args2.split(",", 1)[1]):
+                    consumed = True
+                    if not waited:
+                        issues.append(f"v{dst}: v_readfirstlane at {insts[j][0]:#x} with no vmcnt wait after the atomic")
+                    break
+                ops = args2.split(",", 1)
+                read = _vregs(args2) if op2.startswith(stores) or (op2.startswith("global_atomic")
+                                                                   and "sc0" not in args2) else \
+                    (_vregs(ops[1]) if len(ops) > 1 else set())
+                if dst in read:          # a copy / use of the value before it has landed
+                    issues.append(f"v{dst}: '{op2} {args2}' at {insts[j][0]:#x} reads it between the atomic "
+                                  f"and its vmcnt + readfirstlane")
+                    break
+                if dst in _vregs(ops[0]):    # overwritten: the value is dead on this path (the
+                    break                    # allocator's view of a path the kernel never takes)
+                if op2 == "s_endpgm":
+                    break
+                if tgt is not None:
+                    if tgt not in at:
+                        issues.append(f"v{dst}: branch to unknown address {tgt:#x}")
+                        break
+                    if op2 == "s_branch":
+                        j = at[tgt]
+                        continue
+                    todo.append((at[tgt], waited))
+                j += 1
+        if not consumed:
+            issues.append(f"v{dst}: never consumed by a v_readfirstlane on any path")
+    return n_atomics, issues
+
+
 def main():
     obj = sys.argv[1]
     bad = []
@@ -91,13 +180,21 @@ def main():
             bad.append(f"{name}: {scratch[name]} B of scratch")
         if na < 1:
             bad.append(f"{name}: no returning tile-queue atomic")
+        bad += [f"{name}: {msg}" for msg in queue_value_hazards(body)[1]]
         checked += 1
     if checked < 13:
         bad.append(f"only {checked} gemm_*_4w kernels found (expected 13)")
+    nq = 0
+    for name, body in ks.items():            # the attention kernels take items from the same queues
+        if "attn_fwd_w4" in name:
+            n, issues = queue_value_hazards(body)
+            nq += n
+            bad += [f"{name}: {msg}" for msg in issues]
     if bad:
         print("check_isa: FAILED\n  " + "\n  ".join(bad))
         sys.exit(1)
-    print(f"check_isa: {checked} gemm_*_4w kernels OK (no accumulator AGPR copies, 512 acc_rd reads, no scratch)")
+    print(f"check_isa: {checked} gemm_*_4w kernels OK (no accumulator AGPR copies, 512 acc_rd reads, no scratch, "
+          f"queue atomics consumed only behind their vmcnt wait; {nq} in the attention kernels)")
 
 
 if __name__ == "__main__":

@@ -43,6 +43,7 @@ class CpuUlysses(UlyssesGroup):
         o.copy_(self.attn_fn(q, k, v, heads, batch))
 
     def _all_gather(self, recv, send):
+        self.collective_calls += 1
         parts = list(recv.chunk(self.world_size))
         dist.all_gather(parts, send.contiguous(), group=self.group)
 
@@ -54,6 +55,7 @@ class HostStagedUlysses(UlyssesGroup):
     capturable = False
 
     def _all_to_all(self, recv, send):
+        self.collective_calls += 1
         torch.cuda.synchronize()
         r = torch.empty(recv.shape, dtype=recv.dtype)
         dist.all_to_all_single(r, send.cpu(), group=self.group)
@@ -61,6 +63,7 @@ class HostStagedUlysses(UlyssesGroup):
         return _Done()
 
     def _all_gather(self, recv, send):
+        self.collective_calls += 1
         torch.cuda.synchronize()
         parts = [torch.empty(send.shape, dtype=send.dtype) for _ in range(self.world_size)]
         dist.all_gather(parts, send.cpu().contiguous(), group=self.group)

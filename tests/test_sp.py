@@ -1,10 +1,15 @@
-"""Ulysses sequence parallelism (vstyler/usp.py) at world size 2.
+"""Ulysses sequence parallelism (vstyler/usp.py) at world sizes 2, 4 and 8.
 
 * CPU (gloo): the product's shard / all-to-all / gather orchestration, with the permute kernel
-  re-stated in torch (tests/sp_util.py) and the oracle attention: SP output == full attention.
-* GPU: two processes share cuda:0, the product model runs its HIP kernels under SP=2 with
-  host-staged gloo collectives; the result must be bit-identical to the SP=1 forward (every
-  kernel is row/head-local with a fixed reduction order, so sharding changes no rounding).
+  re-stated in torch (tests/sp_util.py) and the oracle attention: SP output == full attention, at
+  world 2 / 4 / 8 with 8 heads (1 head per rank at SP = 8), batch 2 (re-laid-out exchange) and
+  batch 1 (q|k|v rows delivered in token order, the `e.rows` path).
+* GPU: `world` processes share cuda:0, the product model runs its HIP kernels under Ulysses SP =
+  world with host-staged gloo collectives.  The result must be bit-identical to the SP=1 forward
+  (every kernel is row/head-local with a fixed reduction order, so sharding changes no rounding)
+  AND within NOISE_X (2) times the fp32/fp64 noise floor of the oracle (`O.model_fn`, per CFG
+  sample).
+  World 4 / 8 run the 8-head "sp8" model (the tiny model has 2 heads).
 """
 import os
 import sys
@@ -15,6 +20,12 @@ import torch
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# The oracle's fp32-vs-fp64 accumulation floor does not model the attention kernel's own bf16
+# roundings (the pre-scaled Q, the bf16 P of the PV product), which at these few-block, 128-token
+# models are a visible share of the error: the SP=1 product forward of the tiny model sits at 1.58x
+# that floor in rel-L2 (profiles/r6/pytest_sp_oracle_s1.log), so the SP outputs -- bit-identical
+# to SP=1 -- are held to 2x.  The production-shape tests (C2/C3/C4) keep 1.5x.
+NOISE_X = 2.0
 
 
 def _port():
@@ -34,6 +45,19 @@ def _init(rank, world, port):
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
 
 
+def _spawn(target, world, *args, timeout=300):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=timeout) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+    return res
+
+
 def _cpu_worker(rank, world, port, q, B=2):
     try:
         _init(rank, world, port)
@@ -41,7 +65,7 @@ def _cpu_worker(rank, world, port, q, B=2):
         from sp_util import CpuUlysses
         from vstyler.models import RunCtx, Workspace
         torch.manual_seed(0)
-        S, H = 48, 4
+        S, H = 48, 8
         D = H * 128
         qf, kf, vf = (torch.randn(B, S, D).to(torch.bfloat16) for _ in range(3))
         ref = O.attention(qf, kf, vf, H)
@@ -58,76 +82,107 @@ def _cpu_worker(rank, world, port, q, B=2):
         kl = sp.shard_tokens(kf.view(B * S, D), None, rc)[0].clone()
         vl = sp.shard_tokens(vf.view(B * S, D), None, rc)[0].clone()
         o = torch.empty_like(ql)
-        sp.attention(ql, kl, vl, o, H, B)
+        e = sp.exchange_start(ql, kl, vl, H, B)
+        rows_path = e.rows
+        sp.finish(sp.attend(e), o)
         Sl = S // world
         want = ref[:, rank * Sl:(rank + 1) * Sl].reshape(B * Sl, D)
         ok_attn = torch.equal(o, want)
         full = sp.gather_tokens(o[:, :64].contiguous(), rc2)
         ok_gather = torch.equal(full.view(B, S, 64), ref[..., :64])
-        q.put((rank, ok_attn, ok_gather, rc2.token_offset))
+        q.put((rank, ok_attn, ok_gather, rc2.token_offset, rows_path, sp.collective_calls))
     except Exception as e:  # pragma: no cover
-        q.put((rank, repr(e), None, None))
+        import traceback
+        q.put((rank, traceback.format_exc(), None, None, None, None))
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("B", [2, 1])     # B=1: q|k|v rows delivered in token order, no re-layout
-def test_ulysses_exchange_cpu_gloo_world2(B):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _port()
-    procs = [ctx.Process(target=_cpu_worker, args=(r, 2, port, q, B)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=300) for _ in procs)
-    for p in procs:
-        p.join(60)
-    for rank, ok_attn, ok_gather, off in res:
+def test_ulysses_exchange_cpu_gloo(world, B):
+    res = _spawn(_cpu_worker, world, B)
+    assert len(res) == world
+    for rank, ok_attn, ok_gather, off, rows_path, calls in res:
         assert ok_attn is True, res
         assert ok_gather is True, res
-        assert off == rank * 24
+        assert off == rank * (48 // world)
+        assert rows_path is (B == 1), res
+        assert calls == 3, res                # q|k|v out, o back, the token gather
 
 
-def _gpu_worker(rank, world, port, q):
+def _oracle_check(out, cfg, W, lat, t, contexts, vc, tag):
+    """out [B, 16, T, H, W] (one row per context) vs O.model_fn per context within NOISE_X times
+    the fp32 / fp64 accumulation floor of the oracle."""
+    from oracle import wan_oracle as O
+    from gpu_util import err
+
+    def run():
+        return torch.cat([O.model_fn(W, cfg, lat, t.cpu(), c, vc) for c in contexts])
+    ref32 = run()
+    O.ACC_DTYPE = torch.float64
+    try:
+        ref64 = run()
+    finally:
+        O.ACC_DTYPE = torch.float32
+    mx, rl = err(out, ref32)
+    fmx, frl = err(ref32, ref64)
+    ok = mx <= NOISE_X * fmx + 1e-3 and rl <= NOISE_X * frl + 1e-4
+    return ok, (f"{tag}: max-abs {mx:.4g} rel-L2 {rl:.4g} (floor {fmx:.4g} / {frl:.4g}; "
+                f"{mx / max(fmx, 1e-30):.2f}x / {rl / max(frl, 1e-30):.2f}x)")
+
+
+def _gpu_worker(rank, world, port, q, cfg_name="tiny"):
     try:
         _init(rank, world, port)
         from oracle import wan_oracle as O
         from sp_util import HostStagedUlysses
         from vstyler import model_fn_wan_video
         from test_model_gpu import build
-        cfg = O.WAN_CONFIGS["tiny"]
+        cfg = O.WAN_CONFIGS[cfg_name]
         W = O.random_weights(cfg, seed=5)
         dit, vace = build(cfg, W, "cuda:0")
         lat, cp, cn, vc = O.synthetic_inputs(cfg, 5, 128, 128)
         t = torch.tensor([833.3333]).to(torch.bfloat16).cuda()
         ctx = torch.cat([cp, cn]).cuda()
+        res = {}
         single = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx, vace_context=vc.cuda())
-        same, mx = True, 0.0
-        for overlap in (True, False):   # per-sample micro-batch overlap schedule, then sequential
+        par = None
+        for overlap in (True, False):   # per-sample micro-batch overlap schedule (B=1 rows path), then B=2
             sp = HostStagedUlysses()
             sp.overlap = overlap
             par = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx,
                                      vace_context=vc.cuda(), use_unified_sequence_parallel=True, sp_group=sp)
             torch.cuda.synchronize()
-            same = same and torch.equal(single.cpu(), par.cpu())
-            mx = max(mx, (single.float() - par.float()).abs().max().item())
-        q.put((rank, same, mx))
-    except Exception as e:  # pragma: no cover
+            res[f"overlap{int(overlap)}"] = torch.equal(single.cpu(), par.cpu())
+        # a batch-1 forward (cfg_scale 1): one sample through the rows path without the overlap split
+        single1 = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx[0:1],
+                                     vace_context=vc.cuda())
+        par1 = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx[0:1],
+                                  vace_context=vc.cuda(), use_unified_sequence_parallel=True,
+                                  sp_group=HostStagedUlysses())
+        torch.cuda.synchronize()
+        res["nocfg"] = torch.equal(single1.cpu(), par1.cpu())
+        if rank == 0:           # the SP output against the oracle itself, not only against SP = 1
+            res["oracle"], res["oracle_msg"] = _oracle_check(par.cpu(), cfg, W, lat, t, (cp, cn), vc,
+                                                             f"Ulysses SP={world} {cfg_name}")
+        q.put((rank, res))
+    except Exception:  # pragma: no cover
         import traceback
-        q.put((rank, traceback.format_exc(), None))
+        q.put((rank, traceback.format_exc()))
 
 
 @pytest.mark.gpu
-def test_ulysses_sp2_model_bit_identical_on_one_gpu():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _port()
-    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=600) for _ in procs)
-    for p in procs:
-        p.join(60)
-    for rank, same, mx in res:
-        assert same is True, res
+@pytest.mark.parametrize("world,cfg_name", [(2, "tiny"), (4, "sp8"), (8, "sp8")])
+def test_ulysses_model_on_one_gpu_vs_sp1_and_oracle(world, cfg_name):
+    """Ulysses at SP = 2 / 4 / 8 through the product orchestration (UlyssesGroup with the HIP permute
+    and attention kernels; collectives host-staged so the ranks can share one GPU): bit-identical to
+    the SP=1 forward under both schedules and for a batch-1 forward, and within the oracle's floor."""
+    res = _spawn(_gpu_worker, world, cfg_name, timeout=600)
+    assert len(res) == world
+    for rank, r in res:
+        assert isinstance(r, dict), res
+        assert r["overlap1"] is True and r["overlap0"] is True and r["nocfg"] is True, (rank, r)
+    print(res[0][1]["oracle_msg"])
+    assert res[0][1]["oracle"] is True, res[0][1]["oracle_msg"]
 
 
 def _rccl_worker(port, q, graph=False):
@@ -343,30 +398,24 @@ def _cfg_cpu_worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
-def test_cfg_parallel_plan_cpu_gloo_world4():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _port()
-    procs = [ctx.Process(target=_cfg_cpu_worker, args=(r, 4, port, q)) for r in range(4)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=300) for _ in procs)
-    for p in procs:
-        p.join(60)
-    assert all(ok is True for _, ok in res), res
+@pytest.mark.parametrize("world", [4, 8])
+def test_cfg_parallel_plan_cpu_gloo(world):
+    res = _spawn(_cfg_cpu_worker, world)
+    assert len(res) == world and all(ok is True for _, ok in res), res
 
 
-def _cfg_gpu_worker(rank, world, port, q):
-    """world ranks share cuda:0: CFG sample per half (Ulysses inside a half when world = 4), the
+def _cfg_gpu_worker(rank, world, port, q, cfg_name="tiny"):
+    """world ranks share cuda:0: CFG sample per half (Ulysses inside a half when world >= 4), the
     velocities all-gathered across halves == the single-GPU batch-2 forward, bit for bit; also with
-    skip-layer guidance (sample 1 skips block 1) and for a batch-1 forward (the Ulysses fallback)."""
+    skip-layer guidance (sample 1 skips block 1) and for a batch-1 forward (the Ulysses fallback over
+    all ranks); the CFG output within the oracle's floor."""
     try:
         _init(rank, world, port)
         from oracle import wan_oracle as O
         from sp_util import HostStagedCfgParallel
         from vstyler import model_fn_wan_video
         from test_model_gpu import build
-        cfg = O.WAN_CONFIGS["tiny"]
+        cfg = O.WAN_CONFIGS[cfg_name]
         W = O.random_weights(cfg, seed=5)
         dit, vace = build(cfg, W, "cuda:0")
         lat, cp, cn, vc = O.synthetic_inputs(cfg, 5, 128, 128)
@@ -375,8 +424,9 @@ def _cfg_gpu_worker(rank, world, port, q):
         plan = HostStagedCfgParallel()
         res = {}
         cases = [("cfg", ctx, ()), ("cfg_slg", ctx, (1,))]
-        if world == 2:        # the fallback is Ulysses over all ranks: the tiny model has 2 heads
+        if cfg["num_heads"] % world == 0:     # the fallback is Ulysses over all ranks
             cases.append(("nocfg", ctx[0:1], ()))
+        outs = {}
         for name, c, slg in cases:
             single = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=c,
                                         vace_context=vc.cuda(), slg_blocks=slg)
@@ -385,7 +435,11 @@ def _cfg_gpu_worker(rank, world, port, q):
                                      sp_group=plan)
             torch.cuda.synchronize()
             res[name] = torch.equal(single.cpu(), par.cpu())
+            outs[name] = par.cpu()
         res["gathers"] = plan.collective_calls
+        if rank == 0:
+            res["oracle"], res["oracle_msg"] = _oracle_check(outs["cfg"], cfg, W, lat, t, (cp, cn), vc,
+                                                             f"CFG parallel world {world} {cfg_name}")
         q.put((rank, res))
     except Exception:  # pragma: no cover
         import traceback
@@ -393,21 +447,16 @@ def _cfg_gpu_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
-def test_cfg_parallel_model_bit_identical_on_one_gpu(world):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _port()
-    procs = [ctx.Process(target=_cfg_gpu_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=600) for _ in procs)
-    for p in procs:
-        p.join(60)
+@pytest.mark.parametrize("world,cfg_name", [(2, "tiny"), (4, "tiny"), (8, "sp8")])
+def test_cfg_parallel_model_bit_identical_on_one_gpu(world, cfg_name):
+    res = _spawn(_cfg_gpu_worker, world, cfg_name, timeout=600)
+    assert len(res) == world
     for rank, r in res:
         assert isinstance(r, dict), res
         assert r["cfg"] is True and r["cfg_slg"] is True and r.get("nocfg", True) is True, res
         assert r["gathers"] == 2, res
+    print(res[0][1]["oracle_msg"])
+    assert res[0][1]["oracle"] is True, res[0][1]["oracle_msg"]
 
 
 def test_plan_native_comms_cpu():
