@@ -7,8 +7,8 @@ contexts / VACE context of the real shapes (no checkpoints or datasets are reach
 
   python bench.py [--gpus N --steps K --warmup W]
 
-N > 1: one process per GPU, Ulysses SP over all N ranks over RCCL (VSTYLER_CFG_PARALLEL=1 selects CFG
-parallelism).  Under torchrun (WORLD_SIZE set) WORLD_SIZE must equal N; without a launcher this
+N > 1: one process per GPU, Ulysses SP over all N ranks over RCCL (VSTYLER_OPTS=cfg_parallel=1 selects
+CFG parallelism; sp_comm=native,sp_graph=1 captures the collectives into the step's hipGraph).  Under torchrun (WORLD_SIZE set) WORLD_SIZE must equal N; without a launcher this
 process spawns the N ranks itself (launch_ranks: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR
 127.0.0.1 / MASTER_PORT per child, rank 0 prints the line, exit code = the worst child's) and refuses
 when fewer than N GPUs are visible.  The line carries `rccl_world` and every rank's device and
@@ -405,7 +405,9 @@ def main():
         # Ulysses SP with the RCCL collectives inside the graph).  Capture happens inside the warmup.
         from vstyler.pipeline import sp_graph_ok
         use_graph = not args.no_graph and args.warmup >= 1 and (world == 1 or sp_graph_ok(sp))
-        stepper = DenoiseStepper(step_fn, ts, ds, use_graph=use_graph)
+        from vstyler.usp import plan_native_comms
+        stepper = DenoiseStepper(step_fn, ts, ds, use_graph=use_graph, plan=sp,
+                                 comms=plan_native_comms(sp) if use_graph and sp is not None else ())
         for i in range(args.warmup):
             stepper(i)
             torch.cuda.synchronize()

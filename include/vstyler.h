@@ -27,6 +27,8 @@ extern "C" {
 #define VS_E_COMM 4        /* RCCL missing or returned an error (vs_sp_last_error)     */
 
 const char* vs_strerror(int code);
+/* 2 since r6: vs_blaslt_library is gone (r5) and workspace kinds 2 / 3 are unused
+ * (vs_split_workspace_bytes returns 0); 1: r1-r5. */
 int vs_abi_version(void);
 
 /*
@@ -158,6 +160,10 @@ long long vs_split_workspace_bytes(int kind);
 int vs_split_workspace_bind(int kind, void* ptr, long long bytes, void* stream);
 
 /*
+ * Row kernels (vs_layernorm_modulate, _fp8, vs_residual_layernorm, vs_rmsnorm_rope): one 128-thread
+ * block per row, 5 chunks of 8 elements per thread, so dim % 8 == 0 and dim <= 5120 (every Wan
+ * width: 1536 / 5120); wider rows return VS_E_INVALID (r1-r4 accepted up to 6144).
+ *
  * out = bf16(LN(x)) [affine: weight/bias] then, if shift/scale given, modulate:
  * bf16(bf16(n * bf16(1+scale)) + shift) with shift/scale rows selected per batch.
  * Replaces WanAutoCastLayerNorm (layers.py:63-92) + modulate (wan_video_dit.py:64-65,225,228,268).

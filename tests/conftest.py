@@ -13,7 +13,7 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box via gpurun)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
     config.addinivalue_line("markers", "gpu_long: MI355X test whose oracle takes minutes (C4 block pair, "
-                                       "480x832 VAE): outside the round-end -m gpu tier, run by scripts/r4_parity.sh")
+                                       "480x832 VAE): outside the round-end -m gpu tier, run by scripts/ab/r4_parity.sh")
 
 
 def pytest_collection_modifyitems(config, items):

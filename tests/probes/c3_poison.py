@@ -1,5 +1,5 @@
 """14B-dim block pair, CFG batch 2 at 832x480x73: run the product forward twice (fresh Workspace
-buffers NaN-poisoned when VSTYLER_WS_POISON=1) and compare with each other and the oracle."""
+buffers NaN-poisoned with VSTYLER_OPTS=ws_poison=1) and compare with each other and the oracle."""
 import os, sys
 ROOT = os.path.join(os.path.dirname(__file__), "..", "..")
 sys.path[:0] = [ROOT, os.path.join(ROOT, "video-styler_amd"), os.path.join(ROOT, "tests")]
@@ -24,7 +24,8 @@ ref = O.model_fn(W, cfg, torch.cat([lat, lat]), t.expand(2), ctx, torch.cat([vc,
 for _ in range(2):
     outs.append(model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=ctx, vace_context=vc).clone())
 torch.cuda.synchronize()
-tag = f"poison={os.environ.get('VSTYLER_WS_POISON', '0')} order={first}"
+from vstyler.options import host_option
+tag = f"poison={host_option('ws_poison')} order={first}"
 for i, o in enumerate(outs):
     d = o.float() - ref.float()
     print(f"[{tag}] run {i}: finite {bool(torch.isfinite(o.float()).all())} rel vs oracle "

@@ -29,7 +29,8 @@ cfg = O.WAN_CONFIGS["tiny"]
 W = O.random_weights(cfg, seed=5)
 dit, vace = build(cfg, W, "cuda:0")
 lat, cp, cn, vc = O.synthetic_inputs(cfg, 5, 128, 128)
-os.environ["VSTYLER_SP_GRAPH"] = "1"
+from vstyler.options import set_host_option
+set_host_option("sp_graph", 1)
 for graph in (False, True):
     pipe = WanVideoPipeline(device="cuda")
     pipe.dit, pipe.vace = dit, vace

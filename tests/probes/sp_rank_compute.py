@@ -44,8 +44,9 @@ lat = torch.randn(1, 16, T, Hl, Wl, generator=g).to(torch.bfloat16).to(dev)
 ctx = (0.1 * torch.randn(2, 512, 4096, generator=g)).to(torch.bfloat16).to(dev)
 vc = torch.ones(1, 96, T, Hl, Wl).to(torch.bfloat16).to(dev)
 t = torch.tensor([999.0], device=dev).to(torch.bfloat16)
-OVL = os.environ.get("VSTYLER_SP_OVERLAP", "1") != "0"
-AB = os.environ.get("SPC_AB")        # "VAR=a,b": interleaved rounds of the env settings, one process
+from vstyler.options import host_option, set_host_option
+OVL = bool(host_option("sp_overlap"))      # VSTYLER_OPTS=sp_overlap=0 turns it off
+AB = os.environ.get("SPC_AB")        # "OPT=a,b": interleaved rounds of a host option's values, one process
 if AB:
     var, vals = AB.split("=")
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 8
@@ -55,7 +56,7 @@ if AB:
     res = {v: [] for v in vals.split(",")}
     for rnd in range(4):
         for v in res:
-            os.environ[var] = v
+            set_host_option(var, v)
             fn(); torch.cuda.synchronize()
             ts = []
             for _ in range(2):
@@ -66,7 +67,7 @@ if AB:
     sys.exit(0)
 if os.environ.get("SPC_GRAPH") == "1":
     # the per-rank step eager vs hipGraph-replayed (the exchanges are device copies on the caller's
-    # stream, so the step is capturable as with vs_sp_* under VSTYLER_SP_GRAPH=1): the launch cost
+    # stream, so the step is capturable as with vs_sp_* under host option sp_graph=1): the launch cost
     # the SP graph removes, interleaved rounds on one stream
     for a in sys.argv[1:] or ["8"]:
         P = int(a)

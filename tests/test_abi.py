@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     for s in header_symbols():
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, f"{s} has no ctypes signature"
-    assert lib.vs_abi_version() == 1
+    assert lib.vs_abi_version() == 2
 
 
 def test_error_codes_and_messages():

@@ -106,7 +106,6 @@ def test_residual_ln_fusion_follows_the_gemm_route(monkeypatch):
     epilogue (r5, include/vstyler.h), so the model never stages an output.  Host-only."""
     from vstyler import kernels as K
     from vstyler.models import _fusable_lt, quantize_fp8_
-    monkeypatch.delenv("VSTYLER_FUSE_RES_LN", raising=False)
     o = nn.Linear(5120, 5120, dtype=BF16)              # o-proj / cross-attention o shape
     down = nn.Linear(13824, 5120, dtype=BF16)          # FFN-down
     for M in (59280, 7410):

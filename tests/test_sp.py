@@ -204,6 +204,7 @@ def _rccl_worker(port, q, graph=False):
         from vstyler import model_fn_wan_video
         from vstyler.models import RunCtx, Workspace
         from vstyler.usp import UlyssesGroup, init_distributed
+        from vstyler.options import set_host_option
         from test_model_gpu import build
         init_distributed()
         assert torch.distributed.get_backend() == "nccl"
@@ -239,7 +240,7 @@ def _rccl_worker(port, q, graph=False):
         # overlap on with phase 4 merged over both samples (default) and per sample, then off
         for overlap, merge, key in ((True, "1", "model_overlap1"), (True, "0", "model_overlap1_permicro"),
                                     (False, "1", "model_overlap0")):
-            os.environ["VSTYLER_SP_MERGE_FFN"] = merge
+            set_host_option("sp_merge_ffn", merge)
             sp = UlyssesGroup(force_collectives=True)
             sp.overlap = overlap
             par = model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx,
@@ -250,7 +251,7 @@ def _rccl_worker(port, q, graph=False):
             want_calls = nblk * 2 * (2 if overlap else 1) + 1
             res[key] = torch.equal(single.cpu(), par.cpu()) and sp.collective_calls == want_calls
             res["calls_" + key] = (sp.collective_calls, want_calls)
-        os.environ.pop("VSTYLER_SP_MERGE_FFN")
+        set_host_option("sp_merge_ffn", 1)
         print("[rccl worker] 4 native", file=sys.stderr, flush=True)
         # (4) the C-ABI collectives (vs_sp_*: RCCL opened by libvstyler itself, its own communicator
         # and comm stream) under the overlap schedule: bit-identical too, and the raw exchanges
@@ -269,11 +270,11 @@ def _rccl_worker(port, q, graph=False):
         nblk = cfg["num_layers"] + len(cfg["vace_layers"])
         res["native_model"] = torch.equal(single.cpu(), par.cpu()) and sp.collective_calls == 2 + nblk * 4 + 1
         sp.native.close()
-        # (5) the SP denoising step with RCCL inside a hipGraph (VSTYLER_SP_GRAPH=1, set in this
+        # (5) the SP denoising step with RCCL inside a hipGraph (host option sp_graph=1, set in this
         # worker process only): its own test below
         if graph:
             print("[rccl worker] 5 graph", file=sys.stderr, flush=True)
-            os.environ["VSTYLER_SP_GRAPH"] = "1"
+            set_host_option("sp_graph", 1)
             # wan_video_new.py:515-542's loop with the collectives captured: libvstyler's own
             # communicator (on the capture stream) replays bit-identical to eager steps;
             # torch.distributed's RCCL is not capturable here and must fall back to eager steps
@@ -318,7 +319,7 @@ def test_ulysses_rccl_world1_bit_identical():
 
 @pytest.mark.gpu
 def test_ulysses_rccl_world1_graph_capture():
-    """The Ulysses denoising step captured with its RCCL collectives (VSTYLER_SP_GRAPH=1) over
+    """The Ulysses denoising step captured with its RCCL collectives (host option sp_graph=1) over
     vs_sp_* on the capture stream: replays bit-identical to eager steps.  torch.distributed's RCCL
     (process-group stream; its capture segfaults in hipStreamEndCapture on this HIP) is reported not
     capturable and runs the same steps eagerly."""
@@ -342,11 +343,12 @@ def _capturable_worker(port, q):
         from vstyler.pipeline import sp_graph_ok
         from vstyler.usp import UlyssesGroup
         from sp_util import CpuUlysses
+        from vstyler.options import set_host_option
         torch_plan = UlyssesGroup(comm="torch")
-        os.environ["VSTYLER_SP_GRAPH"] = "1"
+        set_host_option("sp_graph", 1)
         res = {"torch_plan": torch_plan.capturable, "torch_ok": sp_graph_ok(torch_plan),
                "host_staged_ok": sp_graph_ok(CpuUlysses(None, None)), "no_plan_ok": sp_graph_ok(None)}
-        os.environ["VSTYLER_SP_GRAPH"] = "0"
+        set_host_option("sp_graph", 0)
         res["opt_out_ok"] = sp_graph_ok(None)
         torch.distributed.destroy_process_group()
         q.put(res)
@@ -358,7 +360,7 @@ def _capturable_worker(port, q):
 def test_sp_graph_capturable_plans_cpu():
     """torch.distributed plans (RCCL on the process group's stream; also the default plan that
     sp_graph_ok falls back to when handed none) and host-staged substitutes are never captured,
-    and nothing is without VSTYLER_SP_GRAPH=1."""
+    and nothing is without host option sp_graph=1."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_capturable_worker, args=(_port(), q))
@@ -478,21 +480,21 @@ def test_plan_native_comms_cpu():
 
 
 def test_unbound_side_comms_guard():
-    """DenoiseStepper.capture refuses to capture while a live side-stream NativeComm is not bound to
-    the capture stream (RCCL forked into a capture from a side stream segfaulted in
-    hipStreamEndCapture), whatever plan attribute holds the communicator."""
+    """DenoiseStepper.capture refuses to capture while an open side-stream NativeComm reachable from
+    the step's plan is not bound to the capture stream (RCCL forked into a capture from a
+    side stream segfaulted in hipStreamEndCapture), whatever plan attribute holds the communicator;
+    communicators of other plans, and closed ones, do not count."""
+    from types import SimpleNamespace as NS
     from vstyler import usp
 
-    class FakeComm:                      # the attributes unbound_side_comms reads
-        def __init__(self, stream):
-            self.stream = stream
-    side, caller = FakeComm("side-stream"), FakeComm(None)
-    usp.NativeComm._live.add(side)
-    usp.NativeComm._live.add(caller)
-    try:
-        assert usp.unbound_side_comms("capture-origin") == [side]
-        side.stream = "capture-origin"   # what bind_stream does for the capture
-        assert usp.unbound_side_comms("capture-origin") == []
-    finally:
-        usp.NativeComm._live.discard(side)
-        usp.NativeComm._live.discard(caller)
+    def fake(stream, open_=True):        # a NativeComm without RCCL: the attributes the guard reads
+        c = usp.NativeComm.__new__(usp.NativeComm)
+        c.stream, c.handle = stream, (1 if open_ else None)
+        return c
+    side, caller, closed, other = fake("side-stream"), fake(None), fake("side-stream", False), fake("side-stream")
+    plan = NS(native=None, extra={"x": [NS(comm=side)]}, c=caller, gone=closed)
+    assert usp.unbound_side_comms("capture-origin", plan) == [side]
+    side.stream = "capture-origin"       # what bind_stream does for the capture
+    assert usp.unbound_side_comms("capture-origin", plan) == []
+    assert usp.unbound_side_comms("capture-origin", NS(native=None)) == []     # `other` is not the plan's
+    assert other.stream == "side-stream"

@@ -1100,12 +1100,7 @@ extern "C" int vs_attn_split_plan(int batch, int sq, int skv, int heads, int cus
 extern "C" long long vs_split_workspace_bytes(int kind) {
     if (kind == 0) return (long long)MAX_PIECES * BQ * PROW * (long long)sizeof(float);
     if (kind == 1) return vs_gemm_split_workspace_bytes_impl();
-#ifdef VS_AB
-    if (kind == 2) return 128LL << 20;          // the A/B build's vendor library (stream-K partials)
-    if (kind == 3) return -1;                   // its epilogue staging: m * n * 2 of the largest GEMM
-#else
     if (kind == 2 || kind == 3) return 0;       // not used (no vendor-library route in this build)
-#endif
     if (kind == 4) return 1LL << 20;            // attention item flags (int per item; zero-filled)
     if (kind == 5) return 4096;                 // GEMM tile-queue words (zero-filled; gemm.hip W4Sched)
     return -1;

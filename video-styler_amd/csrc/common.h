@@ -152,12 +152,3 @@ inline float* vs_split_workspace(int kind, size_t bytes, hipStream_t stream) {
 }
 
 long long vs_gemm_split_workspace_bytes_impl();   // gemm.hip
-#ifdef VS_AB
-// the A/B build's vendor-library route (blaslt.hip; -DVS_AB only, never the product library)
-int vs_lt_gemm_bias(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc, int m,
-                    int n, int k, const void* bias, hipStream_t stream);   // blaslt.hip
-int vs_lt_gemm_bias_gelu(const void* a, long long lda, const void* w, long long ldw, void* c, long long ldc, int m,
-                         int n, int k, const void* bias, hipStream_t stream);
-int vs_lt_gemm_fp8(const void* a8, long long lda, const float* scale_a, const void* w8, long long ldw, void* c,
-                   long long ldc, int m, int n, int k, const void* bias, bool gelu, hipStream_t stream);   // blaslt.hip
-#endif

@@ -734,7 +734,7 @@ extern "C" const char* vs_strerror(int code) {
     }
 }
 
-extern "C" int vs_abi_version(void) { return 1; }
+extern "C" int vs_abi_version(void) { return 2; }
 
 extern "C" int vs_unipc_update(float* out, const float* x, const float* m0, const float* m1, const float* mt,
                                long long n, int mode, const float* coef, void* stream) {

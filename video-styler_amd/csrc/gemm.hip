@@ -10,7 +10,7 @@
 //
 // Kernels sharing the epilogue:
 //  * gemm_bf16_tn_8p (K >= 4096 and >= 240 tiles of 256x256): the staggered 8-phase schedule (see
-//    its header) -- the DiT projections and FFN wherever hipBLASLt does not run them (lt_route);
+//    its header) -- the un-merged LoRA second phase and VS_OPT_GEMM_KERNEL 8;
 //  * gemm_fp8_tn_8p: the fp8 (config 5) variant of the same skeleton;
 //  * gemm_bf16_tn (everything else): the structure described below.
 // Structure: 128x128x64 tile, 4 waves (2x2, 64x64 each), v_mfma_f32_16x16x32_bf16 computing the
@@ -59,9 +59,6 @@ __device__ __forceinline__ void loadw(const bf16_t* p, float* v) {
         for (int i = 0; i < 4; ++i) { v[2 * i] = bflo(w[i]); v[2 * i + 1] = bfhi(w[i]); }
     }
 }
-#ifdef VS_AB
-__device__ __forceinline__ void load4(const bf16_t* p, float* v) { loadw<4>(p, v); }
-#endif
 
 // the op that follows each linear, on W consecutive columns of row m: y = bf16(acc + bias), then
 // GELU / SiLU / gate-residual [+ hint] / residual with the reference's bf16 rounding points
@@ -259,33 +256,6 @@ __global__ __launch_bounds__(256) void gemm_split_combine(const float* __restric
     epilogue_store(a, m, n, C, ldc, ep);
 }
 
-#ifdef VS_AB
-// Epilogue continuation after a hipBLASLt GEMM: y = bf16(acc + bias) is already materialised in
-// Y; feed it to the fused epilogue with no bias (rbf(y + 0) == y) so GELU / SiLU / gate-residual
-// [+ hint] / residual round exactly as in the fused kernels.  One thread per 4 columns.
-__global__ __launch_bounds__(256) void gemm_epi_apply(const bf16_t* Y, long long ldy, bf16_t* C, long long ldc,
-                                                      int M, int N, Epi ep) {
-    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-    const int n4 = N / 4;
-    if (idx >= (long long)M * n4) return;
-    const int m = (int)(idx / n4), n = 4 * (int)(idx % n4);
-    float v[4];
-    load4(Y + (long long)m * ldy + n, v);
-    epilogue_store(f32x4_t{v[0], v[1], v[2], v[3]}, m, n, C, ldc, ep);
-}
-
-// The same, 8 columns per thread with 16-B accesses and a (row, column-chunk) grid: no 64-bit
-// index division, one pass at the HBM rate (N % 8 == 0 and 16-B aligned rows; host-checked).
-__global__ __launch_bounds__(256) void gemm_epi_apply8(const bf16_t* Y, long long ldy, bf16_t* C, long long ldc,
-                                                       int N, Epi ep) {
-    const int m = blockIdx.x;
-    const int n = 8 * (blockIdx.y * 256 + threadIdx.x);
-    if (n >= N) return;
-    float v[8];
-    loadw<8>(Y + (long long)m * ldy + n, v);
-    epilogue_store_w<8>(v, m, n, C, ldc, ep);
-}
-#endif
 
 // ---------------------------------------------------------------------------------------------
 // gemm_bf16_tn_8p: 256x256x64 tile, 8 waves, 4 phases per K-tile (cdna_hip_programming.md §5,
@@ -1974,64 +1944,7 @@ KSplit plan_ksplit(int ntiles, int nh, int cus, int step = 64) {
 // vs 1410-1413, o-proj 1438-1441 vs 1291-1296), reads fewer L2->fabric bytes on q|k|v (16.8 vs
 // 17.9 GB per dispatch), and the whole step is as fast: 0.3906 / 0.3882 vs 0.3888 / 0.3881 steps/s
 // with the library routes, same box, interleaved (profiles/r5/queue_ab_s2.log,
-// pmc_fetch_queue_s2.txt, bench_own_vs_lt_ab_s2.log).  The library route survives only in the A/B
-// build (-DVS_AB, `make ab`; VS_GEMM_BACKEND=lt there), never in libvstyler.so.
-#ifdef VS_AB
-bool vs_lt_is_private();
-// A/B build only: VS_GEMM_BACKEND=lt sends every eligible GEMM (no LoRA phase) to hipBLASLt, =r4 the
-// r4 routing (plain-bias GEMMs of >= 1024 tiles, the GELU FFN-up, the small-grid context GEMMs)
-static bool lt_route(int m, int n, int k, int epilogue = VS_EPI_BIAS) {
-    const char* e = getenv("VS_GEMM_BACKEND");
-    if (!e || (e[0] != 'l' && e[0] != 'r')) return false;
-    if (e[0] == 'l') return true;
-    const bool resid = epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES;
-    const long long tiles = (long long)((m + 255) / 256) * ((n + 255) / 256);
-    if (resid || (k >= 12288 && m <= 16384) || (epilogue == VS_EPI_GELU && k <= 8192 && m <= 8192)) return false;
-    return tiles >= 1024 || (tiles >= 256 && (k <= 8192 || vs_lt_is_private())) ||
-           (k <= 8192 && n >= 2048 && k >= 1024);
-}
-static bool fp8_lt_route(int n, int k, int epilogue) {
-    const char* e = getenv("VS_GEMM_BACKEND");
-    return e && (e[0] == 'l' || (e[0] == 'r' && epilogue == VS_EPI_BIAS && n >= 2 * k));
-}
-
-// hipBLASLt for bf16(A W^T [* scale] + bias) (gemm(y, ldy)), then the rest of the epilogue with
-// the fused kernels' code (see blaslt.hip).  false: no workspace bound or hipBLASLt declined the
-// shape -- the caller falls through to the MFMA kernels.
-template <class Gemm>
-static bool lt_with_epilogue(void* c, long long ldc, int m, int n, int epilogue, const Epi& ep, hipStream_t stream,
-                             Gemm gemm) {
-    const bool staged = epilogue == VS_EPI_GATE_RES || epilogue == VS_EPI_RES;
-    bf16_t* y = (bf16_t*)c;
-    long long ldy = ldc;
-    if (staged) {
-        y = (bf16_t*)vs_split_workspace(3, (size_t)m * n * 2, stream);
-        ldy = n;
-    }
-    if (!y || gemm((void*)y, ldy) != VS_OK) return false;
-    if (epilogue != VS_EPI_BIAS) {
-        Epi e2 = ep;
-        e2.bias = nullptr;
-        const bool w8 = n % 8 == 0 && ldy % 8 == 0 && ldc % 8 == 0 && aligned16(y) && aligned16(c) &&
-                        (!e2.res || (e2.ld_res % 8 == 0 && aligned16(e2.res))) &&
-                        (!e2.gate || (e2.gate_bstride % 8 == 0 && aligned16(e2.gate))) &&
-                        (!e2.hint || (e2.ld_hint % 8 == 0 && aligned16(e2.hint)));
-        if (w8) {
-            hipLaunchKernelGGL(gemm_epi_apply8, dim3((unsigned)m, (unsigned)((n / 8 + 255) / 256)), dim3(256), 0,
-                               stream, y, ldy, (bf16_t*)c, ldc, n, e2);
-        } else {
-            const long long threads = (long long)m * (n / 4);
-            hipLaunchKernelGGL(gemm_epi_apply, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, y, ldy,
-                               (bf16_t*)c, ldc, m, n, e2);
-        }
-        if (hipGetLastError() != hipSuccess) return false;
-    }
-    return true;
-}
-#else
-static bool lt_route(int, int, int, int = VS_EPI_BIAS) { return false; }
-static bool fp8_lt_route(int, int, int) { return false; }
-#endif
+// pmc_fetch_queue_s2.txt, bench_own_vs_lt_ab_s2.log).  r6 removed the A/B build's library route.
 
 // which 256x256 kernel runs the un-split-phase (k2 == 0) GEMMs: the 4-wave kernel (default since
 // r4: 1-5 % over the 8-phase kernel on every 14B shape at 59 280 and 7410 rows) | VS_OPT_GEMM_KERNEL 8
@@ -2108,13 +2021,6 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
     const long long tiles256 = (long long)((m + BT - 1) / BT) * ((n + BT - 1) / BT);
     const bool big = force ? force == 256
                            : (tiles256 >= 240 && k >= 4096) || (tiles256 >= 128 && k >= 1024 && k2 == 0 && use_4w());
-#ifdef VS_AB
-    if (k2 == 0 && lt_route(m, n, k, epilogue) &&
-        lt_with_epilogue(c, ldc, m, n, epilogue, ep, (hipStream_t)stream, [&](void* y, long long ldy) {
-            return vs_lt_gemm_bias(a, lda, w, ldw, y, ldy, m, n, k, ep.bias, (hipStream_t)stream);
-        }))
-        return VS_OK;
-#endif
     if (big) {
         // 256x256 staggered 8-phase kernel (LoRA second phase included); the last partial round of
         // tiles runs as K pieces + combine (split tail)
@@ -2206,13 +2112,6 @@ extern "C" int vs_gemm_fp8(const void* a8, long long lda, const float* scale_a, 
     // the 4-wave kernel runs it at 3013 vs 3068 and every fused-epilogue shape ahead of the library
     // + its epilogue pass (FFN-up 2839 vs 2500, o-proj 2652 vs 2225: profiles/r5/
     // gemm_fp8_queue_ab_s1.log), so every fp8 GEMM runs here (the library only in the A/B build)
-#ifdef VS_AB
-    if (fp8_lt_route(n, k, epilogue) &&
-        lt_with_epilogue(c, ldc, m, n, epilogue, ep, (hipStream_t)stream, [&](void* y, long long ldy) {
-            return vs_lt_gemm_fp8(a8, lda, scale_a, w8, ldw, y, ldy, m, n, k, ep.bias, false, (hipStream_t)stream);
-        }))
-        return VS_OK;
-#endif
     // the fp8 MFMA kernels (K-tiles of 128 fp8)
     const int tm = (m + BT - 1) / BT, tn = (n + BT - 1) / BT;
     static bool attr8 = false;
@@ -2286,10 +2185,11 @@ extern "C" int vs_quant_fp8_rows(const void* x, long long ldx, void* x8, long lo
 }
 
 // the route of a GEMM (include/vstyler.h): 0 = the MFMA kernels with the fused epilogue, the only
-// route of the product library; the A/B build reports its library route (1) as r4 did
+// route there is (r1-r4's vendor-library route, 1, is gone)
 extern "C" int vs_gemm_route_epi(int m, int n, int k, int epilogue, int fp8) {
     if (m <= 0 || n <= 0 || k <= 0 || epilogue < VS_EPI_BIAS || epilogue > VS_EPI_RES) return -VS_E_INVALID;
-    return (fp8 ? fp8_lt_route(n, k, epilogue) : lt_route(m, n, k, epilogue)) ? 1 : 0;
+    (void)fp8;
+    return 0;
 }
 extern "C" int vs_gemm_route(int m, int n, int k) { return vs_gemm_route_epi(m, n, k, VS_EPI_BIAS, 0); }
 

@@ -9,7 +9,8 @@ from .flow_match import FlowMatchScheduler
 from .models import VaceWanModel, WanModel, init_random_
 from .pipeline import ModelConfig, WanVideoPipeline, model_fn_wan_video
 
-if os.environ.get("VSTYLER_OPTS"):     # path selection for a whole A/B run (kernels.apply_env_options)
+if os.environ.get("VSTYLER_OPTS"):     # path selection for a whole A/B run (kernels.apply_env_options;
+    # host option names: vstyler.options, the rest libvstyler's VS_OPT_*)
     from .kernels import apply_env_options
     apply_env_options()
 

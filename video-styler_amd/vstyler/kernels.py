@@ -50,21 +50,20 @@ class options:
 
 
 def apply_env_options():
-    """VSTYLER_OPTS="queue=0,attn_nc=0": the one environment hook, read by the Python host (never
-    by the library) so that A/B scripts can select paths of a whole run."""
-    spec = os.environ.get("VSTYLER_OPTS", "")
-    for item in filter(None, (x.strip() for x in spec.split(","))):
-        name, _, value = item.partition("=")
-        set_option(name.strip(), int(value))
+    """VSTYLER_OPTS="queue=0,sp_comm=native": the one environment hook, read by the Python host
+    (never by the library) so that A/B scripts can select paths of a whole run: host option names
+    (vstyler.options) set the host's table, every other name a library option."""
+    from .options import apply_spec
+    apply_spec(os.environ.get("VSTYLER_OPTS", ""), set_option)
 
 
 _SPLIT_WS = {}
 
 
 def _split_ws(kind, t, nbytes=None):
-    """Bind library scratch of `kind` (0 attention split tail, 1 GEMM split tail, 2 / 3 the A/B build's
-    vendor-library workspace and epilogue staging, 4 attention item flags, 5 GEMM tile and attention
-    item queues) for the current stream of t's device from the torch
+    """Bind library scratch of `kind` (0 attention split tail, 1 GEMM split tail, 2 / 3 unused since
+    r6 (the removed vendor-library route), 4 attention item flags, 5 GEMM tile and attention item
+    queues) for the current stream of t's device from the torch
     allocator (vs_split_workspace_bind: the library never allocates).  Re-bound larger when a
     bigger one is needed; never inside a graph capture (the library then takes its fallback)."""
     stream = _stream(t)
@@ -74,7 +73,7 @@ def _split_ws(kind, t, nbytes=None):
         if have is not None:
             return
         nbytes = _lib.load().vs_split_workspace_bytes(kind)
-        if nbytes <= 0:             # a kind this build does not use (2, 3: the A/B build's library route)
+        if nbytes <= 0:             # a kind this build does not use (2, 3)
             return
     elif have is not None and have.numel() >= nbytes:
         return

@@ -9,12 +9,12 @@ Reference: diffsynth/models/wan_video_dit.py (DiTBlock :196-230, Head :253-269, 
 (diffsynth/pipelines/wan_video_new.py:1260-1468).
 """
 import math
-import os
 
 import torch
 import torch.nn as nn
 
 from . import kernels as K
+from .options import host_option
 
 BF16 = torch.bfloat16
 
@@ -97,8 +97,8 @@ def _fusable_lt(lin, M, epilogue):
     product library fuses every epilogue), i.e. when that pass could fuse with the LayerNorm that
     follows (vs_residual_layernorm) with the same rounding points.  Otherwise the residual epilogue is
     fused into the GEMM and the LayerNorm runs alone.  A hot-loaded LoRA keeps the MFMA kernel's fused
-    epilogue.  VSTYLER_FUSE_RES_LN=0 disables."""
-    if getattr(lin, "lora_A", None) is not None or os.environ.get("VSTYLER_FUSE_RES_LN", "1") == "0":
+    epilogue.  Host option fuse_res_ln=0 disables."""
+    if getattr(lin, "lora_A", None) is not None or not host_option("fuse_res_ln"):
         return False
     fp8 = getattr(lin, "weight_fp8", None) is not None
     return K.gemm_route(M, lin.out_features, lin.in_features, epilogue=epilogue, fp8=fp8)
@@ -249,13 +249,10 @@ class Workspace:
         t = self.bufs.get(name)
         if t is None or t.shape != shape or t.dtype != dtype:
             t = torch.empty(shape, device=self.device, dtype=dtype)
-            if _POISON:                 # debugging aid: NaN-fill so a read-before-write shows up
+            if host_option("ws_poison"):    # debugging aid: NaN-fill so a read-before-write shows up
                 t.view(torch.uint8).fill_(0xFF)
             self.bufs[name] = t
         return t
-
-
-_POISON = os.environ.get("VSTYLER_WS_POISON", "0") == "1"
 
 
 class KernelTimer:
@@ -350,7 +347,7 @@ class DiTBlock(nn.Module):
         0's q|k|v all-to-all runs under sample 1's projections, sample 1's under sample 0's
         attention, sample 0's return exchange under sample 1's attention and sample 1's under sample
         0's o-proj; phase 4 then runs once on both samples' rows (GEMMs of 2S/p rows instead of two
-        of S/p: VSTYLER_SP_MERGE_FFN=0 keeps it per sample)."""
+        of S/p: host option sp_merge_ffn=0 keeps it per sample)."""
         B, S, D, ws = rc.batch, rc.seq, self.dim, rc.ws
         if rc.pre_mod is not None:          # the previous block already ran this one's LN1
             mod, ln1_done = rc.pre_mod, True
@@ -371,12 +368,12 @@ class DiTBlock(nn.Module):
             p["ln1_done"] = ln1_done
         # phase 4 on all rows at once (the overlapped SP micro-batches)
         tail = self._part(x, mod, rc, 0, B, hint, "") if len(parts) > 1 and \
-            os.environ.get("VSTYLER_SP_MERGE_FFN", "1") != "0" else None
+            host_option("sp_merge_ffn") else None
         # the fused FFN-down epilogue needs the consumer's modulation first (its own mod buffer)
         fuse = None
         if nxt is not None and only_batch is None and \
                 _fusable_lt(self.ffn[2], (tail or parts[0])["M"], K.VS_EPI_GATE_RES) and \
-                os.environ.get("VSTYLER_FUSE_FFN_LN", "1") != "0":
+                host_option("fuse_ffn_ln"):
             if isinstance(nxt, DiTBlock):
                 nslot = rc.mod_slot ^ 1
                 nmod = ws.get(f"mod{nslot}", (B, 6, D))

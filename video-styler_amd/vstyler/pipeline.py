@@ -16,6 +16,7 @@ import torch
 from . import kernels as K
 from .flow_match import FlowMatchScheduler
 from .models import RunCtx, Workspace, WanModel, VaceWanModel
+from .options import host_option
 
 BF16 = torch.bfloat16
 
@@ -211,14 +212,14 @@ def redirect_model_configs(model_configs):
 
 def sp_graph_ok(plan):
     """True when the sequence-parallel plan's collectives can be captured into the step's hipGraph:
-    VSTYLER_SP_GRAPH=1 and RCCL through libvstyler's vs_sp_* (VSTYLER_SP_COMM=native) -- not
+    host options sp_graph=1 and sp_comm=native (RCCL through libvstyler's vs_sp_*) -- not
     torch.distributed's RCCL, whose process-group stream the capture does not survive on this
     image's HIP (segfault in hipStreamEndCapture, profiles/r3/sp_graph_probe_faulthandler.log), and
     not host-staged substitutes (tests).  NativeComm in side-stream mode keeps its exchange/compute
     overlap in the graph: DenoiseStepper binds its comm stream to the capture origin and forks the
     compute (usp.NativeComm).  Opt-in: only world size 1 has run on hardware
     (test_ulysses_rccl_world1_graph_capture); SP steps run eager by default."""
-    if os.environ.get("VSTYLER_SP_GRAPH", "0") != "1":
+    if not host_option("sp_graph"):
         return False
     if plan is None:
         from .usp import get_default_group
@@ -241,15 +242,18 @@ class DenoiseStepper:
     comms: side-stream NativeComm objects of an SP plan (usp.plan_native_comms).  With a graph they
     are bound to the stepper's stream -- the capture origin -- and the step's compute runs on a
     second stream forked from it and joined back, so the collectives overlap the compute inside
-    the graph while RCCL itself only ever runs on the origin stream."""
+    the graph while RCCL itself only ever runs on the origin stream.  plan: the step's SP plan (None
+    without SP): the capture is refused while a side-stream communicator reachable from it is not
+    bound to the capture stream (usp.unbound_side_comms)."""
 
-    def __init__(self, step_fn, timesteps_bf16, dsigmas_f32, use_graph=True, on_replay=None, comms=()):
+    def __init__(self, step_fn, timesteps_bf16, dsigmas_f32, use_graph=True, on_replay=None, comms=(), plan=None):
         self.step_fn, self.ts, self.ds = step_fn, timesteps_bf16, dsigmas_f32
         self.t_buf, self.d_buf = timesteps_bf16[0:1].clone(), dsigmas_f32[0:1].clone()
         self.use_graph, self.graph, self.on_replay = use_graph, None, on_replay
         dev = self.t_buf.device
         self.stream = torch.cuda.Stream(device=dev) if use_graph else None
         self.comms = list(comms) if use_graph else []
+        self.plan = plan
         self.compute = torch.cuda.Stream(device=dev) if self.comms else None
 
     def _run(self):
@@ -287,8 +291,10 @@ class DenoiseStepper:
     def capture(self):
         g = torch.cuda.CUDAGraph()
         err = None
-        from .usp import unbound_side_comms
-        stray = unbound_side_comms(self.stream)
+        stray = []
+        if self.plan is not None:
+            from .usp import unbound_side_comms
+            stray = unbound_side_comms(self.stream, self.plan)
         if stray:                   # RCCL forked into the capture from a side stream: never capture
             err = RuntimeError(f"{len(stray)} side-stream communicator(s) not bound to the capture stream")
         else:
@@ -441,13 +447,13 @@ class WanVideoPipeline:
         (torch.cuda.CUDAGraph over hipStreamBeginCapture) and replayed for every later step.  The
         graph reads the step's bf16 timestep and fp32 dsigma from two device slots refreshed before
         each replay, so one capture serves all steps.  Under Ulysses SP the RCCL collectives (async
-        all-to-alls on RCCL's stream, event-ordered) are captured with the step only with
-        VSTYLER_SP_GRAPH=1 (sp_graph_ok); eager with use_graph=False / VSTYLER_GRAPH=0."""
+        all-to-alls on RCCL's stream, event-ordered) are captured with the step only with host option
+        sp_graph=1 (sp_graph_ok); eager with use_graph=False / host option graph=0."""
         self.scheduler.set_timesteps(num_inference_steps, denoising_strength=denoising_strength, shift=sigma_shift)
         n_steps = len(self.scheduler.timesteps)
         use_cfg = cfg_scale != 1.0
         if use_graph is None:
-            use_graph = os.environ.get("VSTYLER_GRAPH", "1") != "0"
+            use_graph = bool(host_option("graph"))
         # TeaCache decides per step on the host (wan_video_new.py:1173-1192): eager steps
         use_graph = use_graph and n_steps > 1 and tea_cache is None and \
             (not self.use_unified_sequence_parallel or sp_graph_ok(self.sp_group))
@@ -464,11 +470,12 @@ class WanVideoPipeline:
                               sp_group=self.sp_group, tea_cache=tea_cache)
             K.cfg_euler_dev(v[0:1], v[1:2] if use_cfg else None, latents, cfg_scale, d_buf)
 
-        comms = ()
-        if use_graph and self.use_unified_sequence_parallel:
-            from .usp import plan_native_comms
-            comms = plan_native_comms(self.sp_group)
-        stepper = DenoiseStepper(step, ts, ds, use_graph, comms=comms)
+        comms, plan = (), None
+        if self.use_unified_sequence_parallel:
+            from .usp import get_default_group, plan_native_comms
+            plan = self.sp_group if self.sp_group is not None else get_default_group()
+            comms = plan_native_comms(plan) if use_graph else ()
+        stepper = DenoiseStepper(step, ts, ds, use_graph, comms=comms, plan=plan)
         steps = range(n_steps)
         if progress_bar_cmd is not None:
             steps = progress_bar_cmd(steps)

@@ -11,7 +11,6 @@ carries the output back; layout transforms are the vs_ulysses_permute kernel.  R
 S % p == 0 and heads % p == 0 (asserted instead of the reference's silent zero padding).
 """
 import ctypes
-import weakref
 import os
 
 import torch
@@ -19,6 +18,7 @@ import torch.distributed as dist
 
 from . import kernels as K
 from .models import RunCtx
+from .options import host_option
 
 _DEFAULT = None
 
@@ -43,16 +43,14 @@ def init_distributed():
 
 def get_default_group():
     """The parallel plan of the whole world: one UlyssesGroup over all ranks (the reference's USP,
-    "0", the default), or CfgParallel when VSTYLER_CFG_PARALLEL selects it ("1": at every even world
-    size, Ulysses inside each half; "auto": at world size 2 only, where Ulysses would send half of
+    "0", the default), or CfgParallel when host option cfg_parallel selects it ("1": at every even
+    world size, Ulysses inside each half; "auto": at world size 2 only, where Ulysses would send half of
     every q|k|v over one xGMI link per block while CFG parallelism needs one 2-sample velocity
     exchange per step).  CfgParallel stays opt-in until a multi-GPU RCCL run has shown its output
     bit-identical to the single-GPU forward (the tests cover it with host-staged collectives)."""
     global _DEFAULT
     if _DEFAULT is None and dist.is_initialized():
-        mode = os.environ.get("VSTYLER_CFG_PARALLEL", "0")
-        if mode not in ("auto", "0", "1"):
-            raise ValueError(f"VSTYLER_CFG_PARALLEL must be auto, 0 or 1, not {mode!r}")
+        mode = host_option("cfg_parallel")
         world = dist.get_world_size()
         if world % 2 == 0 and (mode == "1" or (mode == "auto" and world == 2)):
             _DEFAULT = CfgParallel()
@@ -85,8 +83,8 @@ class NativeComm:
     communicator runs on ONE dedicated stream, ordered after the work enqueued so far on the caller's
     stream (RCCL's async pattern), so collectives of one communicator never reorder; all_gather then
     makes the caller's stream wait for it (synchronous to the caller, as torch's all_gather).  The
-    communicator is destroyed by close() or when the object is collected.  Selected with
-    VSTYLER_SP_COMM=native."""
+    communicator is destroyed by close() or when the object is collected.  Selected with host
+    option sp_comm=native."""
 
     def __init__(self, group=None, stream=None):
         from . import _lib
@@ -105,7 +103,7 @@ class NativeComm:
                                    ctypes.byref(self.handle)))
         # stream="side" (default): the collectives run on a stream of their own, ordered after the
         # caller's work by events, so they overlap the compute enqueued meanwhile.  "caller"
-        # (VSTYLER_SP_COMM_STREAM=caller): on the caller's stream, in order with the compute.
+        # (host option sp_comm_stream=caller): on the caller's stream, in order with the compute.
         # hipGraph capture: RCCL on a side stream FORKED into a capture segfaults in
         # hipStreamEndCapture on this image's HIP 7.0 (torch's ProcessGroupNCCL stream and this
         # class's own alike; profiles/r3/sp_graph_probe_faulthandler.log), while RCCL on the capture's
@@ -114,20 +112,22 @@ class NativeComm:
         # is bound to the capture origin (bind_stream) and the compute runs on a stream forked from
         # it -- the same event-ordered overlap, with RCCL where the capture accepts it.
         if stream is None:
-            stream = os.environ.get("VSTYLER_SP_COMM_STREAM") or "side"
+            stream = host_option("sp_comm_stream")
         if stream not in ("caller", "side"):
-            raise ValueError(f"VSTYLER_SP_COMM_STREAM must be 'caller' or 'side', not {stream!r}")
+            raise ValueError(f"sp_comm_stream must be 'caller' or 'side', not {stream!r}")
         self.stream = None if stream == "caller" else torch.cuda.Stream()
-        NativeComm._live.add(self)
-
-    _live = weakref.WeakSet()           # every communicator of the process (unbound_side_comms)
 
     @property
     def capturable(self):
         """On the caller's stream, or on a side stream the step's capture binds to its origin --
-        DenoiseStepper.capture refuses to capture while any live side-stream communicator is not
-        bound to the capture stream (unbound_side_comms), whatever plan attribute holds it."""
+        DenoiseStepper.capture refuses to capture while an open side-stream communicator reachable
+        from the step's plan is not bound to the capture stream (unbound_side_comms), whatever plan
+        attribute holds it."""
         return True
+
+    @property
+    def is_open(self):
+        return bool(getattr(self, "handle", None))
 
     def bind_stream(self, stream):
         """Run the side-stream collectives on `stream` (the capture origin of DenoiseStepper);
@@ -194,11 +194,11 @@ class _Exchange:
 class UlyssesGroup:
     """overlap: split the CFG batch into per-sample micro-batches inside each block so one half's
     all-to-alls (async on RCCL's stream) run under the other half's GEMMs / attention / FFN
-    (VSTYLER_SP_OVERLAP=0 disables).  force_collectives: run the sharded path (permutes and RCCL
+    (host option sp_overlap=0 disables).  force_collectives: run the sharded path (permutes and RCCL
     collectives) even at world size 1, where model_fn_wan_video otherwise takes the plain path
     (tests use it to drive the real collectives on a one-GPU box).  comm: "torch" (torch.distributed
     on the process group, default) or "native" (NativeComm: RCCL through libvstyler's vs_sp_* ABI);
-    default from VSTYLER_SP_COMM."""
+    default from host option sp_comm."""
 
     @property
     def capturable(self):
@@ -211,12 +211,12 @@ class UlyssesGroup:
         self.group = group
         self.world_size = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.overlap = os.environ.get("VSTYLER_SP_OVERLAP", "1") != "0"
+        self.overlap = bool(host_option("sp_overlap"))
         self.force_collectives = force_collectives
         self.collective_calls = 0
-        comm = comm or os.environ.get("VSTYLER_SP_COMM", "torch")
+        comm = comm or host_option("sp_comm")
         if comm not in ("torch", "native"):
-            raise ValueError(f"VSTYLER_SP_COMM must be 'torch' or 'native', not {comm!r}")
+            raise ValueError(f"sp_comm must be 'torch' or 'native', not {comm!r}")
         self.native = NativeComm(group) if comm == "native" else None
 
     # -------------------------------------------------------------- layout helpers (kernels)
@@ -295,7 +295,7 @@ class UlyssesGroup:
         # one sample: chunk j holds its tokens' q|k|v rows for rank j's heads ([Sl, 3 cpr]), so the
         # received buffer is the whole sequence's q|k|v rows in token order -- attention reads it in
         # place.  Several samples: chunk j is [q | k | v] of [B, Sl, cpr] each, re-laid out on arrival.
-        e.rows = batch == 1 and os.environ.get("VSTYLER_SP_ROWS", "1") != "0"
+        e.rows = batch == 1 and bool(host_option("sp_rows"))
         for i, t in enumerate((q, k, v)):     # row stride: q/k/v may be column slices of a fused q|k|v
             if e.rows:
                 self._permute(t, send[i * e.cpr:], 1, e.Sl, e.cpr, t.stride(0), 3 * e.chunk, 0, 3 * e.cpr)
@@ -341,11 +341,39 @@ class UlyssesGroup:
 _WS_BY_DEV = {}
 
 
-def unbound_side_comms(stream):
-    """The live side-stream NativeComm objects whose collectives would NOT run on `stream` (a graph
-    capture's origin): RCCL forked into a capture from any other stream segfaulted in
-    hipStreamEndCapture (NativeComm's comment), so a capture must see this list empty."""
-    return [c for c in list(NativeComm._live) if c.stream is not None and c.stream != stream]
+def reachable_native_comms(plan, depth=4):
+    """Every open NativeComm reachable from a parallel plan through its attributes (any name, lists,
+    tuples and dicts included, `depth` levels deep)."""
+    out, seen = [], set()
+
+    def visit(o, d):
+        if o is None or id(o) in seen or d < 0 or isinstance(o, (str, bytes, int, float, torch.Tensor)):
+            return
+        seen.add(id(o))
+        if isinstance(o, NativeComm):
+            if o.is_open:
+                out.append(o)
+            return
+        if isinstance(o, dict):
+            items = list(o.values())
+        elif isinstance(o, (list, tuple, set)):
+            items = list(o)
+        elif hasattr(o, "__dict__"):
+            items = list(vars(o).values())
+        else:
+            return
+        for x in items:
+            visit(x, d - 1)
+    visit(plan, depth)
+    return out
+
+
+def unbound_side_comms(stream, plan):
+    """The open side-stream NativeComm objects of `plan` (reachable_native_comms) whose collectives
+    would NOT run on `stream` (a graph capture's origin): RCCL forked into a capture from any other
+    stream segfaulted in hipStreamEndCapture (NativeComm's comment), so a capture must see this list
+    empty.  Communicators of other plans are not launched by the step and do not count."""
+    return [c for c in reachable_native_comms(plan) if c.stream is not None and c.stream != stream]
 
 
 def plan_native_comms(plan):
@@ -401,7 +429,7 @@ class CfgParallel:
         self.pair_group = pairs[self.half_rank]
         self.ulysses = ulysses_cls(halves[self.cfg_rank], comm=comm) if u > 1 else None
         self.full = ulysses_cls(group, comm=comm)
-        comm = comm or os.environ.get("VSTYLER_SP_COMM", "torch")
+        comm = comm or host_option("sp_comm")
         # the velocity exchange goes through the same comm kind as the Ulysses exchanges
         self.pair_native = NativeComm(self.pair_group) if comm == "native" else None
         self.collective_calls = 0
