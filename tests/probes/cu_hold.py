@@ -58,16 +58,26 @@ def case(name, fn, variants):
 
 g = torch.Generator(device="cuda").manual_seed(1)
 GEMM = {"queue": dict(queue=1), "static": dict(queue=0)}      # (the attention's item queues too)
+# r6: split-tail pieces from the queue's piece pool (default) vs as workgroups of their own
+GEMM_PIECES = {"queue": dict(queue=1, piece_queue=1), "queue_piece_blocks": dict(queue=1, piece_queue=0),
+               "static": dict(queue=0)}
+only = os.environ.get("CH_ONLY")          # e.g. "ffn-down" (a substring of the case names)
 for M, N, Kd, epi, name in ((59280, 13824, 5120, K.VS_EPI_GELU, "ffn-up 59280"), (7410, 15360, 5120, K.VS_EPI_BIAS,
-                            "q|k|v 7410 (SP=8 rows)"), (7410, 5120, 13824, K.VS_EPI_BIAS, "ffn-down 7410")):
+                            "q|k|v 7410 (SP=8 rows)"), (7410, 5120, 13824, K.VS_EPI_BIAS, "ffn-down 7410"),
+                            (59280, 5120, 13824, K.VS_EPI_BIAS, "ffn-down 59280"),
+                            (7410, 5120, 5120, K.VS_EPI_BIAS, "o-proj 7410")):
+    if only and only not in name:
+        continue
     a = torch.randn(M, Kd, device="cuda", generator=g).to(torch.bfloat16)
     w = (0.05 * torch.randn(N, Kd, device="cuda", generator=g)).to(torch.bfloat16)
     b = (0.1 * torch.randn(N, device="cuda", generator=g)).to(torch.bfloat16)
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    case(name, lambda: K.gemm(a, w, out, epilogue=epi, bias=b), GEMM)
+    case(name, lambda: K.gemm(a, w, out, epilogue=epi, bias=b), GEMM_PIECES)
     del a, w, b, out
 # self-attention at the SP = 8 rank shape (5 heads, full sequence) and at SP = 1
 for H, name in ((5, "attention SP=8 (5 heads)"), (40, "attention SP=1 (40 heads)")):
+    if only and only not in name:
+        continue
     B, S = 2, 29640
     q, k_, v = (torch.randn(B * S, H * 128, device="cuda", generator=g).to(torch.bfloat16) for _ in range(3))
     o = torch.empty_like(q)

@@ -44,7 +44,7 @@ lat = torch.randn(1, 16, T, Hl, Wl, generator=g).to(torch.bfloat16).to(dev)
 ctx = (0.1 * torch.randn(2, 512, 4096, generator=g)).to(torch.bfloat16).to(dev)
 vc = torch.ones(1, 96, T, Hl, Wl).to(torch.bfloat16).to(dev)
 t = torch.tensor([999.0], device=dev).to(torch.bfloat16)
-from vstyler.options import host_option, set_host_option
+from vstyler.options import HOST_DEFAULTS, host_option, set_host_option
 OVL = bool(host_option("sp_overlap"))      # VSTYLER_OPTS=sp_overlap=0 turns it off
 AB = os.environ.get("SPC_AB")        # "OPT=a,b": interleaved rounds of a host option's values, one process
 if AB:
@@ -56,7 +56,10 @@ if AB:
     res = {v: [] for v in vals.split(",")}
     for rnd in range(4):
         for v in res:
-            set_host_option(var, v)
+            if var in HOST_DEFAULTS:
+                set_host_option(var, v)
+            else:                       # a libvstyler option (e.g. piece_queue)
+                K.set_option(var, int(v))
             fn(); torch.cuda.synchronize()
             ts = []
             for _ in range(2):

@@ -178,7 +178,7 @@ def test_options_table():
     lib = _lib.load()
     defaults = {"gemm_tile": 0, "gemm_kernel": 4, "gemm_split": 1, "queue": 1, "attn_impl": 0,
                 "attn_mfma": 16, "attn_nc": 1, "attn_split": 1, "attn_persist": 1, "vae_pxb": 2, "vae_pre": 3,
-                "vae_halo": 1}
+                "vae_halo": 1, "piece_queue": 1}
     assert set(defaults) == set(_lib.OPTIONS)
     for name, v in defaults.items():
         assert K.get_option(name) == v, name

@@ -23,9 +23,12 @@ def ints(*shape, g, lo=-3, hi=4):
     return torch.randint(lo, hi, shape, generator=g, device="cuda").to(BF16)
 
 
-@pytest.fixture(params=["queue", "static"])
+@pytest.fixture(params=["queue", "queue_piece_blocks", "static"])
 def sched(opt, request):
-    opt(gemm_tile=256, gemm_kernel=4, queue=1 if request.param == "queue" else 0)
+    # queue: split-tail pieces from the queue's piece pool (r6 default); queue_piece_blocks: the
+    # pieces as workgroups of their own after the persistent ones (r5, option piece_queue=0)
+    opt(gemm_tile=256, gemm_kernel=4, queue=0 if request.param == "static" else 1,
+        piece_queue=0 if request.param == "queue_piece_blocks" else 1)
     from vstyler import kernels
     return kernels
 
@@ -38,8 +41,11 @@ def queue_words_zero(K):
 
 # (M, N, K): 561 tiles (2 per workgroup + a 49-tile remainder pool), 833 tiles (3 per workgroup: one
 # queued tile per slot + a 65-tile remainder), 833 tiles at K = 4096 (a split tail: 768 main tiles
-# = 3 per workgroup, 65 tail tiles as 3 K pieces), 1537 tiles (6 per workgroup, 1 left over)
-SHAPES = [(8200, 4104, 1024), (12300, 4104, 1024), (12300, 4104, 4096), (24580, 4104, 1024)]
+# = 3 per workgroup, 65 tail tiles as 3 K pieces), 1537 tiles (6 per workgroup, 1 left over), the
+# Ulysses SP = 8 FFN-down (7410 rows, K 13 824: 580 tiles = 2 per workgroup + 68 tail tiles in K
+# pieces, which the persistent blocks take from the piece pool since r6)
+SHAPES = [(8200, 4104, 1024), (12300, 4104, 1024), (12300, 4104, 4096), (24580, 4104, 1024),
+          (7410, 5120, 13824)]
 
 
 @pytest.mark.parametrize("M,N,Kd", SHAPES)

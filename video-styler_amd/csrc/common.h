@@ -64,7 +64,7 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 
 // Path-selection options (include/vstyler.h VS_OPT_*; set by vs_set_option, attention.hip): one
 // process-wide table, product defaults; the library reads no environment variable.
-inline volatile int g_vs_opt[VS_OPT_COUNT] = {0, 4, 1, 1, 0, 16, 1, 1, 1, 2, 3, 1};
+inline volatile int g_vs_opt[VS_OPT_COUNT] = {0, 4, 1, 1, 0, 16, 1, 1, 1, 2, 3, 1, 1};
 inline int vs_opt(int id) { return g_vs_opt[id]; }
 
 // ---- work queues of the persistent kernels (gemm.hip W4Grab, attention_w4.hip): head words in a

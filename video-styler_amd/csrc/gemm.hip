@@ -837,12 +837,14 @@ static_assert(4 * W4_ROWB == 0x1080, "the 4w kernel's M0 step");
 // blocks of their own.  The blocks after those run the split-tail K pieces of the last tiles.
 // ---------------------------------------------------------------------------------------------
 constexpr int WQ_LINE = VS_Q_LINE;            // queue words 128 B apart (a line each, common.h)
-constexpr int WQ_BYTES = 10 * WQ_LINE * 4;    // 8 XCD heads, the remainder head, the exit count
+constexpr int WQ_BYTES = 11 * WQ_LINE * 4;    // 8 XCD heads, the remainder head, the piece head, the exit count
 struct W4Sched {
     unsigned* q;      // queue words (null: static lists)
     int npers;        // persistent blocks (a multiple of 8, or 0)
     int tp;           // tiles per slot of an XCD range
     int nrem;         // whole tiles past npers * tp
+    int npiece;       // split-tail pieces taken from the piece pool q[9] by the persistent blocks (r6;
+                      // 0: the pieces run as blocks of their own after the persistent ones)
 };
 struct W4Work {
     int first, second;  // the block's first two tile ids (-1: none)
@@ -888,6 +890,7 @@ struct W4Grab {
     int k = 2;                  // static list: position of the next tile
     bool local = true;          // the XCD's own queue may still hold tiles
     bool steal = true;          // another XCD's queue may
+    bool rem_dry = false;       // the remainder pool has run dry
     unsigned t0 = 0;
     __device__ __forceinline__ explicit W4Grab(const W4Sched& s) : sc(s) {}
     __device__ __forceinline__ void issue() {
@@ -925,17 +928,27 @@ struct W4Grab {
             if (t < qlen) return v * g8 * sc.tp + (int)t;
         }
         steal = false;
-        if (sc.nrem > 0) {
+        if (sc.nrem > 0 && !rem_dry) {
             unsigned u = 0;
             if (lane == 0) u = wq_add(sc.q + 8 * WQ_LINE);
             u = (unsigned)__builtin_amdgcn_readfirstlane((int)u);
             if (u < (unsigned)sc.nrem) return sc.npers * sc.tp + (int)u;
+            rem_dry = true;
+        }
+        // then the split-tail pieces (work ids nmain + p, see w4_item), so they run on the CUs that
+        // finish their whole tiles first instead of as blocks dispatched behind the persistent ones
+        if (sc.npiece > 0) {
+            unsigned u = 0;
+            if (lane == 0) u = wq_add(sc.q + 9 * WQ_LINE);
+            u = (unsigned)__builtin_amdgcn_readfirstlane((int)u);
+            if (u < (unsigned)sc.npiece) return sc.npers * sc.tp + sc.nrem + (int)u;
         }
         return -1;
     }
-    // after the block's last tile: the last persistent block to finish zeroes the queue words
+    // after the block's last tile: the last persistent block to finish (exit count q[10]) zeroes the
+    // queue words
     __device__ __forceinline__ void done(int tid) {
-        if (sc.q && (int)blockIdx.x < sc.npers && tid == 0) vs_queue_done(sc.q, 10, sc.npers);
+        if (sc.q && (int)blockIdx.x < sc.npers && tid == 0) vs_queue_done(sc.q, 11, sc.npers);
     }
 };
 
@@ -959,7 +972,13 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
 #if defined(__HIP_DEVICE_COMPILE__)     // (the AGPR asm operands are not host constraints)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const W4Work wk = w4_work(sc, K, nmain, ksplit, piece_k, 64);
-    const int nt = wk.nt;
+    // work ids (r6): id < nmain a whole tile, id >= nmain split-tail piece p = id - nmain (tile
+    // nmain + p / ksplit, K range p % ksplit) -- a persistent block takes pieces from the queue's
+    // piece pool after the whole tiles (W4Grab), a piece block of its own starts with its piece's id
+    const int kt_all = K / 64;
+    auto nt_of = [&](int id) {
+        return id < nmain ? kt_all : min(K - ((id - nmain) % ksplit) * piece_k, piece_k) / 64;
+    };
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1004,27 +1023,35 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     const char* abp = nullptr;
     const char* wbp = nullptr;
     int arec = 0, wrec = 0;
+    int dnt = 0;                    // K-tiles of the work the DMA cursor is in
     auto dma_tile = [&](int id) {
-        int tm, tn;
-        tile_of(id, ntm, ntn, ep.gm, tm, tn);
+        int tm, tn, tile = id, kb = 0;
+        if (id >= nmain) {
+            const int p = id - nmain;
+            tile = nmain + p / ksplit;
+            kb = (p % ksplit) * piece_k;
+        }
+        dnt = nt_of(id);
+        tile_of(tile, ntm, ntn, ep.gm, tm, tn);
         const int m0 = tm * 256, n0 = tn * 256;
-        abp = (const char*)(A + (long long)m0 * lda + wk.kb);
-        wbp = (const char*)(W + (long long)n0 * ldw + wk.kb);
+        abp = (const char*)(A + (long long)m0 * lda + kb);
+        wbp = (const char*)(W + (long long)n0 * ldw + kb);
         arec = __builtin_amdgcn_readfirstlane(rows_bytes(M - m0, ldab));
         wrec = __builtin_amdgcn_readfirstlane(rows_bytes(N - n0, ldwb));
     };
     // tiles: cur (computing), nxt (the next one, read from the LDS word in cur's first K-tile) and
     // dnext (where the DMA cursor goes when it leaves cur; -1: re-read)
-    int cur = wk.first, nxt = wk.second, dnext = wk.second;
+    int cur = wk.piece >= 0 ? nmain + (wk.first - nmain) * ksplit + wk.piece : wk.first;
+    int nxt = wk.second, dnext = wk.second;
     int dkt = 0;
     auto dma_advance = [&]() {
-        if (++dkt == nt) {
+        if (++dkt == dnt) {
             if (dnext >= 0) {
                 dkt = 0;
                 dma_tile(dnext);
                 dnext = -1;
             } else {
-                dkt = nt - 1;
+                dkt = dnt - 1;
             }
         }
     };
@@ -1211,6 +1238,7 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
 
 #pragma nounroll
     for (;;) {
+        const int nt = nt_of(cur);
         ktile(std::true_type{});
 #pragma nounroll
         for (int t = 1; t < nt; ++t) ktile(std::false_type{});
@@ -1219,17 +1247,18 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
         asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
 
         int tm, tn;
-        tile_of(cur, ntm, ntn, ep.gm, tm, tn);
+        const int cur_tile = cur < nmain ? cur : nmain + (cur - nmain) / ksplit;
+        tile_of(cur_tile, ntm, ntn, ep.gm, tm, tn);
         const int m0 = tm * 256, n0 = tn * 256;
         // the tile after nxt: wave 0's queue atomic goes out under this epilogue
         if (nxt >= 0 && wave == 0) grab.issue();
         // output: acc[i][j][e] = C[m][n], m = m0 + 128 wm + 16 i + (lane & 15), n = n0 + 128 wn + 16 j + 4 (lane >> 4) + e
-        if (wk.piece >= 0) {
+        if (cur >= nmain) {
             // fp32 partial tile through one buffer resource: a per-lane offset, the row block i in
             // soffset and the column block j in the immediate (64 precomputed 64-bit addresses,
             // hoisted out of the tile loop by the compiler, were spilled)
             const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-                part + ((long long)(cur - nmain) * ksplit + wk.piece) * 256 * 256, 0, 256 * 256 * 4, 0x00020000);
+                part + (long long)(cur - nmain) * 256 * 256, 0, 256 * 256 * 4, 0x00020000);
             const int vo = ((128 * wm + (lane & 15)) * 256 + 128 * wn + 4 * (lane >> 4)) * 4;
 #pragma unroll
             for (int i = 0; i < 8; ++i)
@@ -1936,6 +1965,29 @@ KSplit plan_ksplit(int ntiles, int nh, int cus, int step = 64) {
     return p;
 }
 
+// r6, with the piece pool (VS_OPT_PIECE_QUEUE): a GEMM of 1-3 whole rounds also keeps 1/16 of every
+// round's capacity as K pieces.  Under the Ulysses overlap RCCL's all-to-all kernels hold some CUs;
+// with exactly R rounds of whole tiles the tiles those CUs cannot take form an extra round of WHOLE
+// tiles on the others (the SP = 8 FFN-down: 580 tiles = 2 rounds + 68, 1.17x its unheld time with
+// 16 CUs held), while pieces of a quarter tile spread over every CU that is free.  Larger grids
+// (>= 4 rounds) balance through the queues alone (profiles/r5/cu_hold_s5.log).
+KSplit plan_ksplit_held(int ntiles, int nh, int cus, int step) {
+    KSplit p = plan_ksplit(ntiles, nh, cus, step);
+    const int R = cus > 0 ? ntiles / cus : 0;
+    if (R < 1 || R > 3 || cus < 16) return p;
+    const int tail = ntiles % cus + R * (cus / 16);
+    int f = 0;
+    for (int c = 4; c >= 2 && !f; --c)
+        if (tail * c <= MAX_SPLIT_PIECES && nh * step / c >= 512) f = c;
+    if (!f) return p;
+    const int piece_h = (nh + f - 1) / f;
+    p.ntail = tail;
+    p.nmain = ntiles - tail;
+    p.piece_k = piece_h * step;
+    p.ksplit = (nh + piece_h - 1) / piece_h;
+    return p;
+}
+
 // Routing (r5): every GEMM of the path runs on the kernels of this file.  r1-r4 sent the plain-bias
 // q|k|v / cross-q projections, the GELU FFN-up and the context GEMMs at SP = 1 to a private copy of
 // ROCm's hipBLASLt (+ a separate epilogue pass), which beat the hand-written kernels there (r4: q|k|v
@@ -1954,8 +2006,10 @@ static bool use_4w() { return vs_opt(VS_OPT_GEMM_KERNEL) == 4; }
 // every CU and a tile has >= 3 K-tiles (the tile-id hand-off, see the schedule's comment), fed by the
 // XCD tile queues when the stream has a queue workspace (kind 5) bound (VS_OPT_QUEUE 0: the
 // static lists)
-static W4Sched w4_sched(int nmain, int nt, hipStream_t stream) {
-    W4Sched s{nullptr, 0, 0, 0};
+// npiece: the launch's split-tail pieces, taken by the persistent blocks from the queue's piece pool
+// after the whole tiles (the bf16 kernel, r6); 0 (the fp8 kernel, or no queue): blocks of their own
+static W4Sched w4_sched(int nmain, int nt, hipStream_t stream, int npiece = 0) {
+    W4Sched s{nullptr, 0, 0, 0, 0};
     const int cus = vs_cus_for_split(false);
     if (cus >= 8 && cus % 8 == 0 && nmain >= cus && nt >= 3) {
         s.npers = cus;
@@ -1963,10 +2017,11 @@ static W4Sched w4_sched(int nmain, int nt, hipStream_t stream) {
     }
     s.nrem = nmain - s.npers * s.tp;
     if (s.npers && vs_opt(VS_OPT_QUEUE)) s.q = (unsigned*)vs_split_workspace(5, WQ_BYTES, stream);
+    if (s.q) s.npiece = npiece;
     return s;
 }
 static unsigned w4_grid(const W4Sched& s, const KSplit& sp) {
-    return (unsigned)(s.npers + (s.q ? 0 : s.nrem) + sp.ntail * sp.ksplit);
+    return (unsigned)(s.npers + (s.q ? 0 : s.nrem) + (s.npiece ? 0 : sp.ntail * sp.ksplit));
 }
 
 static int fill_epi(Epi& ep, int epilogue, const vs_epilogue* epi, int m, int n) {
@@ -2043,6 +2098,18 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
             part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
             if (!part) sp = KSplit{tm * tn, 0, 1, 0};
         }
+        if (k2 == 0 && wide && use_4w() && vs_opt(VS_OPT_QUEUE) && vs_opt(VS_OPT_PIECE_QUEUE) &&
+            vs_opt(VS_OPT_GEMM_SPLIT)) {
+            const KSplit held = plan_ksplit_held(tm * tn, k / 64, vs_cus_for_split(false), 64);
+            if (held.ntail > sp.ntail) {
+                float* p2 = vs_split_workspace(1, (size_t)held.ntail * held.ksplit * BT * BT * sizeof(float),
+                                               (hipStream_t)stream);
+                if (p2) {
+                    sp = held;
+                    part = p2;
+                }
+            }
+        }
         if (k2 == 0 && wide && use_4w()) {
             using K4 = void (*)(const bf16_t*, long long, const bf16_t*, long long, bf16_t*, long long, int, int, int,
                                 Epi, int, int, int, int, int, float*, W4Sched);
@@ -2057,7 +2124,8 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
                 attr4 = true;
             }
             const K4 kf = kern4[(ep.mode == VS_EPI_GATE_RES && ep.hint) ? 5 : ep.mode];
-            const W4Sched sc = w4_sched(sp.nmain, k / 64, (hipStream_t)stream);
+            const W4Sched sc = w4_sched(sp.nmain, k / 64, (hipStream_t)stream,
+                                        vs_opt(VS_OPT_PIECE_QUEUE) ? sp.ntail * sp.ksplit : 0);
             hipLaunchKernelGGL(kf, dim3(w4_grid(sc, sp)), dim3(256), W4_LDS + 16,
                                (hipStream_t)stream, (const bf16_t*)a, lda, (const bf16_t*)w, ldw, (bf16_t*)c, ldc, m,
                                n, k, ep, tm, tn, sp.nmain, sp.ksplit, sp.piece_k, part, sc);

@@ -13,7 +13,7 @@ VS_EPI_BIAS, VS_EPI_GELU, VS_EPI_SILU, VS_EPI_GATE_RES, VS_EPI_RES = range(5)
 # path-selection options (include/vstyler.h VS_OPT_*): name -> id
 OPTIONS = {"gemm_tile": 0, "gemm_kernel": 1, "gemm_split": 2, "queue": 3, "attn_impl": 4, "attn_mfma": 5,
            "attn_nc": 6, "attn_split": 7, "attn_persist": 8, "vae_pxb": 9, "vae_pre": 10,
-           "vae_halo": 11}
+           "vae_halo": 11, "piece_queue": 12}
 
 
 class VsEpilogue(ctypes.Structure):
