@@ -50,7 +50,7 @@ int vs_abi_version(void);
 #define VS_OPT_VAE_PXB 9       /* 2 (default) / 1: 128-pixel blocks per wave of the VAE conv            */
 #define VS_OPT_VAE_PRE 10      /* 3 (default) / 2 / 1: register stages of the VAE conv's gathers        */
 #define VS_OPT_VAE_HALO 11     /* 1 (default): the VAE's 3x3(x3) stride-1 convs on the patch-resident kernel; 0: per-tap gathers */
-#define VS_OPT_PIECE_QUEUE 12  /* 1 (default, r6): the 4-wave bf16 GEMM's split-tail pieces taken by its persistent blocks from the queue after the whole tiles; 0: blocks of their own */
+#define VS_OPT_PIECE_QUEUE 12  /* 1 (default, r6): the 4-wave bf16 GEMM's split-tail pieces taken by its persistent blocks from the queue after the whole tiles; 0: blocks of their own; 2: 1 + grids of 1-3 rounds keep 1/16 of each round as pieces (held-CU reserve) */
 #define VS_OPT_COUNT 13
 int vs_set_option(int id, int value);
 int vs_get_option(int id);

@@ -14,6 +14,8 @@ from vstyler import model_fn_wan_video
 from vstyler.models import VaceWanModel, WanModel, init_random_
 from vstyler.usp import UlyssesGroup, _Done
 from vstyler import kernels as K
+from vstyler import _lib
+from vstyler.options import HOST_DEFAULTS, set_host_option
 
 lib = ctypes.CDLL(os.path.join(os.path.dirname(__file__), "fakecomm", "libfakecomm.so"))
 lib.fake_comm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
@@ -70,14 +72,18 @@ Gs = [int(x) for x in os.environ.get("SPC_G", "0,16,64").split(",")]
 pers = os.environ.get("SPC_PERSIST", "1,0").split(",")
 queues = os.environ.get("SPC_QUEUE", "1").split(",")
 ovs = [o == "1" for o in os.environ.get("SPC_OVERLAP", "1,0").split(",")]
-ev = os.environ.get("SPC_ENV", "")          # "VAR=a,b": one more interleaved dimension
+ev = os.environ.get("SPC_ENV", "")          # "OPT=a,b": one more interleaved dimension (an option or env var)
 evar, evals = ev.split("=") if ev else ("", "-")
 cases = [(G, pz, ov, e, qu) for G in Gs for pz in pers for ov in ovs for e in evals.split(",") for qu in queues]
 res = {c: [] for c in cases}
 for rnd in range(3):
     for c in cases:
         G, pz, ov, e, qu = c
-        if evar:
+        if evar in _lib.OPTIONS:          # a libvstyler option (e.g. piece_queue)
+            K.set_option(evar, int(e))
+        elif evar in HOST_DEFAULTS:
+            set_host_option(evar, e)
+        elif evar:
             os.environ[evar] = e
         K.set_option("attn_persist", 1 if pz == "1" else 0)
         K.set_option("queue", int(qu))

@@ -185,7 +185,8 @@ def test_options_table():
     with K.options(gemm_kernel=8, queue=0, attn_mfma=32):
         assert (K.get_option("gemm_kernel"), K.get_option("queue"), K.get_option("attn_mfma")) == (8, 0, 32)
     assert (K.get_option("gemm_kernel"), K.get_option("queue"), K.get_option("attn_mfma")) == (4, 1, 16)
-    for name, bad in (("gemm_tile", 64), ("gemm_kernel", 5), ("attn_mfma", 8), ("vae_pre", 4), ("gemm_split", 2)):
+    for name, bad in (("gemm_tile", 64), ("gemm_kernel", 5), ("attn_mfma", 8), ("vae_pre", 4), ("gemm_split", 2),
+                      ("piece_queue", 3)):
         with pytest.raises(ValueError):
             K.set_option(name, bad)
     assert lib.vs_set_option(99, 0) < 0 and lib.vs_get_option(-1) < 0

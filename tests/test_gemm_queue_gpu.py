@@ -23,12 +23,13 @@ def ints(*shape, g, lo=-3, hi=4):
     return torch.randint(lo, hi, shape, generator=g, device="cuda").to(BF16)
 
 
-@pytest.fixture(params=["queue", "queue_piece_blocks", "static"])
+@pytest.fixture(params=["queue", "queue_piece_blocks", "queue_held_reserve", "static"])
 def sched(opt, request):
     # queue: split-tail pieces from the queue's piece pool (r6 default); queue_piece_blocks: the
-    # pieces as workgroups of their own after the persistent ones (r5, option piece_queue=0)
+    # pieces as workgroups of their own after the persistent ones (r5, option piece_queue=0);
+    # queue_held_reserve: the pool + 1-3 round grids keeping 1/16 of each round as pieces (2)
     opt(gemm_tile=256, gemm_kernel=4, queue=0 if request.param == "static" else 1,
-        piece_queue=0 if request.param == "queue_piece_blocks" else 1)
+        piece_queue={"queue_piece_blocks": 0, "queue_held_reserve": 2}.get(request.param, 1))
     from vstyler import kernels
     return kernels
 

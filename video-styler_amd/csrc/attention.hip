@@ -1117,6 +1117,7 @@ extern "C" int vs_set_option(int id, int value) {
         case VS_OPT_ATTN_MFMA: ok = value == 16 || value == 32; break;
         case VS_OPT_VAE_PXB: ok = value == 1 || value == 2; break;
         case VS_OPT_VAE_PRE: ok = value >= 1 && value <= 3; break;
+        case VS_OPT_PIECE_QUEUE: ok = value >= 0 && value <= 2; break;
         default: ok = value == 0 || value == 1; break;           // the on / off options
     }
     if (!ok) return -VS_E_INVALID;

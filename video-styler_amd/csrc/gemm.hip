@@ -2098,7 +2098,7 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
             part = vs_split_workspace(1, (size_t)sp.ntail * sp.ksplit * BT * BT * sizeof(float), (hipStream_t)stream);
             if (!part) sp = KSplit{tm * tn, 0, 1, 0};
         }
-        if (k2 == 0 && wide && use_4w() && vs_opt(VS_OPT_QUEUE) && vs_opt(VS_OPT_PIECE_QUEUE) &&
+        if (k2 == 0 && wide && use_4w() && vs_opt(VS_OPT_QUEUE) && vs_opt(VS_OPT_PIECE_QUEUE) == 2 &&
             vs_opt(VS_OPT_GEMM_SPLIT)) {
             const KSplit held = plan_ksplit_held(tm * tn, k / 64, vs_cus_for_split(false), 64);
             if (held.ntail > sp.ntail) {
