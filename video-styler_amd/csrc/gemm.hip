@@ -1083,8 +1083,12 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
         else asm volatile("s_add_u32 m0, m0, 0x1080" ::: "memory");   // (see m0_step_note)
     };
     auto dma_go = [&](int d) {
+#ifdef VS_W4_DIAG_NODMA     // diagnostic build only (scripts/build_diag.sh): no operand DMA, garbage results
+        (void)d;
+#else
         if (d < 8) asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" :: "v"(vow[d]), "s"(rsw) : "memory");
         else asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" :: "v"(voa[d - 8]), "s"(rsa) : "memory");
+#endif
     };
     auto dma_now = [&](int d) {                     // outside the pipelined body: M0, nop, load
         asm volatile("s_mov_b32 m0, %0" :: "s"(dma_lds(d)) : "m0");
@@ -1099,7 +1103,11 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_tn_4w(
     int atog = abase ^ (abase + W4_OPB), wtog = wbase ^ (wbase + W4_OPB);
     asm volatile("" : "+v"(abase), "+v"(wbase), "+v"(atog), "+v"(wtog));
     auto frag = [&](int addr) {
+#ifdef VS_W4_DIAG_NOREAD    // diagnostic build only: no fragment reads (the MFMAs see constant operands)
+        return bf16x8_t{(__bf16)(float)(addr & 1), 0, 0, 0, 0, 0, 0, 0};
+#else
         return *reinterpret_cast<const LDS_AS bf16x8_t*>((const LDS_AS char*)(uintptr_t)(unsigned)addr);
+#endif
     };
     bf16x8_t fa0[8], fa1[8], fw0[8], fw1[8];
     auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
