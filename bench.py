@@ -123,7 +123,7 @@ def cpu_baseline(m, S, rows=2048):
                       f"({nm} x main + {nv} x VACE) x {S}/{rows} tokens x 2 CFG = {sec_per_step:.0f} s/step"}
 
 
-def pmc_traffic(path=os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r5", "pmc_attn_w4_r5",
+def pmc_traffic(path=os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r6", "pmc_attn_w4_r6b",
                                    "summary.txt")):
     """HBM bytes per self-attention launch from the committed rocprofv3 --pmc measurement of the same
     kernel at the same shape (scripts/pmc.sh attn: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE,
@@ -487,7 +487,7 @@ def main():
                      "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                      # the committed PMC measurement is of the default workload (14B 832x480x73)
                      "traffic": pmc_traffic() if world == 1 and default_shape else None,
-                     "traffic_source": "rocprofv3 --pmc FETCH_SIZE*2+WRITE_SIZE per launch, profiles/r5/pmc_attn_w4_r5 "
+                     "traffic_source": "rocprofv3 --pmc FETCH_SIZE*2+WRITE_SIZE per launch, profiles/r6/pmc_attn_w4_r6b "
                                        "(same kernel, same shape; algorithmic Q+K+V+O = 2.43e9 B)",
                      "avg_launch_ms": round(attn_ms, 3), "launches": attn_n,
                      "timing": "HIP events on the launch stream, " + ("one instrumented eager step after the "
