@@ -47,7 +47,7 @@ def get_default_group():
     world size, Ulysses inside each half; "auto": at world size 2 only, where Ulysses would send half of
     every q|k|v over one xGMI link per block while CFG parallelism needs one 2-sample velocity
     exchange per step).  CfgParallel stays opt-in until a multi-GPU RCCL run has shown its output
-    bit-identical to the single-GPU forward (the tests cover it with host-staged collectives)."""
+    equal to the single-GPU forward (the tests cover it with host-staged collectives)."""
     global _DEFAULT
     if _DEFAULT is None and dist.is_initialized():
         mode = host_option("cfg_parallel")
