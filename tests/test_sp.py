@@ -164,6 +164,35 @@ def _gpu_worker(rank, world, port, q, cfg_name="tiny"):
         if rank == 0:           # the SP output against the oracle itself, not only against SP = 1
             res["oracle"], res["oracle_msg"] = _oracle_check(par.cpu(), cfg, W, lat, t, (cp, cn), vc,
                                                              f"Ulysses SP={world} {cfg_name}")
+        if world >= 4:
+            # the denoising loop itself under SP (wan_video_new.py:515-542: scheduler, CFG 5, Euler over
+            # 2 steps; eager steps -- host-staged collectives are not capturable) == the single-GPU loop
+            # (hipGraph replay), and the final latents within the oracle's floor (O.denoise)
+            from vstyler import WanVideoPipeline
+            outs = []
+            for plan in (None, HostStagedUlysses()):
+                pipe = WanVideoPipeline(device="cuda")
+                pipe.dit, pipe.vace = dit, vace
+                pipe.use_unified_sequence_parallel, pipe.sp_group = plan is not None, plan
+                outs.append(pipe.denoise(lat.cuda(), cp.cuda(), cn.cuda(), vc.cuda(), num_inference_steps=2).cpu())
+            res["denoise_same"] = torch.equal(outs[0], outs[1])
+            if rank == 0:
+                from oracle import wan_oracle as O2
+                from gpu_util import err
+
+                def run():
+                    return O2.denoise(W, cfg, lat, cp, cn, vc, num_inference_steps=2)
+                ref32 = run()
+                O2.ACC_DTYPE = torch.float64
+                try:
+                    ref64 = run()
+                finally:
+                    O2.ACC_DTYPE = torch.float32
+                mx, rl = err(outs[1], ref32)
+                fmx, frl = err(ref32, ref64)
+                res["denoise_oracle"] = mx <= NOISE_X * fmx + 1e-3 and rl <= NOISE_X * frl + 1e-4
+                res["denoise_msg"] = (f"SP={world} {cfg_name} 2-step denoise: max-abs {mx:.4g} rel-L2 {rl:.4g} "
+                                      f"(floor {fmx:.4g} / {frl:.4g})")
         q.put((rank, res))
     except Exception:  # pragma: no cover
         import traceback
@@ -181,8 +210,10 @@ def test_ulysses_model_on_one_gpu_vs_sp1_and_oracle(world, cfg_name):
     for rank, r in res:
         assert isinstance(r, dict), res
         assert r["overlap1"] is True and r["overlap0"] is True and r["nocfg"] is True, (rank, r)
-    print(res[0][1]["oracle_msg"])
+        assert r.get("denoise_same", True) is True, (rank, r)
+    print(res[0][1]["oracle_msg"], res[0][1].get("denoise_msg", ""))
     assert res[0][1]["oracle"] is True, res[0][1]["oracle_msg"]
+    assert res[0][1].get("denoise_oracle", True) is True, res[0][1]["denoise_msg"]
 
 
 def _gpu14b_worker(rank, world, port, q):
