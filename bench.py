@@ -342,6 +342,7 @@ def main():
     from vstyler.flow_match import FlowMatchScheduler
     from vstyler.pipeline import DenoiseStepper
     from vstyler.models import TIMER, VaceWanModel, WanModel, init_random_
+    from vstyler.options import host_option
 
     m = MODELS[args.model]
     T = (args.frames - 1) // 4 + 1
@@ -475,6 +476,7 @@ def main():
                    "model": f"Wan2.1-VACE-{args.model}", "global_batch": 1, "seq_len": S,
                    "latent_shape": [1, 16, T, Hl, Wl], "parallelism": _parallelism(sp, world),
                    "lora": "merged (zero runtime cost, as the reference's GeneralLoRALoader)",
+                   "cfg_shared_prefix": bool(host_option("cfg_prefix")),
                    "step_exec": "hipGraph replay" if use_graph else "eager launches",
                    "sampler": ("UniPC bh2 order 2, cfg 1.2, shift 2.0, SLG block 2 @ 0.2-0.7, VACE 0.975"
                                if args.config == "fp8" else "flow-match Euler, cfg 5.0, shift 5.0")},

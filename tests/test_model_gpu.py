@@ -74,6 +74,27 @@ def test_model_fn_batched_cfg_equals_two_calls(tiny):
     assert torch.equal(both[0:1], p) and torch.equal(both[1:2], n)
 
 
+def test_cfg_shared_prefix_bit_identical(tiny):
+    """The first DiT / VACE block's phases 1-3 computed once for both CFG samples (host option
+    cfg_prefix, default on) give the batch-2 forward of the option off bit for bit, and the forward of
+    per-sample latents (no shared prefix possible) agrees with both."""
+    from vstyler import model_fn_wan_video
+    from vstyler.options import host_options
+    cfg, W, dit, vace = tiny
+    lat, cp, cn, vc = O.synthetic_inputs(cfg, 5, 128, 128)
+    t = torch.tensor([777.0]).to(BF16).cuda()
+    ctx = torch.cat([cp, cn]).cuda()
+    outs = []
+    for on in (1, 0):
+        with host_options(cfg_prefix=on):
+            outs.append(model_fn_wan_video(dit, vace=vace, latents=lat.cuda(), timestep=t, context=ctx,
+                                           vace_context=vc.cuda()).clone())
+    lat2 = torch.cat([lat, lat]).cuda()          # batch-2 latents: the shared-prefix test cannot apply
+    outs.append(model_fn_wan_video(dit, vace=vace, latents=lat2, timestep=t, context=ctx,
+                                   vace_context=torch.cat([vc, vc]).cuda()))
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
 def test_denoise_tiny_vs_golden(tiny):
     from vstyler import WanVideoPipeline
     cfg, W, dit, vace = tiny

@@ -333,7 +333,7 @@ class DiTBlock(nn.Module):
         self.ffn = Sequential3(Linear(dim, ffn_dim, device=device), Linear(ffn_dim, dim, device=device))
         self.modulation = _param(1, 6, dim, device=device)
 
-    def forward(self, x, t_mod, rc, hint=None, hint_scale=1.0, only_batch=None, nxt=None):
+    def forward(self, x, t_mod, rc, hint=None, hint_scale=1.0, only_batch=None, nxt=None, shared_prefix=False):
         """x: [B*S, D] updated in place.  t_mod: [B, 6, D].  hint: [B*S, D] added after the block.
         only_batch: run the block for that CFG sample only (skip-layer guidance leaves the others'
         rows untouched).  nxt: the module that consumes x next (a DiTBlock or the Head) when it runs
@@ -347,7 +347,14 @@ class DiTBlock(nn.Module):
         0's q|k|v all-to-all runs under sample 1's projections, sample 1's under sample 0's
         attention, sample 0's return exchange under sample 1's attention and sample 1's under sample
         0's o-proj; phase 4 then runs once on both samples' rows (GEMMs of 2S/p rows instead of two
-        of S/p: host option sp_merge_ffn=0 keeps it per sample)."""
+        of S/p: host option sp_merge_ffn=0 keeps it per sample).
+
+        shared_prefix (r6): the caller guarantees that every CFG sample's rows of x and of t_mod are
+        equal (the first DiT block and the first VACE block, when the latents, the timestep and the VACE
+        context are shared -- they differ only through the context, which phase 4 first reads), so
+        phases 1-3 run on sample 0's rows alone and their outputs (x after the gated o-proj, the LN3
+        rows) are copied to the other samples before phase 4 runs on all rows: the same per-row
+        arithmetic, bit-identical (tests/test_model_gpu.py), half the self-attention of those blocks."""
         B, S, D, ws = rc.batch, rc.seq, self.dim, rc.ws
         if rc.pre_mod is not None:          # the previous block already ran this one's LN1
             mod, ln1_done = rc.pre_mod, True
@@ -357,18 +364,21 @@ class DiTBlock(nn.Module):
             mod, ln1_done = ws.get(f"mod{rc.mod_slot}", (B, 6, D)), False
             K.mod_add(self.modulation.view(6, D), t_mod, mod, 6 * D, D)   # :218-219
         sp = rc.sp
+        shared = shared_prefix and B > 1 and only_batch is None and bool(host_option("cfg_prefix"))
         if only_batch is not None:
             assert not ln1_done, "a skip-layer-guidance block cannot start from a fused LN1"
             parts = [self._part(x, mod, rc, only_batch, 1, hint, f".{only_batch}")]
+        elif shared:
+            parts = [self._part(x, mod, rc, 0, 1, hint, ".0")]
         elif sp is not None and B > 1 and getattr(sp, "overlap", False):
             parts = [self._part(x, mod, rc, b, 1, hint, f".{b}") for b in range(B)]
         else:
             parts = [self._part(x, mod, rc, 0, B, hint, "")]
         for p in parts:
             p["ln1_done"] = ln1_done
-        # phase 4 on all rows at once (the overlapped SP micro-batches)
-        tail = self._part(x, mod, rc, 0, B, hint, "") if len(parts) > 1 and \
-            host_option("sp_merge_ffn") else None
+        # phase 4 on all rows at once (the overlapped SP micro-batches, the shared prefix)
+        tail = self._part(x, mod, rc, 0, B, hint, "") if shared or (len(parts) > 1 and
+                                                                    host_option("sp_merge_ffn")) else None
         # the fused FFN-down epilogue needs the consumer's modulation first (its own mod buffer)
         fuse = None
         if nxt is not None and only_batch is None and \
@@ -390,6 +400,11 @@ class DiTBlock(nn.Module):
             self._phase_o(p, rc, direct=tail is None)
             if tail is None:
                 self._phase_cross_ffn(p, rc, hint_scale, fuse)
+        if shared:                          # sample 0's phase 1-3 results are every sample's
+            xs = x.view(B, S, D)
+            hs = ws.get("h", (B * S, D)).view(B, S, D)
+            xs[1:].copy_(xs[0:1].expand(B - 1, S, D))
+            hs[1:].copy_(hs[0:1].expand(B - 1, S, D))
         if tail is not None:
             self._phase_cross_ffn(tail, rc, hint_scale, fuse)
         if fuse is not None:
@@ -627,9 +642,10 @@ class VaceWanModel(nn.Module):
         self.vace_patch_embedding = PatchEmbed(vace_in_dim, dim, device)
         self.dim = dim
 
-    def forward(self, x, vace_cols_out, t_mod, rc):
+    def forward(self, x, vace_cols_out, t_mod, rc, shared_prefix=False):
         """x: patch-embedded main tokens [B*S, D]; vace_cols_out: patch-embedded control tokens
-        [B*S, D] (overwritten, becomes c).  Returns the list of hint buffers [B*S, D]."""
+        [B*S, D] (overwritten, becomes c).  Returns the list of hint buffers [B*S, D].  shared_prefix:
+        every CFG sample's rows of x, of the control tokens and of t_mod are equal (DiTBlock)."""
         ws, D = rc.ws, self.dim
         M = rc.batch * rc.seq
         c = vace_cols_out
@@ -640,7 +656,8 @@ class VaceWanModel(nn.Module):
                 c0 = ws.get("vace_c", (M, D))
                 linear(blk.before_proj, c, c0, ws, epilogue=K.VS_EPI_RES, residual=x)
                 c = c0
-            blk(c, t_mod, rc, nxt=self.vace_blocks[n + 1] if n + 1 < nb else None)
+            blk(c, t_mod, rc, nxt=self.vace_blocks[n + 1] if n + 1 < nb else None,
+                shared_prefix=shared_prefix and n == 0)
             hint = ws.get(f"vace_hint{n}", (M, D))
             linear(blk.after_proj, c, hint, ws)
             hints.append(hint)

@@ -19,10 +19,14 @@ option), read once when the package is imported.
   fuse_ffn_ln     1      the next block's LN1 fused after the FFN-down epilogue (models)
   ws_poison       0      Workspace fills every fresh buffer with NaN (debugging stale reads)
   graph           1      hipGraph replay of the denoising step (pipeline.WanVideoPipeline.denoise)
+  cfg_prefix      1      the first DiT block's and the first VACE block's phases 1-3 (LN1, q|k|v,
+                         self-attention, o-proj, LN3) run once for both CFG samples when their rows are
+                         equal (shared latents / timestep / VACE context): bit-identical (DiTBlock)
 """
 HOST_DEFAULTS = {
     "sp_overlap": 1, "sp_comm": "torch", "sp_comm_stream": "side", "sp_graph": 0, "sp_rows": 1,
     "sp_merge_ffn": 1, "cfg_parallel": "0", "fuse_res_ln": 1, "fuse_ffn_ln": 1, "ws_poison": 0, "graph": 1,
+    "cfg_prefix": 1,
 }
 _CHOICES = {"sp_comm": ("torch", "native"), "sp_comm_stream": ("side", "caller"),
             "cfg_parallel": ("0", "1", "auto")}

@@ -78,6 +78,11 @@ def model_fn_wan_video(dit: WanModel, motion_controller=None, vace: VaceWanModel
     device = latents.device
     ws = _workspace(device)
     B, L = context.shape[0], context.shape[1]
+    # every CFG sample starts from the same rows when the latents, the timestep (and the VACE context)
+    # are shared (the cfg_merge broadcast below): the first blocks' self-attention halves are then
+    # computed once for all samples (DiTBlock shared_prefix)
+    shared = B > 1 and latents.shape[0] == 1 and timestep.numel() == 1
+    shared_vace = shared and vace_context is not None and vace_context.shape[0] == 1
     if latents.shape[0] != B:
         latents = latents.expand(B, *latents.shape[1:])
     latents = latents.to(BF16).contiguous()
@@ -118,7 +123,7 @@ def model_fn_wan_video(dit: WanModel, motion_controller=None, vace: VaceWanModel
         if tea_cache is not None:
             tea_cache.begin(x)
         rc.t_emb = t
-        hints = vace(x, vace_x, t_mod, rc) if vace_x is not None else None
+        hints = vace(x, vace_x, t_mod, rc, shared_prefix=shared_vace) if vace_x is not None else None
         vmap = vace.vace_layers_mapping if hints is not None else {}
         nblk = len(dit.blocks)
         # a batch-1 forward of CFG sample 1 (CFG-parallel rank) skips the slg blocks outright
@@ -134,7 +139,8 @@ def model_fn_wan_video(dit: WanModel, motion_controller=None, vace: VaceWanModel
                 nxt = None if (slg_here and i + 1 in slg_blocks) else dit.blocks[i + 1]
             else:
                 nxt = None if tea_cache is not None else dit.head
-            blk(x, t_mod, rc, hint=hint, hint_scale=float(vace_scale), only_batch=0 if skip else None, nxt=nxt)
+            blk(x, t_mod, rc, hint=hint, hint_scale=float(vace_scale), only_batch=0 if skip else None, nxt=nxt,
+                shared_prefix=shared and i == 0)
         if tea_cache is not None:
             tea_cache.store(x)                                  # :1455-1456
     out = dit.head(x, t, rc)
