@@ -353,8 +353,9 @@ class DiTBlock(nn.Module):
         equal (the first DiT block and the first VACE block, when the latents, the timestep and the VACE
         context are shared -- they differ only through the context, which phase 4 first reads), so
         phases 1-3 run on sample 0's rows alone and their outputs (x after the gated o-proj, the LN3
-        rows) are copied to the other samples before phase 4 runs on all rows: the same per-row
-        arithmetic, bit-identical (tests/test_model_gpu.py), half the self-attention of those blocks."""
+        rows) are copied to the other samples before phase 4 runs on all rows -- its cross-attention
+        query too comes from sample 0's rows alone: the same per-row arithmetic, bit-identical
+        (tests/test_model_gpu.py), half the self-attention of those blocks."""
         B, S, D, ws = rc.batch, rc.seq, self.dim, rc.ws
         if rc.pre_mod is not None:          # the previous block already ran this one's LN1
             mod, ln1_done = rc.pre_mod, True
@@ -400,11 +401,10 @@ class DiTBlock(nn.Module):
             self._phase_o(p, rc, direct=tail is None)
             if tail is None:
                 self._phase_cross_ffn(p, rc, hint_scale, fuse)
-        if shared:                          # sample 0's phase 1-3 results are every sample's
-            xs = x.view(B, S, D)
-            hs = ws.get("h", (B * S, D)).view(B, S, D)
+        if shared:                          # sample 0's phase 1-3 results are every sample's: x, and the
+            xs = x.view(B, S, D)            # cross-attention query (from sample 0's LN3 rows in h)
             xs[1:].copy_(xs[0:1].expand(B - 1, S, D))
-            hs[1:].copy_(hs[0:1].expand(B - 1, S, D))
+            tail["shared_q"] = True
         if tail is not None:
             self._phase_cross_ffn(tail, rc, hint_scale, fuse)
         if fuse is not None:
@@ -480,8 +480,13 @@ class DiTBlock(nn.Module):
         x, mod, h, q, o, nb, M = p["x"], p["mod"], p["h"], p["q"], p["o"], p["nb"], p["M"]
         ca = self.cross_attn
         L = rc.ctx_len
-        linear(ca.q, p.pop("h3", h), q, ws)
-        K.rmsnorm_rope(q, ca.norm_q.weight, eps)
+        if p.get("shared_q"):               # equal rows per sample (shared prefix): one sample's query
+            linear(ca.q, h[:S], q[:S], ws)
+            K.rmsnorm_rope(q[:S], ca.norm_q.weight, eps)
+            q.view(nb, S, D)[1:].copy_(q[:S].unsqueeze(0).expand(nb - 1, S, D))
+        else:
+            linear(ca.q, p.pop("h3", h), q, ws)
+            K.rmsnorm_rope(q, ca.norm_q.weight, eps)
         kv = fused_linear(ca, p["ctx"], ws, "kvc" + p["tag"])
         if kv is not None:
             kc, vc = kv[:, :D], kv[:, D:]
@@ -651,10 +656,13 @@ class VaceWanModel(nn.Module):
         c = vace_cols_out
         hints = []
         nb = len(self.vace_blocks)
+        # with a shared prefix block 0 reads sample 0's rows of c0 alone and overwrites the others
+        # after its self-attention half, so before_proj runs on those rows only
+        rows = rc.seq if shared_prefix and rc.batch > 1 and host_option("cfg_prefix") else M
         for n, blk in enumerate(self.vace_blocks):
             if n == 0:
                 c0 = ws.get("vace_c", (M, D))
-                linear(blk.before_proj, c, c0, ws, epilogue=K.VS_EPI_RES, residual=x)
+                linear(blk.before_proj, c[:rows], c0[:rows], ws, epilogue=K.VS_EPI_RES, residual=x[:rows])
                 c = c0
             blk(c, t_mod, rc, nxt=self.vace_blocks[n + 1] if n + 1 < nb else None,
                 shared_prefix=shared_prefix and n == 0)
