@@ -162,8 +162,9 @@ int vs_split_workspace_bind(int kind, void* ptr, long long bytes, void* stream);
 
 /*
  * Row kernels (vs_layernorm_modulate, _fp8, vs_residual_layernorm, vs_rmsnorm_rope): one 128-thread
- * block per row, 5 chunks of 8 elements per thread, so dim % 8 == 0 and dim <= 5120 (every Wan
- * width: 1536 / 5120); wider rows return VS_E_INVALID (r1-r4 accepted up to 6144).
+ * block per row, 5 chunks of 8 elements per thread up to dim 5120 (every Wan width: 1536 / 5120),
+ * 8 chunks up to 8192 (r6; r1-r4 accepted up to 6144, r5 only 5120); dim % 8 == 0 and dim <= 8192,
+ * VS_E_INVALID otherwise.
  *
  * out = bf16(LN(x)) [affine: weight/bias] then, if shift/scale given, modulate:
  * bf16(bf16(n * bf16(1+scale)) + shift) with shift/scale rows selected per batch.

@@ -36,7 +36,7 @@ def test_quant_fp8_rows_bit_exact(cols):
     assert torch.equal(x8.cpu(), ref8.view(torch.uint8))
 
 
-@pytest.mark.parametrize("D", [1536, 5120])
+@pytest.mark.parametrize("D", [1536, 5120, 6144])
 @pytest.mark.parametrize("mode", ["modulate", "affine"])
 def test_layernorm_modulate_fp8_equals_two_passes(D, mode):
     """vs_layernorm_modulate_fp8 == vs_layernorm_modulate then vs_quant_fp8_rows, every byte and scale

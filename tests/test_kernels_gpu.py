@@ -447,8 +447,9 @@ def test_attention_strided_views(attn_mfma, K):
     assert err(out.view(B, S, D), ref)[1] < 1e-2
 
 
-def test_layernorm_modulate(K):
-    B, S, D = 2, 37, 1536
+@pytest.mark.parametrize("D", [1536, 5120, 6144, 8192])    # > 5120: the 8-chunk wide-row instantiation
+def test_layernorm_modulate(K, D):
+    B, S = 2, 37
     x = rnd(B * S, D, scale=2.0, seed=50)
     mod = rnd(B, 6, D, scale=0.3, seed=51)
     ref = torch.cat([O.modulate(O.layer_norm(x[b * S:(b + 1) * S]), mod[b, 0], mod[b, 1]) for b in range(B)])
@@ -491,9 +492,10 @@ def test_residual_layernorm_matches_two_passes(K, mode):
     assert torch.equal(h1, h2)
 
 
-def test_rmsnorm_rope(K):
-    B, grid, H = 2, (3, 4, 5), 2
-    S, D = 60, 256
+@pytest.mark.parametrize("H", [2, 48])     # D = 256; 6144 runs on the 8-chunk wide-row instantiation
+def test_rmsnorm_rope(K, H):
+    B, grid = 2, (3, 4, 5)
+    S, D = 60, 128 * H
     x = rnd(B * S, D, scale=3.0, seed=60)
     w = (1 + 0.1 * torch.randn(D, generator=torch.Generator().manual_seed(61))).to(BF16)
     freqs = O.rope_freqs(*grid)

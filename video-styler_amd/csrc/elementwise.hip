@@ -9,7 +9,8 @@ namespace {
 #define VS_RT 128
 #define VS_MAXCH 5
 #endif
-// threads per row-kernel block / 8-element chunks per thread (dim <= RT * MAXCH * 8 = 5120).  r5:
+// threads per row-kernel block / 8-element chunks per thread (dim <= RT * MAXCH * 8 = 5120; wider rows
+// up to 8192 on an 8-chunk instantiation, ROW_MAX).  r5:
 // 128 threads x 5 chunks instead of 256 x 3 -- LayerNorm+modulate at 59 280 x 5120 309-317 -> 279-289 us
 // (the 256-thread rows split 640 chunks 3 / 2 unevenly); 320 and 640 threads were slower
 // (profiles/r5/rowkernel_threads_ab_s41.log)
@@ -62,7 +63,7 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 // quantisation (layers.py:115-151, vs_quant_fp8_rows): per-row s = max(bf16(max|h| / 448), 1) and
 // e4m3(h / (s + 1e-8)) of the bf16 values h the plain kernel would store -- bit-identical to the two
 // passes, without the bf16 write and the quantisation's read (the row's consumer is an fp8 GEMM).
-template <bool Q8>
+template <bool Q8, int MC = MAXCH>
 __global__ __launch_bounds__(RT) void ln_modulate_kernel(
     const bf16_t* __restrict__ x, long long ldx, bf16_t* __restrict__ out, long long ldo, int dim,
     int rpb, const bf16_t* __restrict__ shift, const bf16_t* __restrict__ scale, long long mbs,
@@ -72,10 +73,10 @@ __global__ __launch_bounds__(RT) void ln_modulate_kernel(
     const long long row = blockIdx.x;
     const int nch = dim >> 3;
     const bf16_t* xr = x + row * ldx;
-    float v[MAXCH][8];
+    float v[MC][8];
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < MAXCH; ++c) {
+    for (int c = 0; c < MC; ++c) {
         const int ch = threadIdx.x + c * RT;
         if (ch < nch) {
             unpack8(*reinterpret_cast<const u32x4_t*>(xr + ch * 8), v[c]);
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(RT) void ln_modulate_kernel(
     const float mean = block_sum(s, red) / dim;
     float q = 0.f;
 #pragma unroll
-    for (int c = 0; c < MAXCH; ++c) {
+    for (int c = 0; c < MC; ++c) {
         const int ch = threadIdx.x + c * RT;
         if (ch < nch) {
 #pragma unroll
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(RT) void ln_modulate_kernel(
     const long long bidx = row / rpb;
     bf16_t* orow = out + row * ldo;
 #pragma unroll
-    for (int c = 0; c < MAXCH; ++c) {
+    for (int c = 0; c < MC; ++c) {
         const int ch = threadIdx.x + c * RT;
         if (ch >= nch) continue;
         float y[8];
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(RT) void ln_modulate_kernel(
     if constexpr (Q8) {
         float mx = 0.f;
 #pragma unroll
-        for (int c = 0; c < MAXCH; ++c)
+        for (int c = 0; c < MC; ++c)
             if ((int)threadIdx.x + c * RT < nch)
 #pragma unroll
                 for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf(v[c][e]));
@@ -140,7 +141,7 @@ __global__ __launch_bounds__(RT) void ln_modulate_kernel(
         if (threadIdx.x == 0) qscale[row] = s8;
         uint8_t* yr = x8 + row * ld8;
 #pragma unroll
-        for (int c = 0; c < MAXCH; ++c) {
+        for (int c = 0; c < MC; ++c) {
             const int ch = threadIdx.x + c * RT;
             if (ch >= nch) continue;
             u32x2_t o;
@@ -160,6 +161,7 @@ __global__ __launch_bounds__(RT) void ln_modulate_kernel(
 // (VS_EPI_GATE_RES: x = bf16(x + bf16(gate*y)) [+ bf16(hint*s)]; VS_EPI_RES: x = bf16(x + bf16(alpha*y)))
 // followed by ln_modulate_kernel's arithmetic on the stored bf16 row -- the same rounding points as
 // the two separate passes, one read of x instead of two (wan_video_dit.py:225-228).
+template <int MC = MAXCH>
 __global__ __launch_bounds__(RT) void residual_ln_kernel(
     const bf16_t* __restrict__ y, long long ldy, bf16_t* __restrict__ x, long long ldx, bf16_t* __restrict__ out,
     long long ldo, int dim, int mode, const bf16_t* __restrict__ gate, long long gate_bstride, int rpb_gate,
@@ -172,10 +174,10 @@ __global__ __launch_bounds__(RT) void residual_ln_kernel(
     const bf16_t* yr = y + row * ldy;
     bf16_t* xr = x + row * ldx;
     const bf16_t* gr = gate ? gate + (row / rpb_gate) * gate_bstride : nullptr;
-    float v[MAXCH][8];
+    float v[MC][8];
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < MAXCH; ++c) {
+    for (int c = 0; c < MC; ++c) {
         const int ch = threadIdx.x + c * RT;
         if (ch < nch) {
             float yv[8], xv[8];
@@ -206,7 +208,7 @@ __global__ __launch_bounds__(RT) void residual_ln_kernel(
     const float mean = block_sum(s, red) / dim;
     float q = 0.f;
 #pragma unroll
-    for (int c = 0; c < MAXCH; ++c) {
+    for (int c = 0; c < MC; ++c) {
         const int ch = threadIdx.x + c * RT;
         if (ch < nch) {
 #pragma unroll
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(RT) void residual_ln_kernel(
     const long long bidx = row / rpb;
     bf16_t* orow = out + row * ldo;
 #pragma unroll
-    for (int c = 0; c < MAXCH; ++c) {
+    for (int c = 0; c < MC; ++c) {
         const int ch = threadIdx.x + c * RT;
         if (ch >= nch) continue;
         float o8[8];
@@ -271,7 +273,7 @@ __device__ __forceinline__ void block_sum_n(float* v, float* red) {
 // Measured at the 14B shape on q|k|v slices (tests/probes/rownorm_ab.py, profiles/r1/rownorm_ab_r1s.log):
 // NR = 1 262 us, 2 270 us, 4 331 us -- more rows per block cost occupancy, not latency.  The
 // LDS-gathered RoPE pairs took NR = 1 from 294 us (4 global 8-B gathers per 16-B chunk) to 262 us.
-template <int NR>
+template <int NR, int MC = MAXCH>
 __global__ __launch_bounds__(RT) void rmsnorm_rope_kernel(
     bf16_t* __restrict__ x, long long ldx, int rows, int dim, int hd, const bf16_t* __restrict__ w, float eps,
     const float2* __restrict__ rope, int gf, int gh, int gw, int rpb, int tok_off) {
@@ -295,7 +297,7 @@ __global__ __launch_bounds__(RT) void rmsnorm_rope_kernel(
             rc[i][j] = rope[(long long)pos * half + j];
         }
     }
-    float v[NR][MAXCH][8];
+    float v[NR][MC][8];
     float s[NR];
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
@@ -303,7 +305,7 @@ __global__ __launch_bounds__(RT) void rmsnorm_rope_kernel(
         if (i >= nr) continue;
         const bf16_t* xr = x + (row0 + i) * ldx;
 #pragma unroll
-        for (int c = 0; c < MAXCH; ++c) {
+        for (int c = 0; c < MC; ++c) {
             const int ch = threadIdx.x + c * RT;
             if (ch < nch) unpack8(*reinterpret_cast<const u32x4_t*>(xr + ch * 8), v[i][c]);
         }
@@ -311,7 +313,7 @@ __global__ __launch_bounds__(RT) void rmsnorm_rope_kernel(
 #pragma unroll
     for (int i = 0; i < NR; ++i)
 #pragma unroll
-        for (int c = 0; c < MAXCH; ++c) {
+        for (int c = 0; c < MC; ++c) {
             const int ch = threadIdx.x + c * RT;
             if (i < nr && ch < nch)
 #pragma unroll
@@ -319,7 +321,7 @@ __global__ __launch_bounds__(RT) void rmsnorm_rope_kernel(
         }
     block_sum_n<NR>(s, red);
 #pragma unroll
-    for (int c = 0; c < MAXCH; ++c) {
+    for (int c = 0; c < MC; ++c) {
         const int ch = threadIdx.x + c * RT;
         if (ch >= nch) continue;
         float wv[8];
@@ -523,6 +525,11 @@ __global__ void ulysses_permute_kernel(const bf16_t* __restrict__ src, bf16_t* _
 }
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+// rows up to RT * MAXCH * 8 = 5120 (every Wan width) on the measured 5-chunk instantiation; wider
+// rows, up to RT * MCW * 8 = 8192, on an 8-chunk one (r1-r4 accepted up to 6144)
+constexpr int MCW = 8;
+constexpr int ROW_MAX = RT * MCW * 8;
+bool narrow(int dim) { return dim <= RT * MAXCH * 8; }
 unsigned nblk(long long n, int t) { return (unsigned)((n + t - 1) / t); }
 
 }  // namespace
@@ -531,14 +538,15 @@ extern "C" int vs_layernorm_modulate(const void* x, long long ldx, void* out, lo
                                      int rows, int dim, int rows_per_batch, const void* shift,
                                      const void* scale, long long mod_bstride, const void* weight,
                                      const void* bias, float eps, void* stream) {
-    if (!x || !out || rows <= 0 || dim <= 0 || dim % 8 || dim > MAXCH * RT * 8) return VS_E_INVALID;
+    if (!x || !out || rows <= 0 || dim <= 0 || dim % 8 || dim > ROW_MAX) return VS_E_INVALID;
     if (ldx < dim || ldo < dim || (ldx & 7) || (ldo & 7) || !al16(x) || !al16(out)) return VS_E_INVALID;
     if ((shift == nullptr) != (scale == nullptr)) return VS_E_INVALID;
     if ((weight == nullptr) != (bias == nullptr)) return VS_E_INVALID;
     if (shift && (!al16(shift) || !al16(scale) || (mod_bstride & 7))) return VS_E_INVALID;
     if (weight && (!al16(weight) || !al16(bias))) return VS_E_INVALID;
     if (rows_per_batch <= 0) rows_per_batch = rows;
-    hipLaunchKernelGGL(ln_modulate_kernel<false>, dim3(rows), dim3(RT), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL((narrow(dim) ? ln_modulate_kernel<false> : ln_modulate_kernel<false, MCW>), dim3(rows), dim3(RT), 0,
+                       (hipStream_t)stream,
                        (const bf16_t*)x, ldx, (bf16_t*)out, ldo, dim, rows_per_batch,
                        (const bf16_t*)shift, (const bf16_t*)scale, mod_bstride,
                        (const bf16_t*)weight, (const bf16_t*)bias, eps, nullptr, 0LL, nullptr);
@@ -550,7 +558,7 @@ extern "C" int vs_layernorm_modulate_fp8(const void* x, long long ldx, void* x8,
                                          int rows, int dim, int rows_per_batch, const void* shift,
                                          const void* scale, long long mod_bstride, const void* weight,
                                          const void* bias, float eps, void* stream) {
-    if (!x || !x8 || !qscale || rows <= 0 || dim <= 0 || dim % 8 || dim > MAXCH * RT * 8) return VS_E_INVALID;
+    if (!x || !x8 || !qscale || rows <= 0 || dim <= 0 || dim % 8 || dim > ROW_MAX) return VS_E_INVALID;
     if (ldx < dim || ld8 < dim || (ldx & 7) || (ld8 & 7) || !al16(x) || (reinterpret_cast<uintptr_t>(x8) & 7))
         return VS_E_INVALID;
     if ((shift == nullptr) != (scale == nullptr)) return VS_E_INVALID;
@@ -558,7 +566,8 @@ extern "C" int vs_layernorm_modulate_fp8(const void* x, long long ldx, void* x8,
     if (shift && (!al16(shift) || !al16(scale) || (mod_bstride & 7))) return VS_E_INVALID;
     if (weight && (!al16(weight) || !al16(bias))) return VS_E_INVALID;
     if (rows_per_batch <= 0) rows_per_batch = rows;
-    hipLaunchKernelGGL(ln_modulate_kernel<true>, dim3(rows), dim3(RT), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL((narrow(dim) ? ln_modulate_kernel<true> : ln_modulate_kernel<true, MCW>), dim3(rows), dim3(RT), 0,
+                       (hipStream_t)stream,
                        (const bf16_t*)x, ldx, nullptr, 0LL, dim, rows_per_batch,
                        (const bf16_t*)shift, (const bf16_t*)scale, mod_bstride,
                        (const bf16_t*)weight, (const bf16_t*)bias, eps, (uint8_t*)x8, ld8, qscale);
@@ -570,7 +579,7 @@ extern "C" int vs_residual_layernorm(const void* y, long long ldy, void* x, long
                                      int rows, int dim, int epilogue, const vs_epilogue* epi, int rows_per_batch,
                                      const void* shift, const void* scale, long long mod_bstride,
                                      const void* weight, const void* bias, float eps, void* stream) {
-    if (!y || !x || !out || !epi || rows <= 0 || dim <= 0 || dim % 8 || dim > MAXCH * RT * 8) return VS_E_INVALID;
+    if (!y || !x || !out || !epi || rows <= 0 || dim <= 0 || dim % 8 || dim > ROW_MAX) return VS_E_INVALID;
     if (epilogue != VS_EPI_GATE_RES && epilogue != VS_EPI_RES) return VS_E_INVALID;
     if (ldy < dim || ldx < dim || ldo < dim || ((ldy | ldx | ldo) & 7) || !al16(y) || !al16(x) || !al16(out))
         return VS_E_INVALID;
@@ -584,7 +593,8 @@ extern "C" int vs_residual_layernorm(const void* y, long long ldy, void* x, long
     const int rpb_gate = epi->rows_per_batch > 0 ? epi->rows_per_batch : rows;
     if (rows_per_batch <= 0) rows_per_batch = rows;
     const bool gated = epilogue == VS_EPI_GATE_RES;
-    hipLaunchKernelGGL(residual_ln_kernel, dim3(rows), dim3(RT), 0, (hipStream_t)stream, (const bf16_t*)y, ldy,
+    hipLaunchKernelGGL((narrow(dim) ? residual_ln_kernel<> : residual_ln_kernel<MCW>), dim3(rows), dim3(RT), 0,
+                       (hipStream_t)stream, (const bf16_t*)y, ldy,
                        (bf16_t*)x, ldx, (bf16_t*)out, ldo, dim, epilogue,
                        gated ? (const bf16_t*)epi->gate : nullptr, epi->gate_bstride, rpb_gate, epi->alpha,
                        gated ? (const bf16_t*)epi->hint : nullptr, epi->ld_hint, epi->hint_scale, rows_per_batch,
@@ -598,7 +608,7 @@ extern "C" int vs_rmsnorm_rope(void* x, long long ldx, int rows, int dim, int he
                                const void* weight, float eps, const void* rope, int rope_len,
                                int gf, int gh, int gw, int rows_per_batch, int token_offset,
                                void* stream) {
-    if (!x || !weight || rows <= 0 || dim <= 0 || dim % 8 || dim > MAXCH * RT * 8) return VS_E_INVALID;
+    if (!x || !weight || rows <= 0 || dim <= 0 || dim % 8 || dim > ROW_MAX) return VS_E_INVALID;
     if (ldx < dim || (ldx & 7) || !al16(x) || !al16(weight)) return VS_E_INVALID;
     if (rope) {
         if (head_dim != 128 || dim % head_dim) return VS_E_UNSUPPORTED;
@@ -613,7 +623,8 @@ extern "C" int vs_rmsnorm_rope(void* x, long long ldx, int rows, int dim, int he
 #define VS_RMS_ROWS 1
 #endif
     constexpr int NR = VS_RMS_ROWS;
-    hipLaunchKernelGGL(rmsnorm_rope_kernel<NR>, dim3((unsigned)((rows + NR - 1) / NR)), dim3(RT), 0,
+    hipLaunchKernelGGL((narrow(dim) ? rmsnorm_rope_kernel<NR> : rmsnorm_rope_kernel<NR, MCW>),
+                       dim3((unsigned)((rows + NR - 1) / NR)), dim3(RT), 0,
                        (hipStream_t)stream, (bf16_t*)x, ldx, rows, dim, head_dim, (const bf16_t*)weight, eps,
                        (const float2*)rope, gf, gh, gw, rows_per_batch, token_offset);
     VS_CHECK_LAUNCH();
