@@ -57,7 +57,7 @@ def test_invalid_arguments_rejected_before_launch():
     assert lib.vs_attn_fwd(fake, fake, fake, fake, 1, 16, 16, 1, 64, 64, 64, 64, 64, 0, 0, 0, 0, 1.0, None) == 3
     assert lib.vs_attn_fwd(fake, fake, fake, fake, 1, 16, 16, 1, 128, 130, 128, 128, 128, 0, 0, 0, 0, 1.0, None) == 1
     # rmsnorm dim too large / not multiple of 8
-    assert lib.vs_rmsnorm_rope(fake, 8000, 4, 8000, 128, fake, 1e-6, None, 0, 1, 1, 1, 0, 0, None) == 1
+    assert lib.vs_rmsnorm_rope(fake, 8200, 4, 8200, 128, fake, 1e-6, None, 0, 1, 1, 1, 0, 0, None) == 1
     assert lib.vs_layernorm_modulate(fake, 12, fake, 12, 4, 12, 0, None, None, 0, None, None, 1e-6, None) == 1
     # RoPE token range beyond the grid
     assert lib.vs_rmsnorm_rope(fake, 256, 4, 256, 128, fake, 1e-6, fake, 1024, 1, 1, 2, 4, 0, None) == 1
