@@ -265,6 +265,14 @@ def launch_ranks(n, argv, script=None, gpus=None, env=None, timeout=None):
     base = dict(os.environ if env is None else env)
     procs = [subprocess.Popen([sys.executable, script] + list(argv), env=rank_env(base, r, n, port))
              for r in range(n)]
+
+    def stop_children(signum, frame):       # a launcher killed from outside takes its ranks with it
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        sys.exit(128 + signum)
+    import signal
+    old_handlers = {sig: signal.signal(sig, stop_children) for sig in (signal.SIGTERM, signal.SIGINT)}
     rcs = [None] * n
     first_bad = None
     t0 = time.time()
@@ -286,10 +294,14 @@ def launch_ranks(n, argv, script=None, gpus=None, env=None, timeout=None):
                     p.kill()
                     rcs[r] = p.wait()
             if first_bad is None:
+                for sig, h in old_handlers.items():
+                    signal.signal(sig, h)
                 print(f"[bench] ranks still running after {timeout} s: terminated", file=sys.stderr, flush=True)
                 return 124
             break
         time.sleep(0.2)
+    for sig, h in old_handlers.items():
+        signal.signal(sig, h)
     # the first child to fail is the cause (the ranks terminated after it report SIGTERM)
     return first_bad if first_bad is not None else 0
 

@@ -81,3 +81,25 @@ def test_bench_cli_fails_fast_without_gpus():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
     assert "disagree" in r.stderr
+
+
+def test_launcher_sigterm_ends_the_ranks(tmp_path):
+    """A launcher terminated from outside (a driver's time limit) terminates its ranks too."""
+    import signal
+    stub = _stub(tmp_path)
+    code = ("import sys; sys.path.insert(0, %r); import bench; "
+            "sys.exit(bench.launch_ranks(2, [], script=%r, gpus=2))" % (ROOT, stub))
+    env = dict(os.environ, STUB_DIR=str(tmp_path), STUB_FAIL_RANK="7", STUB_FAIL_RC="1")   # no rank fails: all sleep
+    p = subprocess.Popen([sys.executable, "-c", code], env=env)
+    for _ in range(300):
+        if len(list(tmp_path.glob("rank*.json"))) == 2:
+            break
+        time.sleep(0.1)
+    recs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(60) == 128 + signal.SIGTERM
+    time.sleep(1)
+    import psutil
+    alive = [c for c in psutil.process_iter(["cmdline"]) if c.info["cmdline"] and stub in " ".join(c.info["cmdline"])]
+    assert not alive, alive
+    assert len(recs) == 2
