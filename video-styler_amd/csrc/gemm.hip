@@ -2132,6 +2132,10 @@ extern "C" int vs_gemm(const void* a, long long lda, const void* w, long long ld
                 attr4 = true;
             }
             const K4 kf = kern4[(ep.mode == VS_EPI_GATE_RES && ep.hint) ? 5 : ep.mode];
+            // raster groups of 2 M-tiles for the deep-K FFN-down (K 13 824: 5.47-5.48 vs 5.54-5.57 ms at
+            // 59 280 rows), 4 elsewhere (q|k|v / FFN-up 1-1.5 % slower at 2, 5-15 % at 8-16;
+            // profiles/r6/gemm_gm_s10.log).  The split combine below reads the same ep.gm
+            if (k >= 8192) ep.gm = 2;
             const W4Sched sc = w4_sched(sp.nmain, k / 64, (hipStream_t)stream,
                                         vs_opt(VS_OPT_PIECE_QUEUE) ? sp.ntail * sp.ksplit : 0);
             hipLaunchKernelGGL(kf, dim3(w4_grid(sc, sp)), dim3(256), W4_LDS + 16,
