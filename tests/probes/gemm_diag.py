@@ -7,8 +7,12 @@ import torch
 from vstyler import kernels as K
 
 M = int(os.environ.get("GD_M", "59280"))
-for name, N, Kd, epi in (("qkv", 15360, 5120, K.VS_EPI_BIAS), ("ffn-up", 13824, 5120, K.VS_EPI_GELU),
-                         ("ffn-down", 5120, 13824, K.VS_EPI_BIAS)):
+SHAPES = (("qkv", 15360, 5120, K.VS_EPI_BIAS), ("ffn-up", 13824, 5120, K.VS_EPI_GELU),
+          ("ffn-down", 5120, 13824, K.VS_EPI_BIAS), ("o-proj", 5120, 5120, K.VS_EPI_BIAS))
+only = os.environ.get("GD_SHAPES")
+for name, N, Kd, epi in SHAPES:
+    if only and name not in only.split(","):
+        continue
     g = torch.Generator(device="cuda").manual_seed(1)
     a = torch.randn(M, Kd, device="cuda", generator=g).to(torch.bfloat16)
     w = (0.05 * torch.randn(N, Kd, device="cuda", generator=g)).to(torch.bfloat16)
