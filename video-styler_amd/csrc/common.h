@@ -123,8 +123,8 @@ inline int vs_cus_for_split(bool off) {
 
 // Split-tail scratch is caller-owned (the library never allocates): the host binds one fp32
 // workspace per (kind, device, stream) with vs_split_workspace_bind; a launch on a stream without
-// one runs unsplit.  kind 0: attention split tail, 1: GEMM split tail, 2: hipBLASLt workspace,
-// 3: bf16 staging for epilogues finished after a hipBLASLt GEMM (gate-residual / residual),
+// one runs unsplit.  kind 0: attention split tail, 1: GEMM split tail, 2 / 3: unused (r1-r5's
+// vendor-library workspace and epilogue staging),
 // 4: attention item flags, 5: the 4-wave GEMMs' tile-queue words (4 and 5 bound zero-filled; the
 // kernels leave them zero).
 struct VsWs { float* ptr; long long bytes; };
