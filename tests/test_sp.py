@@ -216,55 +216,69 @@ def test_ulysses_model_on_one_gpu_vs_sp1_and_oracle(world, cfg_name):
     assert res[0][1].get("denoise_oracle", True) is True, res[0][1]["denoise_msg"]
 
 
-def _gpu14b_worker(rank, world, port, q):
-    """The 14B-dim DiT + VACE block pair (D 5120, 40 heads: 5 per rank at SP = 8) at 832x480x73 under
-    Ulysses SP = world with host-staged collectives on one GPU: bit-identical to the unsharded forward;
-    rank 0 also checks the velocity at sampled token rows against the oracle's model_fn_rows
-    (fp32 / fp64 floor, as the C4 test)."""
+SIZES = {"480p": (73, 480, 832), "720p": (121, 720, 1280)}
+
+
+def _gpu14b_worker(rank, world, port, q, size="480p"):
+    """The 14B-dim DiT + VACE block pair (D 5120, 40 heads: 5 per rank at SP = 8) at 832x480x73 (or
+    C4's 1280x720x121) under Ulysses SP = world with host-staged collectives on one GPU.  Rank 0 runs the
+    unsharded forward too (one 14B-dim activation set on the card) and checks: bit-identity with split
+    tails off, with the CFG shared prefix (one micro-batch in both first blocks) and without it (the
+    per-sample micro-batch overlap at the 14B dims); with the product defaults, the velocity at sampled
+    token rows against the oracle's model_fn_rows (fp32 / fp64 floor, as the C4 test)."""
     try:
         _init(rank, world, port)
         from oracle import wan_oracle as O
         from sp_util import HostStagedUlysses
         from vstyler import model_fn_wan_video
+        from vstyler import kernels as K
+        from vstyler.options import host_options
+        from gpu_util import err
         from test_production_model_gpu import build, floor_check, gpu_weights, oracle_both
+        frames, height, width = SIZES[size]
         cfg = dict(O.WAN_CONFIGS["14B"], num_layers=1, vace_layers=(0,))
         W = gpu_weights(cfg, seed=29)
         dit, vace = build(cfg, W)
-        lat, cp, cn, vc = O.synthetic_inputs(cfg, 73, 480, 832)
+        lat, cp, cn, vc = O.synthetic_inputs(cfg, frames, height, width)
         lat, ctx, vc = lat.cuda(), torch.cat([cp, cn]).cuda(), vc.cuda()
         t = torch.tensor([812.5], device="cuda").to(torch.bfloat16)
-        from vstyler import kernels as K
-        from gpu_util import err
 
-        def both():
-            single = model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=ctx, vace_context=vc)
-            sp = HostStagedUlysses()
-            par = model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=ctx, vace_context=vc,
-                                     use_unified_sequence_parallel=True, sp_group=sp)
+        def fwd(sp=None):
+            out = model_fn_wan_video(dit, vace=vace, latents=lat, timestep=t, context=ctx, vace_context=vc,
+                                     use_unified_sequence_parallel=sp is not None, sp_group=sp)
             torch.cuda.synchronize()
-            return single, par, sp.collective_calls
+            return out
+        res = {}
         # without split tails every GEMM tile and attention item is computed whole at any row count,
         # so the sharded forward must equal the unsharded one bit for bit
-        with K.options(gemm_split=0, attn_split=0):
-            single, par, calls = both()
-        res = {"same": torch.equal(single, par), "calls": calls}
+        for prefix in (1, 0):
+            with K.options(gemm_split=0, attn_split=0), host_options(cfg_prefix=prefix):
+                single = fwd() if rank == 0 else None
+                sp = HostStagedUlysses()
+                par = fwd(sp)
+            res[f"calls{prefix}"] = sp.collective_calls
+            if rank == 0:
+                res[f"same{prefix}"] = torch.equal(single, par)
         # with them (the product default) SP changes which tiles / items are split into K pieces (the
         # split-tail plan follows the GEMM's row count and the attention's item count), i.e. the fp32
         # summation order of those tiles: rounding-level differences, the oracle decides
-        single, par, calls = both()
-        res["default_err"] = err(par, single)
-        del single
+        single = fwd() if rank == 0 else None
+        par = fwd(HostStagedUlysses())
         if rank == 0:
-            S = 19 * 30 * 52
+            res["default_err"] = err(par, single)
+            del single
+            T, Hl, Wl = (frames - 1) // 4 + 1, height // 16, width // 16
+            S = T * Hl * Wl
+            fr = Hl * Wl
             g = torch.Generator().manual_seed(321)
             rows = torch.cat([torch.randperm(S, generator=g)[:250],
-                              torch.tensor([0, 1, 1559, 1560, S // world - 1, S // world, S - 2, S - 1])])
+                              torch.tensor([0, 1, fr - 1, fr, S // world - 1, S // world, S - 2, S - 1])])
             rows = rows.unique().cuda()
             ref32, ref64 = oracle_both(lambda: O.model_fn_rows(W, cfg, torch.cat([lat, lat]), t.expand(2), ctx,
                                                                torch.cat([vc, vc]), rows))
             try:
                 floor_check(O.patchify_output(par)[:, rows], ref32, ref64,
-                            f"14B 1+1 blocks 832x480x73 Ulysses SP={world}, {len(rows)} token rows")
+                            f"14B 1+1 blocks {width}x{height}x{frames} Ulysses SP={world}, {len(rows)} token rows")
                 res["oracle"] = True
             except AssertionError as e:
                 res["oracle"] = repr(e)
@@ -274,22 +288,35 @@ def _gpu14b_worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.gpu
-def test_ulysses_14b_block_pair_sp8_on_one_gpu():
-    """Ulysses SP = 8 at the 14B model's own dims (40 heads -> 5 per rank, S = 29 640 -> 3705 tokens per
-    rank, the packed q|k|v rows path under the overlap schedule) through the product orchestration with
-    host-staged collectives: bit-identical to the single-GPU forward with split tails off, and with
-    the product's split tails (whose plans follow the per-rank sizes) within the oracle's floor."""
-    res = _spawn(_gpu14b_worker, 8, timeout=900)
+def _check_14b(res):
     assert len(res) == 8
     for rank, r in res:
         assert isinstance(r, dict), (rank, r)
-        assert r["same"] is True, (rank, r)
-        # 2 blocks x (out, back) + gather: both are first blocks (DiT 0, VACE 0), whose self-attention
-        # runs once for both CFG samples (shared prefix; 2 micro-batches each without it)
-        assert r["calls"] == 2 * 2 + 1, (rank, r)
-    print("SP=8 vs unsharded with split tails (max-abs, rel-L2):", res[0][1]["default_err"])
-    assert res[0][1]["oracle"] is True, res[0][1]
+        # 2 blocks x (out, back) + gather: with the shared prefix both first blocks (DiT 0, VACE 0) run
+        # their self-attention once for both CFG samples; without it, per sample (the overlap schedule)
+        assert r["calls1"] == 2 * 2 + 1 and r["calls0"] == 2 * 2 * 2 + 1, (rank, r)
+    r0 = res[0][1]
+    assert r0["same1"] is True and r0["same0"] is True, r0
+    print("SP=8 vs unsharded with split tails (max-abs, rel-L2):", r0["default_err"])
+    assert r0["oracle"] is True, r0
+
+
+@pytest.mark.gpu
+def test_ulysses_14b_block_pair_sp8_on_one_gpu():
+    """Ulysses SP = 8 at the 14B model's own dims (40 heads -> 5 per rank, S = 29 640 -> 3705 tokens per
+    rank, the packed q|k|v rows path, with and without the per-sample overlap) through the product
+    orchestration with host-staged collectives: bit-identical to the single-GPU forward with split
+    tails off, and with the product's split tails (whose plans follow the per-rank sizes) within the
+    oracle's floor."""
+    _check_14b(_spawn(_gpu14b_worker, 8, "480p", timeout=900))
+
+
+@pytest.mark.gpu
+def test_ulysses_c4_block_pair_sp8_on_one_gpu():
+    """The same at BASELINE C4's 1280x720x121 (S = 111 600 -> 13 950 tokens per rank): the SP = 8 layout
+    of C4 through the product orchestration (host-staged: ~3 GB through gloo per exchange; 16 s on an
+    MI355X box, profiles/r6/pytest_sp8_c4_block_pair.log)."""
+    _check_14b(_spawn(_gpu14b_worker, 8, "720p", timeout=1500))
 
 
 def _rccl_worker(port, q, graph=False):
