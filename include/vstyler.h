@@ -347,6 +347,15 @@ int vs_vae_rmsnorm(const void* x, long long ldx, void* y, long long ldy, const v
 int vs_vae_softmax(const float* s, long long ld_s, void* p, long long ld_p, long long rows, int ncols,
                    void* stream);
 
+/* Flash form of the same attention (csrc/vae_attention.hip): for each of nz frames z,
+ * out[z][r][:c] = softmax(q k^T / sqrt(c)) v over `rows` pixels, with q | k | v the columns [0, c) |
+ * [c, 2c) | [2c, 3c) of qkv[z][r] (the to_qkv output, row stride ld_qkv, frame stride qkv_zs); the
+ * softmax exact (two passes over K), rounded to bf16 before P.V as vs_vae_softmax; no score
+ * buffer.  c % 128 == 0, c <= 384; ld_qkv % 8 == 0, qkv 16-B aligned, ld_o % 4 == 0.
+ * Replaces AttentionBlock's F.scaled_dot_product_attention (wan_video_vae.py:330-335). */
+int vs_vae_attention(const void* qkv, long long qkv_zs, long long ld_qkv, void* out, long long o_zs,
+                     long long ld_o, int nz, int rows, int c, void* stream);
+
 /* vt[z][c][r] = v[z][r][c] for r < rows, 0 for rows <= r < ld_vt (V^T operand of P.V). */
 int vs_vae_transpose(const void* v, long long v_zs, long long ld_v, void* vt, long long vt_zs,
                      long long ld_vt, int nz, int rows, int cols, void* stream);

@@ -61,6 +61,12 @@ def test_invalid_arguments_rejected_before_launch():
     assert lib.vs_layernorm_modulate(fake, 12, fake, 12, 4, 12, 0, None, None, 0, None, None, 1e-6, None) == 1
     # RoPE token range beyond the grid
     assert lib.vs_rmsnorm_rope(fake, 256, 4, 256, 128, fake, 1e-6, fake, 1024, 1, 1, 2, 4, 0, None) == 1
+    # VAE flash attention: c a multiple of 128 up to 384, qkv rows >= 3c, 16-B aligned qkv
+    assert lib.vs_vae_attention(fake, 64 * 576, 576, fake, 64 * 192, 192, 1, 64, 192, None) == 1
+    assert lib.vs_vae_attention(fake, 64 * 1536, 1536, fake, 64 * 512, 512, 1, 64, 512, None) == 1
+    assert lib.vs_vae_attention(fake, 64 * 300, 300, fake, 64 * 128, 128, 1, 64, 128, None) == 1
+    assert lib.vs_vae_attention(fake + 8, 64 * 384, 384, fake, 64 * 128, 128, 1, 64, 128, None) == 1
+    assert lib.vs_vae_attention(fake, 63 * 384, 384, fake, 64 * 128, 128, 1, 64, 128, None) == 1
     # Ulysses permute: columns not a multiple of 8
     assert lib.vs_ulysses_permute(fake, fake, 1, 4, 2, 12, 24, 48, 0, None) == 1
     # SP collectives: argument checks come before RCCL is opened or a device is touched

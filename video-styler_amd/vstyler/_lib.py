@@ -92,6 +92,7 @@ SIGNATURES = {
     "vs_vae_rmsnorm": [_P, _LL, _P, _LL, _P, _LL, _I, _I, _P],
     "vs_vae_softmax": [_P, _LL, _P, _LL, _LL, _I, _P],
     "vs_vae_transpose": [_P, _LL, _LL, _P, _LL, _LL, _I, _I, _I, _P],
+    "vs_vae_attention": [_P, _LL, _LL, _P, _LL, _LL, _I, _I, _I, _P],
     "vs_vae_tile_gather": [_P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P, _P],
     "vs_vae_to_u8": [_P, _P, _I, _I, _I, _P],
     "vs_unipc_update": [_P, _P, _P, _P, _P, _LL, _I, ctypes.POINTER(ctypes.c_float), _P],

@@ -283,15 +283,25 @@ class WanVideoVAE:
         rmsnorm(a, self.params[p + "residual.3.gamma"], silu=True, out=a)
         return self._conv3(a, p + "residual.6.", res=h)
 
-    def _attn_block(self, x, p):
-        """AttentionBlock (:304-342): per frame single-head attention over h*w tokens, d = C."""
+    def _attn_block(self, x, p, flash=None):
+        """AttentionBlock (:304-342): per frame single-head attention over h*w tokens, d = C.  The
+        flash kernel (vs_vae_attention) for C % 128 == 0 (Wan2.1: 384; flash=False selects the GEMM
+        route for A/Bs), else fp32 scores + softmax + P.V through the conv kernel's GEMM mode."""
         n, t, h, w, c = x.shape
         hw, nz = h * w, n * t
-        hwp = _r32(hw)
         xn = rmsnorm(x, self.params[p + "norm.gamma"], silu=False)
         qkv = self._conv1(xn, p + "to_qkv.")                      # [n, t, h, w, 3c]
         del xn
         o = torch.empty((n, t, h, w, c), dtype=BF16, device=x.device)
+        if flash is None:
+            flash = c % 128 == 0 and c <= 384
+        if flash:
+            _lib.check(_lib.load().vs_vae_attention(qkv.data_ptr(), hw * 3 * c, 3 * c, o.data_ptr(), hw * c, c, nz,
+                                                    hw, c, _stream(x)))
+            FLOPS[0] += 4 * nz * hw * hw * c
+            del qkv
+            return conv(o, self.cw[p + "proj."], (t, h, w), res=x)
+        hwp = _r32(hw)
         zc = max(1, min(nz, self.attn_bytes // (hw * hwp * 4)))
         s = torch.empty((zc, hw, hwp), dtype=torch.float32, device=x.device)
         pm = torch.empty((zc, hw, hwp), dtype=BF16, device=x.device)
