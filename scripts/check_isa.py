@@ -12,6 +12,8 @@ And the tile-queue atomic (W4Grab::issue) must be a single returning global atom
 (the compiler's atomic optimizer off for gemm.o: Makefile), whose destination VGPR nothing touches
 between the atomic and the `s_waitcnt vmcnt` + `v_readfirstlane` that consume it (queue_value_hazards;
 also checked in the attention kernels, which take their items from the same kind of queue).
+The VAE flash attention (vae_attn_kernel, three widths) must compile without scratch: its 192
+accumulator registers per lane at C = 384 fit only while the compiler keeps them in AGPRs.
 
 usage: check_isa.py <gemm.o | libvstyler.so>   (exit 1 with the offending kernels listed)"""
 import os
@@ -190,11 +192,20 @@ def main():
             n, issues = queue_value_hazards(body)
             nq += n
             bad += [f"{name}: {msg}" for msg in issues]
+    nv = 0
+    for name, body in ks.items():            # the VAE flash attention: accumulators stay in AGPRs, no spill
+        if "vae_attn_kernel" in name:
+            nv += 1
+            if scratch.get(name, 0):
+                bad.append(f"{name}: {scratch[name]} B of scratch")
+    if nv != 3:
+        bad.append(f"{nv} vae_attn_kernel instances found (expected 3: C = 128, 256, 384)")
     if bad:
         print("check_isa: FAILED\n  " + "\n  ".join(bad))
         sys.exit(1)
     print(f"check_isa: {checked} gemm_*_4w kernels OK (no accumulator AGPR copies, 512 acc_rd reads, no scratch, "
-          f"queue atomics consumed only behind their vmcnt wait; {nq} in the attention kernels)")
+          f"queue atomics consumed only behind their vmcnt wait; {nq} in the attention kernels; "
+          f"{nv} VAE attention kernels without scratch)")
 
 
 if __name__ == "__main__":
