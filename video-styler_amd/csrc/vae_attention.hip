@@ -27,6 +27,8 @@
 // Keys >= rows read the last row (in range) and are masked to -inf; query rows >= rows are not stored.
 #include "common.h"
 
+#include <mutex>
+
 namespace {
 
 constexpr int FA_THR = 256, FA_BQ = 128, FA_BK = 32;
@@ -241,11 +243,10 @@ int launch_vae_attn(const void* qkv, long long qkv_zs, long long ld, void* out, 
                     int nz, int rows, hipStream_t st) {
     using G = FaGeom<NCB>;
     auto kern = vae_attn_kernel<NCB>;
-    static bool attr = false;
-    if (!attr) {
+    static std::once_flag attr;      // (per instantiation; the launch path may run on several host threads)
+    std::call_once(attr, [&] {
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
-        attr = true;
-    }
+    });
     const float sc = 1.4426950408889634f / sqrtf((float)G::C);
     dim3 grid((unsigned)((rows + FA_BQ - 1) / FA_BQ), (unsigned)nz);
     hipLaunchKernelGGL(kern, grid, dim3(FA_THR), G::LDS, st, (const bf16_t*)qkv, qkv_zs, ld, (bf16_t*)out, o_zs,
